@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""Benchmark of the spectral MCM photon march (BASELINE.json metric).
+
+One "step" = one progressive pass of the hot path: R^2 photons x S photon-steps
+(MCMSpectralComputeRenderer.wgsl:123-164), plus — at N > 1 — the RCCL all-reduce
+of the (rgb*n, n) radiance buffer that composites the photon-parallel replicas.
+
+Workload (BASELINE.md C3 at N = 1, C4 at N = 8): 512^3 fBm volume (seed 512),
+spectral TF with HG g = 0.702, R = 512, S = 8, 12 bins, extinction 32, default
+camera. Inputs are resident in HBM before the timed region.
+
+Launch: `python bench.py --gpus N --steps K --warmup W` (N = 1), or under
+`python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`:
+one process per GPU (LOCAL_RANK), RCCL bootstrapped torch-free (rendezvous.py).
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+PKG = REPO / "vpt-spectral-volume-rendering_amd"
+sys.path[:0] = [str(PKG / "python")]
+
+import numpy as np  # noqa: E402
+
+import vptmcm  # noqa: E402
+from vptmcm import configs as cf  # noqa: E402
+from vptmcm import rendezvous  # noqa: E402
+
+METRIC = "Mphoton-steps/sec (+ achieved HBM GB/s), 512³ spectral MCM, 1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200, help="timed passes")
+    ap.add_argument("--warmup", type=int, default=20, help="untimed passes")
+    ap.add_argument("--resolution", type=int, default=512)
+    ap.add_argument("--volume", type=int, default=512)
+    ap.add_argument("--photon-steps", type=int, default=8, help="S: steps per pass")
+    ap.add_argument("--extinction", type=float, default=32.0)
+    ap.add_argument("--layout", choices=["corner8", "linear"], default="corner8")
+    ap.add_argument("--allreduce-every", type=int, default=1,
+                    help="passes between radiance all-reduces (N > 1)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="budget of the CPU-oracle baseline (0 = skip)")
+    ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "pmc_traffic.json"),
+                    help="PMC-derived HBM bytes per launch (profiles/), if present")
+    return ap.parse_args()
+
+
+def cpu_baseline(vol, tf, spec, spd, ldir, mvp, R, S, ext, budget_s):
+    """The C oracle (the 'port') on this host's cores: full R^2 frames, S steps,
+    passes until the time budget is spent."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle as orc  # test-infrastructure checker, timed here as the CPU baseline
+
+    threads = cf.host_threads()
+    o = orc.Oracle(R)
+    o.set_spectrum(spec)
+    o.volume, o.tf, o.light, o.light_dir = vol, tf, spd, ldir
+    o.params.update(extinction=ext, bounces=8, steps=S)
+    o.reset(mvp, cf.seed_bits(0), nthreads=threads)
+    o.render(mvp, cf.seed_bits(1), nthreads=threads)  # warm-up pass
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        o.render(mvp, cf.seed_bits(2 + passes), nthreads=threads)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": round(R * R * S * passes / el / 1e6, 3), "unit": "Mphoton-steps/s",
+            "cores": threads, "kind": "port",
+            "sample": f"C oracle (oracle/mcm_oracle.c), {passes} full passes of the same "
+                      f"{R}x{R}x{S} workload after 1 warm-up pass, {el:.1f} s, {threads} pthreads"}
+
+
+def main():
+    a = parse()
+    rank, world, local = rendezvous.env_world()
+    if world != a.gpus:
+        if "WORLD_SIZE" in os.environ:
+            raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+        world = 1
+    R, S = a.resolution, a.photon_steps
+    layout = vptmcm.LAYOUT_CORNER8 if a.layout == "corner8" else vptmcm.LAYOUT_LINEAR
+
+    # ---- inputs (synthetic)
+    t = time.perf_counter()
+    vol = cf.fbm_volume(a.volume, 512 if a.volume == 512 else a.volume)
+    gen_s = time.perf_counter() - t
+    tf = cf.tf_spectral()
+    spd, ldir = cf.light_default()
+    spec = cf.spectrum_buffer("12")
+    mvp = cf.default_mvp_inverse()
+
+    r = vptmcm.Renderer(R, device=local, layout=layout)
+    r.set_volume(vol)
+    r.set_material_tf(tf)
+    r.set_light(spd, ldir)
+    r.set_spectrum(spec)
+    r.set_params(extinction=a.extinction, bounces=8, steps=S)
+
+    multi = world > 1
+    if multi:
+        key = rendezvous.job_key()
+        uid = rendezvous.exchange_unique_id(rank, vptmcm.unique_id, key=key)
+        r.comm_init(uid, world, rank)
+        r.barrier()
+        if rank == 0:
+            rendezvous.cleanup(key)
+
+    seeds = cf.seed_stream(a.warmup + a.steps + 1, start=0, rank=rank)
+    r.reset(mvp, seeds[0])
+    for k in range(a.warmup):
+        r.render(mvp, seeds[1 + k])
+        if multi and (k + 1) % a.allreduce_every == 0:
+            r.allreduce_radiance()
+    r.synchronize()
+    if multi:
+        r.barrier()
+
+    # ---- timed region: K passes (+ composites), bracketed by barrier + sync
+    r.enable_kernel_timing(True)
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        r.render(mvp, seeds[1 + a.warmup + k])
+        if multi and (k + 1) % a.allreduce_every == 0:
+            r.allreduce_radiance()
+    r.synchronize()
+    if multi:
+        r.read_composite()  # waits for the last all-reduce
+    el = time.perf_counter() - t0
+    if multi:
+        r.barrier()
+    kern_ms, launches = r.kernel_time()
+    vals = np.array([el, kern_ms / max(launches, 1)])
+    if multi:
+        vals = r.allreduce_host(vals, op="max")
+    el_max, kern_avg_ms = float(vals[0]), float(vals[1])
+
+    photon_steps = world * R * R * S * a.steps
+    value = photon_steps / el_max / 1e6
+    bytes_per_launch = cf.algorithmic_bytes_per_pass(R, S)
+    achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
+
+    traffic = None
+    tp = Path(a.traffic_json)
+    if tp.exists():
+        try:
+            t = json.loads(tp.read_text())
+            if t.get("resolution") == R and t.get("steps") == S and t.get("layout") == a.layout:
+                traffic = t.get("hbm_bytes_per_launch")
+        except (ValueError, OSError):
+            traffic = None
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mphoton-steps/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(el_max * 1e3 / a.steps, 5), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {
+                "workload": f"C{'4' if multi else '3'}: {a.volume}^3 fBm volume (seed 512), spectral TF "
+                            f"(HG g=0.702), R={R}, S={S}, 12 bins, extinction {a.extinction}, "
+                            "default camera",
+                "resolution": R, "photon_steps_per_pass": S, "volume": a.volume,
+                "volume_layout": a.layout,
+                "parallelism": (f"photon-parallel replicas x{world}, RCCL all-reduce of (rgb*n, n) "
+                                f"every {a.allreduce_every} pass(es)") if multi else "single GPU",
+            },
+            "hbm_gbps_algorithmic": round(achieved, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic,
+                         "kernel": "k_march", "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
+                         "algorithmic_bytes_per_launch": bytes_per_launch},
+            "cpu_baseline": None,
+            "volume_gen_s": round(gen_s, 2),
+        }
+        if world == 1 and a.cpu_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline(vol, tf, spec, spd, ldir, mvp, R, S, a.extinction,
+                                               a.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    r.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,259 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Bar: bit-exact photon state (NaN == NaN) and bit-exact rgba16float image on the
+same seeded inputs — the arithmetic specification makes the two identical, so
+the fixed-seed tolerance of north_star (<= 1e-4 relative L2) is met with 0.
+Full-size (R = 512, 512^3 volume) frames are small enough for the threaded
+oracle, so the benchmark configuration itself is checked bit for bit.
+"""
+import numpy as np
+import pytest
+
+import oracle as orc
+import vptmcm
+from vptmcm import configs as cf
+
+pytestmark = pytest.mark.gpu
+
+LAYOUTS = [vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_LINEAR]
+
+
+def same_words(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    fa, fb = a.view(np.float32), b.view(np.float32)
+    return (a == b) | (np.isnan(fa) & np.isnan(fb))
+
+
+def assert_photons_equal(got, want, what=""):
+    ok = same_words(got[:, :34], want[:, :34])
+    if not ok.all():
+        bad = np.argwhere(~ok)
+        pix, word = bad[0]
+        raise AssertionError(f"{what}: {len(bad)} words differ; first photon {pix} word {word}: "
+                             f"gpu {got[pix, word]:#x} oracle {want[pix, word]:#x}")
+
+
+def assert_rgba_equal(got, want, what=""):
+    g, w = got.view(np.float16), want.view(np.float16)
+    ok = (got == want) | (np.isnan(g) & np.isnan(w))
+    assert ok.all(), f"{what}: {int((~ok).sum())} rgba16f halfs differ"
+
+
+def make_pair(R, vol, tf, spec="12", ext=32.0, layout=vptmcm.LAYOUT_CORNER8, light_dir=(1, 0, 0),
+              spd=None, bounces=8, steps=8, blur=0.0, upload_spectrum=True):
+    gpu = vptmcm.Renderer(R, device=0, layout=layout)
+    cpu = orc.Oracle(R)
+    spd = np.full(256, 100, np.uint8) if spd is None else spd
+    ld = np.asarray(light_dir, np.float32)
+    if upload_spectrum:
+        buf = cf.spectrum_buffer(spec)
+        gpu.set_spectrum(buf)
+        cpu.set_spectrum(buf)
+    gpu.set_volume(vol)
+    gpu.set_material_tf(tf)
+    gpu.set_light(spd, ld)
+    gpu.set_params(extinction=ext, bounces=bounces, steps=steps, blur=blur)
+    cpu.volume, cpu.tf, cpu.light, cpu.light_dir = vol, tf, spd, ld
+    cpu.params.update(extinction=ext, bounces=bounces, steps=steps, blur=blur)
+    return gpu, cpu
+
+
+def run_and_compare(gpu, cpu, mvp, seeds, what, nthreads=16):
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0], nthreads=nthreads)
+    assert_photons_equal(gpu.read_photons(), cpu.photons, what + " reset")
+    for k, s in enumerate(seeds[1:], 1):
+        gpu.render(mvp, s)
+        _, want = cpu.render(mvp, s, nthreads=nthreads)
+        assert_photons_equal(gpu.read_photons(), cpu.photons, f"{what} pass {k}")
+        assert_rgba_equal(gpu.read_rgba16f(), want, f"{what} pass {k}")
+
+
+def test_math_primitives_bitexact():
+    with vptmcm.Renderer(8, device=0) as gpu:
+        o = orc.Oracle(1)
+        rng = np.random.default_rng(7)
+        u = (rng.integers(0, 2 ** 32, 1 << 20, dtype=np.uint64).astype(np.float32) *
+             np.float32(2.0 ** -32)).astype(np.float32)
+        edge = np.float32([0.0, -0.0, 1.0, 1e-45, 1e-38, 3.0, np.inf, -1.0, np.nan])
+        xs = np.concatenate([u, edge]).view(np.uint32)
+        ang = (np.linspace(0, 6.2831855, 1 << 20, dtype=np.float32)).view(np.uint32)
+        for fn, inp in [(0, xs), (1, ang), (2, ang), (3, rng.integers(0, 2 ** 32, 1 << 20, dtype=np.uint64).astype(np.uint32)),
+                        (4, (rng.standard_normal(1 << 20).astype(np.float32) * 300).view(np.uint32))]:
+            g, c = gpu.debug_eval(fn, inp), o.eval_batch(fn, inp)
+            if fn == 4:
+                g, c = g.astype(np.uint16), c.astype(np.uint16)
+                ok = (g == c) | (np.isnan(g.view(np.float16)) & np.isnan(c.view(np.float16)))
+            elif fn == 3:
+                ok = g == c
+            else:
+                ok = same_words(g, c)
+            assert ok.all(), f"fn {fn}: {int((~ok).sum())} mismatches"
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+@pytest.mark.parametrize("tfname,ext", [("spectral", 1.0), ("spectral", 32.0), ("zero", 1.0),
+                                        ("grey", 32.0)])
+def test_c1_sphere_in_cube(layout, tfname, ext):
+    tf = {"spectral": cf.tf_spectral, "zero": cf.tf_zero, "grey": cf.tf_grey}[tfname]()
+    gpu, cpu = make_pair(64, cf.sphere_in_cube(64), tf, ext=ext, layout=layout)
+    run_and_compare(gpu, cpu, cf.default_mvp_inverse(), cf.seed_stream(9, start=0),
+                    f"C1 {tfname} ext={ext} layout={layout}")
+    gpu.close()
+
+
+@pytest.mark.parametrize("camera", ["near", "orbit", "orbit_tilted"])
+def test_cameras_and_bins(camera):
+    for spec in ("6", "3", "8_uneven", "12_wide"):
+        gpu, cpu = make_pair(48, cf.two_spheres(48), cf.tf_spectral(), spec=spec, ext=16.0)
+        run_and_compare(gpu, cpu, cf.golden_mvp(camera), cf.seed_stream(3, start=0),
+                        f"{camera} bins={spec}")
+        gpu.close()
+
+
+def test_edge_cases():
+    vol = cf.fbm_volume(40, 7, nthreads=8)
+    mvp = cf.default_mvp_inverse()
+    seeds = cf.seed_stream(4, start=0)
+    cases = [
+        dict(R=37, what="R not multiple of 8"),
+        dict(R=32, ext=0.0, what="extinction 0 (inf/NaN distances)"),
+        dict(R=32, bounces=0, what="no scattering"),
+        dict(R=32, light_dir=(0, 0, 0), what="isotropic light"),
+        dict(R=32, blur=0.3, steps=33, what="depth of field + odd steps"),
+        dict(R=32, steps=0, what="zero steps"),
+        dict(R=24, ext=1e4, what="huge majorant"),
+    ]
+    for c in cases:
+        what = c.pop("what")
+        R = c.pop("R")
+        gpu, cpu = make_pair(R, vol, cf.tf_spectral(), **c)
+        run_and_compare(gpu, cpu, mvp, seeds, what)
+        gpu.close()
+
+
+def test_first_reset_quirk_and_spectrum_change():
+    """reset() before the first spectrum upload, then renders with it."""
+    gpu, cpu = make_pair(32, cf.sphere_in_cube(32), cf.tf_spectral(), upload_spectrum=False)
+    mvp = cf.default_mvp_inverse()
+    gpu.reset(mvp, cf.seed_bits(0))
+    cpu.reset(mvp, cf.seed_bits(0))
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "zero-spectrum reset")
+    for k, spec in [(1, "12"), (2, "12"), (3, "6"), (4, "6")]:
+        buf = cf.spectrum_buffer(spec)
+        gpu.set_spectrum(buf)
+        cpu.set_spectrum(buf)
+        gpu.render(mvp, cf.seed_bits(k))
+        _, want = cpu.render(mvp, cf.seed_bits(k))
+        assert_photons_equal(gpu.read_photons(), cpu.photons, f"pass {k} spectrum {spec}")
+        assert_rgba_equal(gpu.read_rgba16f(), want, f"pass {k}")
+    gpu.close()
+
+
+def test_photon_roundtrip_and_resume():
+    gpu, cpu = make_pair(32, cf.sphere_in_cube(32), cf.tf_spectral())
+    mvp = cf.default_mvp_inverse()
+    gpu.reset(mvp, 1)
+    gpu.render(mvp, 2)
+    words = gpu.read_photons()
+    cpu.photons = words.copy()
+    gpu.write_photons(words)
+    assert np.array_equal(gpu.read_photons()[:, :34], words[:, :34])
+    gpu.render(mvp, 3)
+    cpu.render(mvp, 3)
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "resume")
+    gpu.close()
+
+
+def test_blockwise_volume_ingest_equals_whole():
+    """WebGPUVolume.readModality-style per-block writes land where they should."""
+    vol = cf.fbm_volume(48, 99, nthreads=8)
+    blocks = [((x, y, z), vol[z:z + 16, y:y + 24, x:x + 12])
+              for z in range(0, 48, 16) for y in range(0, 48, 24) for x in range(0, 48, 12)]
+    a = vptmcm.Renderer(32, device=0)
+    a.volume_blocks(vol.shape, blocks)
+    b, cpu = make_pair(32, vol, cf.tf_spectral())
+    a.set_spectrum(cf.spectrum_buffer("12"))
+    a.set_material_tf(cf.tf_spectral())
+    a.set_light(*cf.light_default())
+    a.set_params(extinction=32.0)
+    mvp = cf.default_mvp_inverse()
+    for r in (a, b):
+        r.reset(mvp, 5)
+        r.render(mvp, 6)
+    assert np.array_equal(a.read_photons(), b.read_photons())
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("n", [256, 512])
+def test_full_size_benchmark_config(n):
+    """C2 (256^3 grey) and C3 (512^3 spectral, g = 0.702) at R = 512, bit-exact."""
+    vol = cf.fbm_volume(n, 1234 if n == 256 else 512)
+    tf = cf.tf_grey() if n == 256 else cf.tf_spectral()
+    gpu, cpu = make_pair(512, vol, tf, ext=32.0)
+    run_and_compare(gpu, cpu, cf.default_mvp_inverse(), cf.seed_stream(3, start=0),
+                    f"C{2 if n == 256 else 3} R=512")
+    gpu.close()
+
+
+def test_properties_many_passes():
+    """Size-independent properties over many passes at R = 512: sample counts are
+    monotone, radiance is a running mean of values in [0, 5*max(spd)/255]."""
+    vol = cf.fbm_volume(128, 512)
+    gpu = vptmcm.Renderer(512, device=0)
+    gpu.set_spectrum(cf.spectrum_buffer("12"))
+    gpu.set_volume(vol)
+    gpu.set_material_tf(cf.tf_spectral())
+    gpu.set_light(*cf.light_default())
+    gpu.set_params(extinction=32.0)
+    mvp = cf.default_mvp_inverse()
+    gpu.reset(mvp, cf.seed_bits(0))
+    gpu.render_passes(mvp, cf.seed_stream(20))
+    a = gpu.read_photons()
+    gpu.render_passes(mvp, cf.seed_stream(20, start=21))
+    b = gpu.read_photons()
+    assert (b[:, 7] >= a[:, 7]).all() and (b[:, 7] > 0).all()
+    rad = b[:, 10:22].view(np.float32)
+    assert np.isfinite(rad).all() and rad.min() >= 0 and rad.max() <= 5 * 100 / 255 + 1e-6
+    gpu.close()
+
+
+def test_composite_single_rank():
+    """RCCL path with one rank: the composite equals the rank's own image."""
+    gpu, _ = make_pair(64, cf.sphere_in_cube(64), cf.tf_spectral())
+    gpu.comm_init(vptmcm.unique_id(), 1, 0)
+    mvp = cf.default_mvp_inverse()
+    gpu.reset(mvp, 1)
+    for s in cf.seed_stream(3):
+        gpu.render(mvp, s)
+        gpu.allreduce_radiance()
+    rgb, n = gpu.read_composite()
+    img = gpu.read_rgba16f()[..., :3].view(np.float16).astype(np.float32)
+    ph = gpu.read_photons()
+    assert np.array_equal(n.reshape(-1), ph[:, 7].astype(np.float32))
+    m = n > 0
+    np.testing.assert_allclose(rgb[m], img[m], rtol=1e-6, atol=1e-7)
+    gpu.barrier()
+    v = gpu.allreduce_host([1.0, 2.0], op="max")
+    assert list(v) == [1.0, 2.0]
+    gpu.close()
+
+
+def test_kernel_timing_counts_launches():
+    gpu, _ = make_pair(64, cf.sphere_in_cube(64), cf.tf_spectral())
+    mvp = cf.default_mvp_inverse()
+    gpu.reset(mvp, 1)
+    gpu.enable_kernel_timing(True)
+    gpu.render_passes(mvp, cf.seed_stream(5))
+    ms, n = gpu.kernel_time()
+    assert n == 5 and ms > 0
+    gpu.close()
+
+
+def test_render_without_volume_fails_loudly():
+    gpu = vptmcm.Renderer(16, device=0)
+    with pytest.raises(vptmcm.VptError, match="no volume"):
+        gpu.render(cf.default_mvp_inverse(), 1)
+    with pytest.raises(vptmcm.VptError, match="n_bins"):
+        gpu.set_spectrum(np.float32([13.0] + [0] * 63))
+    gpu.close()

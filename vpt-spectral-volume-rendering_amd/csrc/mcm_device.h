@@ -1,0 +1,130 @@
+// mcm_device.h — device-side arithmetic of the spectral MCM march (gfx950).
+//
+// Implements the arithmetic specification of DESIGN.md ("Arithmetic
+// specification"): the WGSL operations of MCMSpectralComputeRenderer.wgsl with
+// every implementation-defined choice (log/sin/cos, FMA contraction, min/max,
+// normalize, mat*vec order, sampler filtering, f16 rounding) fixed, so the
+// kernels agree bit for bit with the CPU oracle. Compiled with
+// -ffp-contract=off; f32 division and sqrt are hipcc's correctly rounded
+// defaults (never -ffast-math).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vpt {
+
+constexpr float kEps = 1e-5f;                     // wgsl:6
+constexpr float kTwoPi = 6.2831854820251465f;     // constants.wgsl:4 as f32
+constexpr float kInv255 = 0.003921568859368563f;  // unorm8 scale
+constexpr int kMaxBins = 12;                      // wgsl:236
+
+struct f3 { float x, y, z; };
+
+__device__ __forceinline__ float as_f(uint32_t u) { return __uint_as_float(u); }
+__device__ __forceinline__ uint32_t as_u(float f) { return __float_as_uint(f); }
+
+// IEEE minNum/maxNum with explicit compares; ties keep the first operand.
+__device__ __forceinline__ float smin(float a, float b) {
+  if (a != a) return b;
+  if (b != b) return a;
+  return b < a ? b : a;
+}
+__device__ __forceinline__ float smax(float a, float b) {
+  if (a != a) return b;
+  if (b != b) return a;
+  return b > a ? b : a;
+}
+
+// log(x) = e*ln2 + 2*atanh(s), s = (m-1)/(m+1), m in [sqrt(.5), sqrt(2)).
+__device__ __forceinline__ float spec_log(float x) {
+  uint32_t b = as_u(x);
+  if (!(x > 0.0f)) return (x == 0.0f) ? -__builtin_inff() : __builtin_nanf("");
+  if (b == 0x7f800000u) return x;
+  int e = 0;
+  if (b < 0x00800000u) {
+    x = x * 33554432.0f;
+    b = as_u(x);
+    e = -25;
+  }
+  e += (int)(b >> 23) - 127;
+  float m = as_f((b & 0x007fffffu) | 0x3f800000u);
+  if (m > 1.41421353816986083984375f) {
+    m = m * 0.5f;
+    e = e + 1;
+  }
+  float f = m - 1.0f;
+  float s = f / (2.0f + f);
+  float z = s * s;
+  float R = z * (0.6666666865348816f +
+                 z * (0.4000000059604645f +
+                      z * (0.2857142984867096f +
+                           z * (0.2222222238779068f + z * 0.1818181872367859f))));
+  float lm = (s + s) + s * R;
+  float ef = (float)e;
+  return (ef * 3.194618329871446e-05f + lm) + ef * 0.693115234375f;
+}
+
+// sin/cos: 3-part Cody-Waite reduction by pi/2, Taylor on |r| <= pi/4.
+__device__ __forceinline__ void spec_sincos(float x, float* so, float* co) {
+  float kf = floorf(x * 0.6366197466850281f + 0.5f);
+  float r = ((x - kf * 1.5703125f) - kf * 0.0004837512969970703f) - kf * 7.549790126404332e-08f;
+  float z = r * r;
+  float s = r + r * z * (-0.1666666716337204f +
+                         z * (0.008333333767950535f +
+                              z * (-0.00019841270113829523f +
+                                   z * (2.7557318844628753e-06f + z * -2.5052107943679403e-08f))));
+  float c = (1.0f - 0.5f * z) +
+            z * z * (0.0416666679084301f +
+                     z * (-0.0013888889225199819f +
+                          z * (2.4801587642286904e-05f + z * -2.755731998149713e-07f)));
+  int k = ((int)kf) & 3;
+  float sa = (k & 1) ? c : s;
+  float ca = (k & 1) ? s : c;
+  *so = (k & 2) ? -sa : sa;
+  *co = ((k + 1) & 2) ? -ca : ca;
+}
+
+// PCG-RXS-M-XS, pcg.wgsl:3-7
+__device__ __forceinline__ uint32_t pcg_hash(uint32_t v) {
+  uint32_t x = v * 747796405u + 2891336453u;
+  x = ((x >> ((x >> 28u) + 4u)) ^ x) * 277803737u;
+  return (x >> 22u) ^ x;
+}
+// squashlinear.wgsl:7-9
+__device__ __forceinline__ uint32_t hash3(uint32_t x, uint32_t y, uint32_t z) {
+  return pcg_hash(19u * x + 47u * y + 101u * z + 131u);
+}
+// uniformdivision.wgsl:3-6; f32(~0u) == 2^32, so the division is exact scaling.
+__device__ __forceinline__ float rnd_uniform(uint32_t& st) {
+  st = pcg_hash(st);
+  return (float)st * 2.3283064365386963e-10f;
+}
+
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ f3 norm3(f3 a) {
+  float l = __builtin_sqrtf(dot3(a, a));
+  return f3{a.x / l, a.y / l, a.z / l};
+}
+
+// float -> half, round to nearest even (v_cvt_f16_f32 under the default mode).
+__device__ __forceinline__ uint16_t f2h(float f) {
+  _Float16 h = (_Float16)f;
+  return __builtin_bit_cast(uint16_t, h);
+}
+
+// ---- sampler (linear, clamp-to-edge) ---------------------------------------
+__device__ __forceinline__ float clampc(float u) {
+  return u >= -1.0f ? (u <= 2.0f ? u : 2.0f) : -1.0f;
+}
+// texel-space coordinate: x = clampc(u)*N - 0.5; returns floor as int and f.
+__device__ __forceinline__ int axis_floor(float u, float n, float* f) {
+  float x = clampc(u) * n - 0.5f;
+  float fl = floorf(x);
+  *f = x - fl;
+  return (int)fl;
+}
+__device__ __forceinline__ int clampi(int i, int hi) { return i < 0 ? 0 : (i > hi ? hi : i); }
+__device__ __forceinline__ float lerp(float a, float b, float f) { return a + f * (b - a); }
+
+}  // namespace vpt

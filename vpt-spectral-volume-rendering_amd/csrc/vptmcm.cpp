@@ -1,0 +1,645 @@
+// vptmcm.cpp — implementation of the C-ABI declared in include/vptmcm.h.
+//
+// Host-side orchestration of one renderer instance on one MI355X:
+// resource ownership (photon planes, render target, volume, TF, light,
+// spectrum), per-pass uniform preparation, kernel launches on an in-order
+// HIP stream, HIP-event kernel timing, and the RCCL photon-parallel
+// composite. Each entry point cites the reference code it replaces.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/vptmcm.h"
+#include "kernels.h"
+
+using namespace vpt;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct EventPair {
+  hipEvent_t beg = nullptr, end = nullptr;
+};
+
+}  // namespace
+
+struct vptmcm {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint32_t R = 0, tiles_x = 0, n_tiles = 0, npad = 0;
+  uint32_t layout = kLayoutLinear;
+
+  float* photons = nullptr;    // kNumPlanes * npad words
+  uint16_t* rgba = nullptr;    // R*R*4 halfs
+  uint8_t* vol_lin = nullptr;  // W*H*D (staging for CORNER8; the volume for LINEAR)
+  void* vol_c8 = nullptr;      // (W+1)(H+1)(D+1) u64
+  uint32_t W = 0, H = 0, D = 0;
+  bool volume_ready = false;
+  uint32_t* tf = nullptr;      // 65536 rgba8 texels
+  uint8_t* light = nullptr;    // 256 bytes
+
+  float spectrum[VPTMCM_SPECTRUM_FLOATS] = {};
+  uint8_t light_host[256];
+  float light_dir[3] = {1.0f, 0.0f, 0.0f};
+  vptmcm_params params{1.0f, 0.0f, 8u, 8u, 0.0f};  // property defaults, js:19-48
+
+  // timing
+  bool timing = false;
+  std::vector<EventPair> events;
+  size_t events_used = 0;
+
+  // multi-GPU
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  hipStream_t comm_stream = nullptr;
+  float4* comp[2] = {nullptr, nullptr};
+  hipEvent_t comp_ready[2] = {nullptr, nullptr};
+  hipEvent_t comp_done[2] = {nullptr, nullptr};
+  int comp_next = 0, comp_last = -1;
+  double* host_scratch = nullptr;
+
+  std::string err;
+};
+
+#define FAIL(h, code, ...)                                              \
+  do {                                                                  \
+    char _b[512];                                                       \
+    snprintf(_b, sizeof _b, __VA_ARGS__);                               \
+    (h)->err = _b;                                                      \
+    return (code);                                                      \
+  } while (0)
+
+#define HIPCHK(h, expr)                                                        \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess)                                                      \
+      FAIL(h, VPTMCM_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(_e),     \
+           __FILE__, __LINE__);                                                \
+  } while (0)
+
+#define NCCLCHK(h, expr)                                                      \
+  do {                                                                        \
+    ncclResult_t _r = (expr);                                                 \
+    if (_r != ncclSuccess)                                                    \
+      FAIL(h, VPTMCM_ECOMM, "%s: %s", #expr, ncclGetErrorString(_r));         \
+  } while (0)
+
+namespace {
+
+// Uniform preparation shared by render and reset (wgsl:8-18, js:295-312).
+// Everything derived here is computed in IEEE f32 exactly as the kernel
+// would compute it per lane (host SSE arithmetic, no contraction).
+MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
+  MarchParams P;
+  memset(&P, 0, sizeof P);
+  memcpy(P.m, mvp, sizeof P.m);
+  P.inv_res[0] = (float)(1.0 / (double)h->R);  // Float32Array([1 / R]), js:297
+  P.inv_res[1] = P.inv_res[0];
+  P.seed = seed;
+  P.blur = h->params.blur;
+  P.extinction = h->params.extinction;
+  P.max_bounces = h->params.max_bounces;
+  P.steps = h->params.steps;
+  const float* s = h->spectrum;
+  float nbf = s[0] + 0.5f;  // u32(spectrum[0] + 0.5)
+  uint32_t nb = (nbf > 0.0f) ? (uint32_t)nbf : 0u;
+  P.nb = nb;
+  for (int i = 0; i < 13; i++) P.lam[i] = s[1 + i];
+  P.min_lam = s[1];
+  P.max_lam = s[nb + 1];
+  for (uint32_t i = 0; i < nb && i < (uint32_t)kMaxBins; i++) {
+    P.xb[i] = s[2 + nb + i];
+    P.yb[i] = s[2 + 2 * nb + i];
+    P.zb[i] = s[2 + 3 * nb + i];
+  }
+  const float* ld = h->light_dir;
+  float dd = (ld[0] * ld[0] + ld[1] * ld[1]) + ld[2] * ld[2];
+  float len = sqrtf(dd);
+  P.light_iso = len < kEps ? 1u : 0u;
+  if (!P.light_iso) {
+    P.light_dir[0] = ld[0] / len;
+    P.light_dir[1] = ld[1] / len;
+    P.light_dir[2] = ld[2] / len;
+  }
+  P.R = h->R;
+  P.tiles_x = h->tiles_x;
+  P.n_tiles = h->n_tiles;
+  P.npad = h->npad;
+  P.W = h->W;
+  P.H = h->H;
+  P.D = h->D;
+  return P;
+}
+
+int check_handle(vptmcm* h) { return h ? VPTMCM_OK : VPTMCM_EINVAL; }
+
+int time_begin(vptmcm* h, EventPair** ep) {
+  *ep = nullptr;
+  if (!h->timing) return VPTMCM_OK;
+  if (h->events_used == h->events.size()) {
+    EventPair e;
+    HIPCHK(h, hipEventCreate(&e.beg));
+    HIPCHK(h, hipEventCreate(&e.end));
+    h->events.push_back(e);
+  }
+  *ep = &h->events[h->events_used++];
+  HIPCHK(h, hipEventRecord((*ep)->beg, h->stream));
+  return VPTMCM_OK;
+}
+
+int do_march(vptmcm* h, const float* mvp, uint32_t seed) {
+  if (!h->volume_ready) FAIL(h, VPTMCM_ESTATE, "render: no volume set (setVolume first)");
+  MarchParams P = make_params(h, mvp, seed);
+  EventPair* ep = nullptr;
+  int rc = time_begin(h, &ep);
+  if (rc) return rc;
+  const uint8_t* vol = h->layout == kLayoutCorner8 ? (const uint8_t*)h->vol_c8 : h->vol_lin;
+  HIPCHK(h, launch_march(h->layout, P, h->photons, vol, h->tf, h->light, h->rgba, h->stream));
+  if (ep) HIPCHK(h, hipEventRecord(ep->end, h->stream));
+  return VPTMCM_OK;
+}
+
+void free_volume(vptmcm* h) {
+  if (h->vol_lin) (void)hipFree(h->vol_lin);
+  if (h->vol_c8) (void)hipFree(h->vol_c8);
+  h->vol_lin = nullptr;
+  h->vol_c8 = nullptr;
+  h->volume_ready = false;
+  h->W = h->H = h->D = 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* vptmcm_version(void) { return "vptmcm 0.1.0 (gfx950)"; }
+
+const char* vptmcm_last_error(const vptmcm* h) {
+  return h ? h->err.c_str() : g_create_error.c_str();
+}
+
+int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
+  g_create_error.clear();
+  if (!cfg || !out) {
+    g_create_error = "vptmcm_create: null argument";
+    return VPTMCM_EINVAL;
+  }
+  *out = nullptr;
+  if (cfg->resolution == 0 || cfg->resolution > 16384) {
+    g_create_error = "vptmcm_create: resolution must be in [1, 16384]";
+    return VPTMCM_EINVAL;
+  }
+  if (cfg->max_bins != VPTMCM_MAX_BINS) {
+    g_create_error = "vptmcm_create: max_bins must be 12 (MAX_N_BINS)";
+    return VPTMCM_EINVAL;
+  }
+  if (cfg->volume_layout > VPTMCM_LAYOUT_CORNER8) {
+    g_create_error = "vptmcm_create: unknown volume layout";
+    return VPTMCM_EINVAL;
+  }
+  vptmcm* h = new vptmcm();
+  auto fail = [&](int code) {
+    g_create_error = h->err;
+    vptmcm_destroy(h);
+    return code;
+  };
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    h->err = "vptmcm_create: no HIP device available";
+    return fail(VPTMCM_EHIP);
+  }
+  if (cfg->device >= 0) {
+    if (cfg->device >= ndev) {
+      h->err = "vptmcm_create: device ordinal out of range";
+      return fail(VPTMCM_EINVAL);
+    }
+    h->device = cfg->device;
+    if (hipSetDevice(h->device) != hipSuccess) {
+      h->err = "vptmcm_create: hipSetDevice failed";
+      return fail(VPTMCM_EHIP);
+    }
+  } else {
+    (void)hipGetDevice(&h->device);
+  }
+  h->layout = cfg->volume_layout;
+  h->R = cfg->resolution;
+  h->tiles_x = (h->R + 7) / 8;
+  h->n_tiles = h->tiles_x * h->tiles_x;
+  h->npad = h->n_tiles * 64;
+  memset(h->light_host, 0, sizeof h->light_host);
+#define CK(expr)                                                     \
+  do {                                                               \
+    hipError_t _e = (expr);                                          \
+    if (_e != hipSuccess) {                                          \
+      h->err = std::string(#expr ": ") + hipGetErrorString(_e);      \
+      return fail(VPTMCM_ENOMEM);                                    \
+    }                                                                \
+  } while (0)
+  CK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  CK(hipMalloc(&h->photons, (size_t)kNumPlanes * h->npad * sizeof(float)));
+  CK(hipMemsetAsync(h->photons, 0, (size_t)kNumPlanes * h->npad * sizeof(float), h->stream));
+  CK(hipMalloc(&h->rgba, (size_t)h->R * h->R * 4 * sizeof(uint16_t)));
+  CK(hipMemsetAsync(h->rgba, 0, (size_t)h->R * h->R * 4 * sizeof(uint16_t), h->stream));
+  CK(hipMalloc(&h->tf, VPTMCM_TF_BYTES));
+  CK(hipMemsetAsync(h->tf, 0, VPTMCM_TF_BYTES, h->stream));  // zero texture, js:85
+  CK(hipMalloc(&h->light, 256));
+  CK(hipMemsetAsync(h->light, 0, 256, h->stream));
+  CK(hipStreamSynchronize(h->stream));
+#undef CK
+  *out = h;
+  return VPTMCM_OK;
+}
+
+void vptmcm_destroy(vptmcm* h) {
+  if (!h) return;
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->comm_stream) (void)hipStreamSynchronize(h->comm_stream);
+  if (h->comm) ncclCommDestroy(h->comm);
+  for (int k = 0; k < 2; k++) {
+    if (h->comp[k]) (void)hipFree(h->comp[k]);
+    if (h->comp_ready[k]) (void)hipEventDestroy(h->comp_ready[k]);
+    if (h->comp_done[k]) (void)hipEventDestroy(h->comp_done[k]);
+  }
+  if (h->host_scratch) (void)hipFree(h->host_scratch);
+  for (auto& e : h->events) {
+    if (e.beg) (void)hipEventDestroy(e.beg);
+    if (e.end) (void)hipEventDestroy(e.end);
+  }
+  free_volume(h);
+  if (h->photons) (void)hipFree(h->photons);
+  if (h->rgba) (void)hipFree(h->rgba);
+  if (h->tf) (void)hipFree(h->tf);
+  if (h->light) (void)hipFree(h->light);
+  if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+// ------------------------------------------------------------------- inputs
+
+int vptmcm_volume_begin(vptmcm* h, uint32_t width, uint32_t height, uint32_t depth) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!width || !height || !depth || width > 8192 || height > 8192 || depth > 8192)
+    FAIL(h, VPTMCM_EINVAL, "volume dimensions must be in [1, 8192]");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  free_volume(h);
+  size_t n = (size_t)width * height * depth;
+  if (hipMalloc(&h->vol_lin, n) != hipSuccess) {
+    h->vol_lin = nullptr;
+    FAIL(h, VPTMCM_ENOMEM, "volume allocation of %zu bytes failed", n);
+  }
+  HIPCHK(h, hipMemsetAsync(h->vol_lin, 0, n, h->stream));  // fresh texture is zero
+  h->W = width;
+  h->H = height;
+  h->D = depth;
+  return VPTMCM_OK;
+}
+
+int vptmcm_volume_write_block(vptmcm* h, const uint8_t* data, uint32_t x, uint32_t y, uint32_t z,
+                              uint32_t bw, uint32_t bh, uint32_t bd) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!h->vol_lin) FAIL(h, VPTMCM_ESTATE, "volume_write_block before volume_begin");
+  if (!data) FAIL(h, VPTMCM_EINVAL, "null block data");
+  if ((uint64_t)x + bw > h->W || (uint64_t)y + bh > h->H || (uint64_t)z + bd > h->D)
+    FAIL(h, VPTMCM_EINVAL, "block [%u,%u,%u]+[%u,%u,%u] exceeds volume %ux%ux%u", x, y, z, bw, bh,
+         bd, h->W, h->H, h->D);
+  HIPCHK(h, hipSetDevice(h->device));
+  if (bw == h->W && bh == h->H && x == 0 && y == 0) {  // whole slices: one contiguous copy
+    HIPCHK(h, hipMemcpy(h->vol_lin + (size_t)z * h->W * h->H, data, (size_t)bw * bh * bd,
+                        hipMemcpyHostToDevice));
+    return VPTMCM_OK;
+  }
+  hipMemcpy3DParms p;
+  memset(&p, 0, sizeof p);
+  p.srcPtr = make_hipPitchedPtr((void*)data, bw, bw, bh);
+  p.dstPtr = make_hipPitchedPtr(h->vol_lin, h->W, h->W, h->H);
+  p.dstPos = make_hipPos(x, y, z);
+  p.extent = make_hipExtent(bw, bh, bd);
+  p.kind = hipMemcpyHostToDevice;
+  HIPCHK(h, hipMemcpy3D(&p));
+  return VPTMCM_OK;
+}
+
+int vptmcm_volume_end(vptmcm* h) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!h->vol_lin) FAIL(h, VPTMCM_ESTATE, "volume_end before volume_begin");
+  HIPCHK(h, hipSetDevice(h->device));
+  if (h->layout == kLayoutCorner8) {
+    size_t ncell = (size_t)(h->W + 1) * (h->H + 1) * (h->D + 1);
+    if (hipMalloc(&h->vol_c8, ncell * 8) != hipSuccess) {
+      h->vol_c8 = nullptr;
+      FAIL(h, VPTMCM_ENOMEM, "corner8 volume allocation of %zu bytes failed", ncell * 8);
+    }
+    HIPCHK(h, launch_corner8(h->vol_lin, h->W, h->H, h->D, h->vol_c8, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipFree(h->vol_lin));
+    h->vol_lin = nullptr;
+  } else {
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  }
+  h->volume_ready = true;
+  return VPTMCM_OK;
+}
+
+int vptmcm_set_volume(vptmcm* h, const uint8_t* voxels, uint32_t width, uint32_t height,
+                      uint32_t depth) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!voxels) FAIL(h, VPTMCM_EINVAL, "set_volume: null voxels");
+  int rc = vptmcm_volume_begin(h, width, height, depth);
+  if (rc) return rc;
+  rc = vptmcm_volume_write_block(h, voxels, 0, 0, 0, width, height, depth);
+  if (rc) return rc;
+  return vptmcm_volume_end(h);
+}
+
+int vptmcm_set_material_tf(vptmcm* h, const uint8_t* rgba) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!rgba) FAIL(h, VPTMCM_EINVAL, "set_material_tf: null data");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipMemcpyAsync(h->tf, rgba, VPTMCM_TF_BYTES, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));  // the caller may reuse its buffer
+  return VPTMCM_OK;
+}
+
+int vptmcm_set_light(vptmcm* h, const uint8_t* spd, const float dir[3]) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!spd || !dir) FAIL(h, VPTMCM_EINVAL, "set_light: null argument");
+  HIPCHK(h, hipSetDevice(h->device));
+  memcpy(h->light_host, spd, 256);
+  memcpy(h->light_dir, dir, sizeof h->light_dir);
+  HIPCHK(h, hipMemcpyAsync(h->light, h->light_host, 256, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return VPTMCM_OK;
+}
+
+int vptmcm_set_spectrum(vptmcm* h, const float* buf) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!buf) FAIL(h, VPTMCM_EINVAL, "set_spectrum: null buffer");
+  float nbf = buf[0] + 0.5f;
+  if (!(nbf >= 0.0f) || nbf >= (float)(VPTMCM_MAX_BINS + 1))
+    FAIL(h, VPTMCM_EINVAL, "set_spectrum: n_bins = %g exceeds MAX_N_BINS (12)", (double)buf[0]);
+  memcpy(h->spectrum, buf, sizeof h->spectrum);
+  return VPTMCM_OK;
+}
+
+int vptmcm_set_params(vptmcm* h, const vptmcm_params* p) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!p) FAIL(h, VPTMCM_EINVAL, "set_params: null params");
+  h->params = *p;
+  return VPTMCM_OK;
+}
+
+// ------------------------------------------------------------------ hot path
+
+int vptmcm_reset(vptmcm* h, const float* mvp, uint32_t seed_bits) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!mvp) FAIL(h, VPTMCM_EINVAL, "reset: null matrix");
+  HIPCHK(h, hipSetDevice(h->device));
+  MarchParams P = make_params(h, mvp, seed_bits);
+  HIPCHK(h, launch_reset(P, h->photons, h->stream));
+  return VPTMCM_OK;
+}
+
+int vptmcm_render(vptmcm* h, const float* mvp, uint32_t seed_bits) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!mvp) FAIL(h, VPTMCM_EINVAL, "render: null matrix");
+  HIPCHK(h, hipSetDevice(h->device));
+  return do_march(h, mvp, seed_bits);
+}
+
+int vptmcm_render_passes(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!mvp || (!seeds && n)) FAIL(h, VPTMCM_EINVAL, "render_passes: null argument");
+  HIPCHK(h, hipSetDevice(h->device));
+  for (uint32_t k = 0; k < n; k++) {
+    int rc = do_march(h, mvp, seeds[k]);
+    if (rc) return rc;
+  }
+  return VPTMCM_OK;
+}
+
+int vptmcm_synchronize(vptmcm* h) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (h->comm_stream) HIPCHK(h, hipStreamSynchronize(h->comm_stream));
+  return VPTMCM_OK;
+}
+
+// ------------------------------------------------------------------ outputs
+
+int vptmcm_read_rgba16f(vptmcm* h, uint16_t* out) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!out) FAIL(h, VPTMCM_EINVAL, "read_rgba16f: null output");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipMemcpyAsync(out, h->rgba, (size_t)h->R * h->R * 8, hipMemcpyDeviceToHost,
+                           h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return VPTMCM_OK;
+}
+
+int vptmcm_read_photons(vptmcm* h, void* out) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!out) FAIL(h, VPTMCM_EINVAL, "read_photons: null output");
+  HIPCHK(h, hipSetDevice(h->device));
+  std::vector<uint32_t> planes((size_t)kNumPlanes * h->npad);
+  HIPCHK(h, hipMemcpyAsync(planes.data(), h->photons, planes.size() * 4, hipMemcpyDeviceToHost,
+                           h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  uint32_t* o = static_cast<uint32_t*>(out);
+  const uint32_t one = 0x3f800000u;
+  for (uint32_t y = 0; y < h->R; y++)
+    for (uint32_t x = 0; x < h->R; x++) {
+      size_t i = (size_t)((y / 8) * h->tiles_x + x / 8) * 64 + (y % 8) * 8 + (x % 8);
+      uint32_t* w = o + ((size_t)y * h->R + x) * (VPTMCM_PHOTON_BYTES / 4);
+      for (int k = 0; k < 3; k++) w[k] = planes[(kPx + k) * (size_t)h->npad + i];
+      w[3] = planes[kBounces * (size_t)h->npad + i];
+      for (int k = 0; k < 3; k++) w[4 + k] = planes[(kDx + k) * (size_t)h->npad + i];
+      w[7] = planes[kSamples * (size_t)h->npad + i];
+      w[8] = planes[kBin * (size_t)h->npad + i];
+      w[9] = planes[kLambda * (size_t)h->npad + i];
+      for (int b = 0; b < kMaxBins; b++) w[10 + b] = planes[(kRad0 + b) * (size_t)h->npad + i];
+      for (int b = 0; b < kMaxBins; b++) w[22 + b] = one;
+      w[34] = w[35] = 0u;  // struct padding to the 144-B stride
+    }
+  return VPTMCM_OK;
+}
+
+int vptmcm_write_photons(vptmcm* h, const void* in) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!in) FAIL(h, VPTMCM_EINVAL, "write_photons: null input");
+  HIPCHK(h, hipSetDevice(h->device));
+  std::vector<uint32_t> planes((size_t)kNumPlanes * h->npad, 0u);
+  const uint32_t* src = static_cast<const uint32_t*>(in);
+  for (uint32_t y = 0; y < h->R; y++)
+    for (uint32_t x = 0; x < h->R; x++) {
+      size_t i = (size_t)((y / 8) * h->tiles_x + x / 8) * 64 + (y % 8) * 8 + (x % 8);
+      const uint32_t* w = src + ((size_t)y * h->R + x) * (VPTMCM_PHOTON_BYTES / 4);
+      for (int k = 0; k < 3; k++) planes[(kPx + k) * (size_t)h->npad + i] = w[k];
+      planes[kBounces * (size_t)h->npad + i] = w[3];
+      for (int k = 0; k < 3; k++) planes[(kDx + k) * (size_t)h->npad + i] = w[4 + k];
+      planes[kSamples * (size_t)h->npad + i] = w[7];
+      planes[kBin * (size_t)h->npad + i] = w[8];
+      planes[kLambda * (size_t)h->npad + i] = w[9];
+      for (int b = 0; b < kMaxBins; b++) planes[(kRad0 + b) * (size_t)h->npad + i] = w[10 + b];
+    }
+  HIPCHK(h, hipMemcpyAsync(h->photons, planes.data(), planes.size() * 4, hipMemcpyHostToDevice,
+                           h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return VPTMCM_OK;
+}
+
+// --------------------------------------------------------------- measurement
+
+int vptmcm_enable_kernel_timing(vptmcm* h, int enable) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->timing = enable != 0;
+  h->events_used = 0;
+  return VPTMCM_OK;
+}
+
+int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!total_ms || !launches) FAIL(h, VPTMCM_EINVAL, "kernel_time: null output");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  double sum = 0.0;
+  for (size_t k = 0; k < h->events_used; k++) {
+    float ms = 0.0f;
+    HIPCHK(h, hipEventElapsedTime(&ms, h->events[k].beg, h->events[k].end));
+    sum += ms;
+  }
+  *total_ms = sum;
+  *launches = h->events_used;
+  return VPTMCM_OK;
+}
+
+// ------------------------------------------------------------------ multi-GPU
+
+int vptmcm_comm_unique_id(uint8_t* out) {
+  if (!out) return VPTMCM_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) {
+    g_create_error = "ncclGetUniqueId failed";
+    return VPTMCM_ECOMM;
+  }
+  static_assert(sizeof(id) == VPTMCM_UNIQUE_ID_BYTES, "ncclUniqueId size");
+  memcpy(out, &id, sizeof id);
+  return VPTMCM_OK;
+}
+
+int vptmcm_comm_init(vptmcm* h, const uint8_t* uid, int nranks, int rank) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!uid || nranks < 1 || rank < 0 || rank >= nranks)
+    FAIL(h, VPTMCM_EINVAL, "comm_init: bad arguments (nranks=%d rank=%d)", nranks, rank);
+  if (h->comm) FAIL(h, VPTMCM_ESTATE, "comm_init: communicator already initialised");
+  HIPCHK(h, hipSetDevice(h->device));
+  ncclUniqueId id;
+  memcpy(&id, uid, sizeof id);
+  NCCLCHK(h, ncclCommInitRank(&h->comm, nranks, id, rank));
+  h->nranks = nranks;
+  h->rank = rank;
+  HIPCHK(h, hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking));
+  size_t bytes = (size_t)h->R * h->R * sizeof(float4);
+  for (int k = 0; k < 2; k++) {
+    HIPCHK(h, hipMalloc(&h->comp[k], bytes));
+    HIPCHK(h, hipEventCreateWithFlags(&h->comp_ready[k], hipEventDisableTiming));
+    HIPCHK(h, hipEventCreateWithFlags(&h->comp_done[k], hipEventDisableTiming));
+    HIPCHK(h, hipEventRecord(h->comp_done[k], h->comm_stream));
+  }
+  HIPCHK(h, hipMalloc(&h->host_scratch, 64 * sizeof(double)));
+  return VPTMCM_OK;
+}
+
+int vptmcm_comm_allreduce_radiance(vptmcm* h) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!h->comm) FAIL(h, VPTMCM_ECOMM, "comm_allreduce_radiance: no communicator");
+  HIPCHK(h, hipSetDevice(h->device));
+  int k = h->comp_next;
+  // the buffer must be free of the all-reduce issued two passes ago
+  HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[k], 0));
+  static const float kNoMatrix[16] = {};  // k_pack only reads the geometry fields
+  MarchParams P = make_params(h, kNoMatrix, 0);
+  HIPCHK(h, launch_pack(P, h->photons, h->rgba, h->comp[k], h->stream));
+  HIPCHK(h, hipEventRecord(h->comp_ready[k], h->stream));
+  HIPCHK(h, hipStreamWaitEvent(h->comm_stream, h->comp_ready[k], 0));
+  NCCLCHK(h, ncclAllReduce(h->comp[k], h->comp[k], (size_t)h->R * h->R * 4, ncclFloat32, ncclSum,
+                           h->comm, h->comm_stream));
+  HIPCHK(h, hipEventRecord(h->comp_done[k], h->comm_stream));
+  h->comp_last = k;
+  h->comp_next = k ^ 1;
+  return VPTMCM_OK;
+}
+
+int vptmcm_comm_read_composite(vptmcm* h, float* rgb, float* counts) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!h->comm || h->comp_last < 0) FAIL(h, VPTMCM_ESTATE, "read_composite: no all-reduce issued");
+  if (!rgb) FAIL(h, VPTMCM_EINVAL, "read_composite: null output");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->comm_stream));
+  size_t npx = (size_t)h->R * h->R;
+  std::vector<float> buf(npx * 4);
+  HIPCHK(h, hipMemcpy(buf.data(), h->comp[h->comp_last], npx * 16, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < npx; i++) {
+    float n = buf[i * 4 + 3];
+    for (int c = 0; c < 3; c++) rgb[i * 3 + c] = n > 0.0f ? buf[i * 4 + c] / n : 0.0f;
+    if (counts) counts[i] = n;
+  }
+  return VPTMCM_OK;
+}
+
+int vptmcm_comm_barrier(vptmcm* h) {
+  double v = 0.0;
+  return vptmcm_comm_allreduce_host(h, &v, 1, 0);
+}
+
+int vptmcm_comm_allreduce_host(vptmcm* h, double* vals, int n, int op) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!h->comm) FAIL(h, VPTMCM_ECOMM, "comm_allreduce_host: no communicator");
+  if (!vals || n < 1 || n > 64 || op < 0 || op > 1)
+    FAIL(h, VPTMCM_EINVAL, "comm_allreduce_host: bad arguments");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->host_scratch, vals, n * sizeof(double), hipMemcpyHostToDevice,
+                           h->comm_stream));
+  NCCLCHK(h, ncclAllReduce(h->host_scratch, h->host_scratch, (size_t)n, ncclFloat64,
+                           op ? ncclMax : ncclSum, h->comm, h->comm_stream));
+  HIPCHK(h, hipMemcpyAsync(vals, h->host_scratch, n * sizeof(double), hipMemcpyDeviceToHost,
+                           h->comm_stream));
+  HIPCHK(h, hipStreamSynchronize(h->comm_stream));
+  return VPTMCM_OK;
+}
+
+// --------------------------------------------------------------- diagnostics
+
+int vptmcm_debug_eval(vptmcm* h, int fn, const uint32_t* in, uint32_t* out, uint32_t n) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (fn < 0 || fn > 4 || (!in && n) || (!out && n)) FAIL(h, VPTMCM_EINVAL, "debug_eval: bad args");
+  if (n == 0) return VPTMCM_OK;
+  HIPCHK(h, hipSetDevice(h->device));
+  uint32_t *din = nullptr, *dout = nullptr;
+  HIPCHK(h, hipMalloc(&din, (size_t)n * 4));
+  if (hipMalloc(&dout, (size_t)n * 4) != hipSuccess) {
+    (void)hipFree(din);
+    FAIL(h, VPTMCM_ENOMEM, "debug_eval: allocation failed");
+  }
+  hipError_t e = hipMemcpy(din, in, (size_t)n * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = launch_debug_eval(fn, din, dout, n, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost);
+  (void)hipFree(din);
+  (void)hipFree(dout);
+  if (e != hipSuccess) FAIL(h, VPTMCM_EHIP, "debug_eval: %s", hipGetErrorString(e));
+  return VPTMCM_OK;
+}
+
+}  // extern "C"

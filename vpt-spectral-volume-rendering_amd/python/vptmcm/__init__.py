@@ -1,0 +1,11 @@
+"""Python harness binding of the MI355X spectral MCM march (libvptmcm.so).
+
+The product host is JavaScript (js/ over napi/); this package is the ctypes
+binding that bench.py and the tests use, plus synthetic input generators and
+the torch-free multi-process rendezvous used to bootstrap RCCL.
+"""
+from ._lib import (EXPORTS, LAYOUT_CORNER8, LAYOUT_LINEAR, PHOTON_BYTES, Renderer, VptError,
+                   lib_path, load, unique_id)
+
+__all__ = ["EXPORTS", "LAYOUT_CORNER8", "LAYOUT_LINEAR", "PHOTON_BYTES", "Renderer", "VptError",
+           "lib_path", "load", "unique_id"]

@@ -1,0 +1,278 @@
+"""ctypes binding of libvptmcm.so (include/vptmcm.h).
+
+Harness plumbing for bench.py and the pytest suite; the product's own host is
+the JavaScript renderer over the N-API shim (js/, napi/). There is no CPU
+fallback: if the HIP library is missing, loading fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+PKG = Path(__file__).resolve().parents[2]
+LIB_DIR = PKG / "lib"
+
+OK, EINVAL, EHIP, ESTATE, ENOMEM, ECOMM = 0, -1, -2, -3, -4, -5
+LAYOUT_LINEAR, LAYOUT_CORNER8 = 0, 1
+PHOTON_BYTES = 144
+MAX_BINS = 12
+
+# every symbol include/vptmcm.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "vptmcm_create", "vptmcm_destroy", "vptmcm_last_error", "vptmcm_set_volume",
+    "vptmcm_volume_begin", "vptmcm_volume_write_block", "vptmcm_volume_end",
+    "vptmcm_set_material_tf", "vptmcm_set_light", "vptmcm_set_spectrum", "vptmcm_set_params",
+    "vptmcm_reset", "vptmcm_render", "vptmcm_render_passes", "vptmcm_synchronize",
+    "vptmcm_read_rgba16f", "vptmcm_read_photons", "vptmcm_write_photons",
+    "vptmcm_enable_kernel_timing", "vptmcm_kernel_time", "vptmcm_comm_unique_id",
+    "vptmcm_comm_init", "vptmcm_comm_allreduce_radiance", "vptmcm_comm_read_composite",
+    "vptmcm_comm_barrier", "vptmcm_comm_allreduce_host", "vptmcm_debug_eval", "vptmcm_version",
+]
+
+
+class Config(C.Structure):
+    _fields_ = [("resolution", C.c_uint32), ("max_bins", C.c_uint32), ("device", C.c_int32),
+                ("volume_layout", C.c_uint32)]
+
+
+class Params(C.Structure):
+    _fields_ = [("extinction", C.c_float), ("anisotropy", C.c_float),
+                ("max_bounces", C.c_uint32), ("steps", C.c_uint32), ("blur", C.c_float)]
+
+
+class VptError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"vptmcm error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib_path() -> Path:
+    return LIB_DIR / "libvptmcm.so"
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = lib_path()
+    if not p.exists():
+        raise RuntimeError(f"{p} is not built: run `python __graft_entry__.py build` "
+                           "(the HIP path has no fallback)")
+    L = C.CDLL(str(p))
+    vp, u8p, f32p, u32p = C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_float), C.POINTER(C.c_uint32)
+    sig = {
+        "vptmcm_create": (C.c_int, [C.POINTER(Config), C.POINTER(vp)]),
+        "vptmcm_destroy": (None, [vp]),
+        "vptmcm_last_error": (C.c_char_p, [vp]),
+        "vptmcm_set_volume": (C.c_int, [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32]),
+        "vptmcm_volume_begin": (C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32]),
+        "vptmcm_volume_write_block": (C.c_int, [vp, vp] + [C.c_uint32] * 6),
+        "vptmcm_volume_end": (C.c_int, [vp]),
+        "vptmcm_set_material_tf": (C.c_int, [vp, vp]),
+        "vptmcm_set_light": (C.c_int, [vp, vp, f32p]),
+        "vptmcm_set_spectrum": (C.c_int, [vp, f32p]),
+        "vptmcm_set_params": (C.c_int, [vp, C.POINTER(Params)]),
+        "vptmcm_reset": (C.c_int, [vp, f32p, C.c_uint32]),
+        "vptmcm_render": (C.c_int, [vp, f32p, C.c_uint32]),
+        "vptmcm_render_passes": (C.c_int, [vp, f32p, u32p, C.c_uint32]),
+        "vptmcm_synchronize": (C.c_int, [vp]),
+        "vptmcm_read_rgba16f": (C.c_int, [vp, vp]),
+        "vptmcm_read_photons": (C.c_int, [vp, vp]),
+        "vptmcm_write_photons": (C.c_int, [vp, vp]),
+        "vptmcm_enable_kernel_timing": (C.c_int, [vp, C.c_int]),
+        "vptmcm_kernel_time": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+        "vptmcm_comm_unique_id": (C.c_int, [u8p]),
+        "vptmcm_comm_init": (C.c_int, [vp, u8p, C.c_int, C.c_int]),
+        "vptmcm_comm_allreduce_radiance": (C.c_int, [vp]),
+        "vptmcm_comm_read_composite": (C.c_int, [vp, f32p, f32p]),
+        "vptmcm_comm_barrier": (C.c_int, [vp]),
+        "vptmcm_comm_allreduce_host": (C.c_int, [vp, C.POINTER(C.c_double), C.c_int, C.c_int]),
+        "vptmcm_debug_eval": (C.c_int, [vp, C.c_int, u32p, u32p, C.c_uint32]),
+        "vptmcm_version": (C.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _ptr(a: np.ndarray, ctype=C.c_void_p):
+    return a.ctypes.data_as(ctype) if ctype is not C.c_void_p else C.c_void_p(a.ctypes.data)
+
+
+def _f32p(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _u32p(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+def mat_f32(mvp) -> np.ndarray:
+    m = np.ascontiguousarray(mvp, dtype=np.float32).reshape(16)
+    return m
+
+
+class Renderer:
+    """Thin handle wrapper (one HIP device, one stream)."""
+
+    def __init__(self, resolution: int = 512, device: int = -1, layout: int = LAYOUT_CORNER8):
+        self.L = load()
+        cfg = Config(resolution, MAX_BINS, device, layout)
+        h = C.c_void_p()
+        rc = self.L.vptmcm_create(C.byref(cfg), C.byref(h))
+        if rc != OK:
+            raise VptError(rc, self.L.vptmcm_last_error(None).decode())
+        self.h = h
+        self.R = resolution
+
+    # -- lifetime
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.L.vptmcm_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _ck(self, rc: int) -> None:
+        if rc != OK:
+            raise VptError(rc, self.L.vptmcm_last_error(self.h).decode())
+
+    # -- inputs
+    def set_volume(self, vol: np.ndarray) -> None:
+        """vol: uint8 array [D, H, W] (x fastest)."""
+        v = np.ascontiguousarray(vol, dtype=np.uint8)
+        D, H, W = v.shape
+        self._ck(self.L.vptmcm_set_volume(self.h, _ptr(v), W, H, D))
+
+    def volume_blocks(self, shape, blocks) -> None:
+        """Block-wise ingest: blocks = iterable of (origin_xyz, uint8 [d,h,w])."""
+        D, H, W = shape
+        self._ck(self.L.vptmcm_volume_begin(self.h, W, H, D))
+        for (x, y, z), b in blocks:
+            b = np.ascontiguousarray(b, dtype=np.uint8)
+            d, hh, w = b.shape
+            self._ck(self.L.vptmcm_volume_write_block(self.h, _ptr(b), x, y, z, w, hh, d))
+        self._ck(self.L.vptmcm_volume_end(self.h))
+
+    def set_material_tf(self, tf: np.ndarray) -> None:
+        t = np.ascontiguousarray(tf, dtype=np.uint8)
+        assert t.size == 256 * 256 * 4
+        self._ck(self.L.vptmcm_set_material_tf(self.h, _ptr(t)))
+
+    def set_light(self, spd: np.ndarray, direction) -> None:
+        s = np.ascontiguousarray(spd, dtype=np.uint8)
+        assert s.size == 256
+        d = np.ascontiguousarray(direction, dtype=np.float32)
+        self._ck(self.L.vptmcm_set_light(self.h, _ptr(s), _f32p(d)))
+
+    def set_spectrum(self, buf: np.ndarray) -> None:
+        b = np.zeros(64, np.float32)
+        src = np.asarray(buf)
+        if src.dtype == np.uint32:
+            src = src.view(np.float32)
+        b[: src.size] = src.astype(np.float32)
+        self._ck(self.L.vptmcm_set_spectrum(self.h, _f32p(b)))
+
+    def set_params(self, extinction=1.0, anisotropy=0.0, bounces=8, steps=8, blur=0.0) -> None:
+        p = Params(extinction, anisotropy, bounces, steps, blur)
+        self._ck(self.L.vptmcm_set_params(self.h, C.byref(p)))
+
+    # -- hot path
+    def reset(self, mvp, seed_bits: int) -> None:
+        m = mat_f32(mvp)
+        self._ck(self.L.vptmcm_reset(self.h, _f32p(m), int(seed_bits) & 0xFFFFFFFF))
+
+    def render(self, mvp, seed_bits: int) -> None:
+        m = mat_f32(mvp)
+        self._ck(self.L.vptmcm_render(self.h, _f32p(m), int(seed_bits) & 0xFFFFFFFF))
+
+    def render_passes(self, mvp, seeds) -> None:
+        m = mat_f32(mvp)
+        s = np.ascontiguousarray(seeds, dtype=np.uint32)
+        self._ck(self.L.vptmcm_render_passes(self.h, _f32p(m), _u32p(s), s.size))
+
+    def synchronize(self) -> None:
+        self._ck(self.L.vptmcm_synchronize(self.h))
+
+    # -- outputs
+    def read_rgba16f(self) -> np.ndarray:
+        out = np.empty((self.R, self.R, 4), np.uint16)
+        self._ck(self.L.vptmcm_read_rgba16f(self.h, _ptr(out)))
+        return out
+
+    def read_photons(self) -> np.ndarray:
+        """(R*R, 36) uint32 words in the reference's 144-B PhotonSpectral layout."""
+        out = np.empty((self.R * self.R, PHOTON_BYTES // 4), np.uint32)
+        self._ck(self.L.vptmcm_read_photons(self.h, _ptr(out)))
+        return out
+
+    def write_photons(self, words: np.ndarray) -> None:
+        w = np.ascontiguousarray(words, dtype=np.uint32)
+        assert w.size == self.R * self.R * PHOTON_BYTES // 4
+        self._ck(self.L.vptmcm_write_photons(self.h, _ptr(w)))
+
+    # -- measurement
+    def enable_kernel_timing(self, on: bool = True) -> None:
+        self._ck(self.L.vptmcm_enable_kernel_timing(self.h, 1 if on else 0))
+
+    def kernel_time(self):
+        ms, n = C.c_double(), C.c_uint64()
+        self._ck(self.L.vptmcm_kernel_time(self.h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    # -- multi-GPU
+    def comm_init(self, uid: bytes, nranks: int, rank: int) -> None:
+        u = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._ck(self.L.vptmcm_comm_init(self.h, u, nranks, rank))
+
+    def allreduce_radiance(self) -> None:
+        self._ck(self.L.vptmcm_comm_allreduce_radiance(self.h))
+
+    def read_composite(self):
+        rgb = np.empty((self.R, self.R, 3), np.float32)
+        n = np.empty((self.R, self.R), np.float32)
+        self._ck(self.L.vptmcm_comm_read_composite(self.h, _f32p(rgb), _f32p(n)))
+        return rgb, n
+
+    def barrier(self) -> None:
+        self._ck(self.L.vptmcm_comm_barrier(self.h))
+
+    def allreduce_host(self, vals, op: str = "sum") -> np.ndarray:
+        v = np.ascontiguousarray(vals, dtype=np.float64).copy()
+        self._ck(self.L.vptmcm_comm_allreduce_host(
+            self.h, v.ctypes.data_as(C.POINTER(C.c_double)), v.size, 1 if op == "max" else 0))
+        return v
+
+    # -- diagnostics
+    def debug_eval(self, fn: int, inp: np.ndarray) -> np.ndarray:
+        i = np.ascontiguousarray(inp, dtype=np.uint32)
+        o = np.empty_like(i)
+        self._ck(self.L.vptmcm_debug_eval(self.h, fn, _u32p(i), _u32p(o), i.size))
+        return o
+
+
+def unique_id() -> bytes:
+    L = load()
+    buf = (C.c_uint8 * 128)()
+    rc = L.vptmcm_comm_unique_id(buf)
+    if rc != OK:
+        raise VptError(rc, L.vptmcm_last_error(None).decode())
+    return bytes(buf)
