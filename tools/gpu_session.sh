@@ -1,0 +1,33 @@
+#!/bin/bash
+# One GPU session on the box: parity tests, bench, rocprofv3 kernel trace.
+# Stops at the first fault-class exit (abort/segv/timeout); a plain test
+# failure (exit 1) still lets the bench run.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+{ node --version; nproc; rocminfo 2>/dev/null | grep -m2 gfx; } > $OUT/env.txt 2>&1
+fault() { case $1 in 0|1|2|3|4|5) return 1;; *) return 0;; esac; }
+STEPS=${STEPS:-tests bench prof}
+for s in $STEPS; do
+  case $s in
+  tests)
+    timeout -k 10 ${TEST_T:-900} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
+    rc=$?; echo "pytest rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc ;;
+  smoke)
+    timeout -k 10 300 python __graft_entry__.py smoke > $OUT/smoke.log 2>&1
+    rc=$?; echo "smoke rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc ;;
+  bench)
+    timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err
+    rc=$?; echo "bench rc=$rc" | tee -a $OUT/status.txt; cat $OUT/bench.json; fault $rc && exit $rc ;;
+  prof)
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 100 --warmup 10 --cpu-seconds 0 ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err")
+    rc=$?; echo "prof rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc ;;
+  pmc)
+    for c in FETCH_SIZE WRITE_SIZE; do
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --pmc $c -d "$GRAFT_REPO_ROOT/$OUT/pmc_$c" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 2 --cpu-seconds 0 ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/$OUT/pmc_$c.json" 2> "$GRAFT_REPO_ROOT/$OUT/pmc_$c.err")
+      rc=$?; echo "pmc $c rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
+    done ;;
+  esac
+done
+exit 0
