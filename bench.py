@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--photon-steps", type=int, default=8, help="S: steps per pass")
     ap.add_argument("--extinction", type=float, default=32.0)
     ap.add_argument("--layout", choices=["corner8", "linear"], default="corner8")
+    ap.add_argument("--tf", choices=["spectral", "grey", "zero"], default="spectral")
     ap.add_argument("--allreduce-every", type=int, default=1,
                     help="passes between radiance all-reduces (N > 1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -96,7 +97,7 @@ def main():
     t = time.perf_counter()
     vol = cf.fbm_volume(a.volume, 512 if a.volume == 512 else a.volume)
     gen_s = time.perf_counter() - t
-    tf = cf.tf_spectral()
+    tf = {"spectral": cf.tf_spectral, "grey": cf.tf_grey, "zero": cf.tf_zero}[a.tf]()
     spd, ldir = cf.light_default()
     spec = cf.spectrum_buffer("12")
     mvp = cf.default_mvp_inverse()

@@ -17,6 +17,9 @@
  *     so CPU and GPU agree to the bit.
  *   - no FMA contraction anywhere (-ffp-contract=off); expressions are
  *     evaluated left to right as written in the WGSL.
+ *   - division: WGSL's f32 `/` is only 2.5-ULP accurate; here a / b is
+ *     defined as a * rcp(b) with rcp(b) = RN(1/b), the correctly rounded
+ *     reciprocal (<= 1.5 ULP), one reciprocal per divisor value.
  *   - min/max: IEEE minNum/maxNum written with explicit compares; ties keep
  *     the first operand.
  *   - normalize(v) = v / sqrt(dot(v,v)); length = sqrt(dot); dot = (x*x+y*y)+z*z.
@@ -52,6 +55,9 @@ _Static_assert(sizeof(orc_photon) == 144, "PhotonSpectral stride");
 
 typedef struct { float x, y, z; } v3;
 typedef struct { float x, y; } v2;
+
+/* correctly rounded reciprocal: the only true division of the spec */
+static inline float rcp(float x) { return 1.0f / x; }
 
 static inline float bitsf(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 static inline uint32_t fbits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
@@ -147,8 +153,8 @@ uint16_t orc_f2h(float f) {
 static inline float dot3(v3 a, v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 static inline float len3(v3 a) { return sqrtf(dot3(a, a)); }
 static inline v3 norm3(v3 a) {
-    float l = len3(a);
-    v3 r = {a.x / l, a.y / l, a.z / l};
+    float il = rcp(len3(a));
+    v3 r = {a.x * il, a.y * il, a.z * il};
     return r;
 }
 
@@ -171,7 +177,7 @@ static inline float rnd_uniform(uint32_t* st) {
 }
 /* exponential.wgsl:3-5 */
 static inline float rnd_exponential(uint32_t* st, float rate) {
-    return -orc_log(rnd_uniform(st)) / rate;
+    return -orc_log(rnd_uniform(st)) * rcp(rate);
 }
 /* disk.wgsl:3-7 */
 static inline v2 rnd_disk(uint32_t* st) {
@@ -272,7 +278,7 @@ typedef struct ctx {
 
 /* sample_light, wgsl:62-73 */
 static float sample_light(const ctx* c, v3 d, float wavelength) {
-    float t = (wavelength - 400.0f) / (700.0f - 400.0f);
+    float t = (wavelength - 400.0f) * rcp(700.0f - 400.0f);
     float intensity = orc_sample_light(c->light, t) * 5.0f;
     v3 ld = {c->u->light_dir[0], c->u->light_dir[1], c->u->light_dir[2]};
     if (len3(ld) < EPS) return intensity;
@@ -285,8 +291,8 @@ static v3 sample_hg(uint32_t* st, float g, v3 dir) {
     v3 u = rnd_sphere(st);
     if (fabsf(g) < EPS) return u;
     float g2 = g * g;
-    float c = (1.0f - g2) / ((1.0f - g) + (2.0f * g) * rnd_uniform(st));
-    float hgcos = ((1.0f + g2) - c * c) / (2.0f * g);
+    float c = (1.0f - g2) * rcp((1.0f - g) + (2.0f * g) * rnd_uniform(st));
+    float hgcos = ((1.0f + g2) - c * c) * rcp(2.0f * g);
     float ud = dot3(u, dir);
     v3 w = {u.x - ud * dir.x, u.y - ud * dir.y, u.z - ud * dir.z};
     v3 circle = norm3(w);
@@ -314,14 +320,17 @@ static void unproject_rand(uint32_t* st, v2 screen, const float* m, const float*
     float fd[4], td[4];
     mat_vec(m, nearp, fd);
     mat_vec(m, farp, td);
-    from->x = fd[0] / fd[3]; from->y = fd[1] / fd[3]; from->z = fd[2] / fd[3];
-    to->x = td[0] / td[3]; to->y = td[1] / td[3]; to->z = td[2] / td[3];
+    float iw = rcp(fd[3]);
+    from->x = fd[0] * iw; from->y = fd[1] * iw; from->z = fd[2] * iw;
+    iw = rcp(td[3]);
+    to->x = td[0] * iw; to->y = td[1] * iw; to->z = td[2] * iw;
 }
 
 /* intersectCube.wgsl:3-11 (only tnear is used by the caller) */
 static float intersect_cube_near(v3 o, v3 d) {
-    float tminx = (0.0f - o.x) / d.x, tminy = (0.0f - o.y) / d.y, tminz = (0.0f - o.z) / d.z;
-    float tmaxx = (1.0f - o.x) / d.x, tmaxy = (1.0f - o.y) / d.y, tmaxz = (1.0f - o.z) / d.z;
+    float rx = rcp(d.x), ry = rcp(d.y), rz = rcp(d.z);
+    float tminx = (0.0f - o.x) * rx, tminy = (0.0f - o.y) * ry, tminz = (0.0f - o.z) * rz;
+    float tmaxx = (1.0f - o.x) * rx, tmaxy = (1.0f - o.y) * ry, tmaxz = (1.0f - o.z) * rz;
     float t1x = smin(tminx, tmaxx), t1y = smin(tminy, tmaxy), t1z = smin(tminz, tmaxz);
     return smax(smax(t1x, t1y), t1z);
 }
@@ -374,12 +383,12 @@ static void photon_full_reset(const ctx* c, orc_photon* p, v2 screen, uint32_t* 
 /* PhotonSpectral_add_radiance, wgsl:292-302 */
 static void add_radiance(const ctx* c, orc_photon* p, float radiance) {
     uint32_t nb = n_bins_of(c->spec);
-    float n = (float)p->samples;
+    float in = rcp((float)p->samples);
     for (uint32_t i = 0u; i < nb && i < MAX_N_BINS; i++) {
         if (i == p->bin)
-            p->radiance[i] += (radiance - p->radiance[i]) / n;
+            p->radiance[i] += (radiance - p->radiance[i]) * in;
         else
-            p->radiance[i] += (0.0f - p->radiance[i]) / n;
+            p->radiance[i] += (0.0f - p->radiance[i]) * in;
     }
 }
 
@@ -418,7 +427,7 @@ static void render_pixel(const ctx* c, uint32_t R, uint32_t x, uint32_t y, orc_p
 
         float dens = orc_sample_volume(c->vol, c->W, c->H, c->D, p.position);
         float smp[3];
-        orc_sample_tf(c->tf, (p.wavelength - 400.0f) / (700.0f - 400.0f), dens, smp);
+        orc_sample_tf(c->tf, (p.wavelength - 400.0f) * rcp(700.0f - 400.0f), dens, smp);
         float albedo = smp[0], alpha = smp[1];
         float aniso = smp[2] * 2.0f - 1.0f;
 

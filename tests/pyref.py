@@ -47,6 +47,11 @@ class Rng:
         return F(self.s) / F(4294967296.0)
 
 
+def rcp(x):
+    """Correctly rounded reciprocal RN(1/x): the spec's only true division."""
+    return F(1) / F(x)
+
+
 def smin(a, b):
     if a != a:
         return b
@@ -110,8 +115,8 @@ def dot(a, b):
 
 
 def normalize(v):
-    l = np.sqrt(dot(v, v))
-    return [v[0] / l, v[1] / l, v[2] / l]
+    il = rcp(np.sqrt(dot(v, v)))
+    return [v[0] * il, v[1] * il, v[2] * il]
 
 
 def axis(u, n):
@@ -221,12 +226,14 @@ class Ref:
         farp = [screen[0] + (sqx * F(2) - F(1)) * self.inv, screen[1] + (sqy * F(2) - F(1)) * self.inv,
                 F(1), F(1)]
         fd, td = self.mat_vec(nearp), self.mat_vec(farp)
-        frm = [fd[0] / fd[3], fd[1] / fd[3], fd[2] / fd[3]]
-        to = [td[0] / td[3], td[1] / td[3], td[2] / td[3]]
+        iw, jw = rcp(fd[3]), rcp(td[3])
+        frm = [fd[0] * iw, fd[1] * iw, fd[2] * iw]
+        to = [td[0] * jw, td[1] * jw, td[2] * jw]
         d = normalize([to[0] - frm[0], to[1] - frm[1], to[2] - frm[2]])
         p.direction = d
         p.bounces = 0
-        t1 = [smin((F(0) - frm[i]) / d[i], (F(1) - frm[i]) / d[i]) for i in range(3)]
+        rd = [rcp(d[i]) for i in range(3)]
+        t1 = [smin((F(0) - frm[i]) * rd[i], (F(1) - frm[i]) * rd[i]) for i in range(3)]
         tn = smax(smax(smax(t1[0], t1[1]), t1[2]), F(0))
         p.position = [frm[i] + tn * d[i] for i in range(3)]
         nb = self.nb()
@@ -248,19 +255,19 @@ class Ref:
         return p
 
     def add_radiance(self, p, L):
-        n = F(p.samples)
+        inv_n = rcp(F(p.samples))
         for i in range(min(self.nb(), 12)):
             tgt = L if i == p.bin else F(0)
-            p.radiance[i] = p.radiance[i] + (tgt - p.radiance[i]) / n
+            p.radiance[i] = p.radiance[i] + (tgt - p.radiance[i]) * inv_n
 
     def render_pixel(self, p, x, y, seed):
         screen = self.screen(x, y)
         rng = Rng(hash3(x, y, seed))
         for _ in range(self.steps):
-            dist = -spec_log(rng.uniform()) / self.ext
+            dist = -spec_log(rng.uniform()) * rcp(self.ext)
             p.position = [p.position[i] + dist * p.direction[i] for i in range(3)]
             dens = tex3d(self.vol, p.position)
-            t = (p.wavelength - F(400)) / (F(700) - F(400))
+            t = (p.wavelength - F(400)) * rcp(F(700) - F(400))
             albedo, alpha, b = tex2d_tf(self.tf, t, dens)
             aniso = b * F(2) - F(1)
             pnull = F(1) - alpha
@@ -304,8 +311,8 @@ class Ref:
         if abs(g) < EPS:
             return u
         g2 = g * g
-        c = (F(1) - g2) / ((F(1) - g) + (F(2) * g) * rng.uniform())
-        cos = ((F(1) + g2) - c * c) / (F(2) * g)
+        c = (F(1) - g2) * rcp((F(1) - g) + (F(2) * g) * rng.uniform())
+        cos = ((F(1) + g2) - c * c) * rcp(F(2) * g)
         ud = dot(u, d)
         circle = normalize([u[0] - ud * d[0], u[1] - ud * d[1], u[2] - ud * d[2]])
         sn = np.sqrt(F(1) - cos * cos)

@@ -51,6 +51,12 @@ __device__ __forceinline__ bool tile_pixel(const MarchParams& P, uint32_t& x, ui
 }
 
 // -------------------------------------------------------------- reset kernel
+__device__ __forceinline__ bool near_fixed(const MarchParams& P, float sx, float sy, f3& from) {
+  bool fixed = P.blur == 0.0f && sx != 0.0f && sy != 0.0f;
+  if (fixed) from = unproject(P.m, sx, sy, -1.0f);
+  return fixed;
+}
+
 __global__ __launch_bounds__(kBlock) void k_reset(const MarchParams P, float* __restrict__ ph) {
   uint32_t x, y;
   size_t i;
@@ -58,9 +64,11 @@ __global__ __launch_bounds__(kBlock) void k_reset(const MarchParams P, float* __
   const size_t S = P.npad;
   float sx, sy;
   screen_of(P, x, y, sx, sy);
+  f3 from{0.0f, 0.0f, 0.0f};
+  bool fixed = near_fixed(P, sx, sy, from);
   uint32_t st = hash3(x, y, P.seed);
   Photon p;
-  photon_reset(P, p, sx, sy, st);
+  photon_reset(P, p, sx, sy, fixed, from, st);
   p.samples = 0u;
   store_state(ph, S, i, p);
 #pragma unroll
@@ -138,13 +146,15 @@ __global__ __launch_bounds__(kBlock) void k_march(const MarchParams P, float* __
   float sx, sy;
   screen_of(P, x, y, sx, sy);
 
+  f3 from{0.0f, 0.0f, 0.0f};
+  bool fixed = near_fixed(P, sx, sy, from);
   Photon p;
   load_photon(ph, S, i, p);
   WaveConst wc = wave_const(p.lambda, s_light);
   uint32_t st = hash3(x, y, P.seed);  // wgsl:122 (state is not carried across passes)
 
   for (uint32_t step = 0; step < P.steps; step++) {
-    float dist = -spec_log(rnd_uniform(st)) / P.extinction;  // exponential.wgsl
+    float dist = -spec_log(rnd_uniform(st)) * P.rcp_extinction;  // exponential.wgsl
     p.pos.x = p.pos.x + dist * p.dir.x;
     p.pos.y = p.pos.y + dist * p.dir.y;
     p.pos.z = p.pos.z + dist * p.dir.z;
@@ -181,15 +191,15 @@ __global__ __launch_bounds__(kBlock) void k_march(const MarchParams P, float* __
         }
       }
       p.samples++;
-      float n = (float)p.samples;
+      float inv_n = rcp((float)p.samples);
 #pragma unroll
       for (int b = 0; b < kMaxBins; b++) {  // PhotonSpectral_add_radiance, wgsl:292-302
         if ((uint32_t)b < P.nb) {
           float tgt = ((uint32_t)b == p.bin) ? rad : 0.0f;
-          p.rad[b] = p.rad[b] + (tgt - p.rad[b]) / n;
+          p.rad[b] = p.rad[b] + (tgt - p.rad[b]) * inv_n;
         }
       }
-      photon_reset(P, p, sx, sy, st);
+      photon_reset(P, p, sx, sy, fixed, from, st);
       wc = wave_const(p.lambda, s_light);
     } else if (wheel < pabs + pscat) {
       p.dir = sample_hg(st, aniso, p.dir);  // wgsl:156-160

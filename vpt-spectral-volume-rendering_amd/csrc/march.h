@@ -2,20 +2,24 @@
 //
 // One lane owns one photon (= one pixel), exactly like the reference's
 // compute_main (MCMSpectralComputeRenderer.wgsl:107-179 render, :213-231
-// reset). What is MI355X-specific is the data layout and mapping:
-//   * photon state is stored as 22 SoA planes of 32-bit words in
-//     "wave-tile" order — wave w of the grid owns an 8x8 pixel tile and lane
+// reset). What is MI355X-specific is the data layout, the mapping and the
+// instruction diet of the divergent paths:
+//   * photon state is stored as SoA planes of 32-bit words in "wave-tile"
+//     order — wave w of the grid owns an 8x8 pixel tile and lane
 //     l = 8*ly + lx its pixel — so every plane load/store is one fully
 //     coalesced 256-B wave access and a wave's rays start in a compact
 //     screen-space footprint (volume gathers hit the same cache lines);
 //   * the volume is either x-fastest u8 (LINEAR) or CORNER8: one u64 per
 //     trilinear cell holding its 8 corner voxels, so the 2x2x2 stencil is a
 //     single 8-B load instead of 8 byte gathers;
-//   * blocks are remapped so consecutive tiles run on the same XCD (shared
-//     L2 for neighbouring rays);
-//   * per-photon constants of the current wavelength (TF column taps and
-//     weight, light intensity) are computed once per (re)set and kept in
-//     registers instead of once per step — bit-identical by construction.
+//   * blocks are remapped so consecutive tiles run on the same XCD;
+//   * a wave of 64 photons almost always has some lane exiting/absorbing and
+//     some lane scattering in every step, so the wave pays for the reset and
+//     scatter paths nearly every step: they are kept short — one correctly
+//     rounded reciprocal per divisor (the spec's division), a branchless bin
+//     search, the per-pixel near point hoisted out of the loop when blur = 0,
+//     and the per-wavelength TF column / light terms cached per photon.
+//   All of these are value-preserving: results are bit-identical to the oracle.
 #pragma once
 
 #include "mcm_device.h"
@@ -35,9 +39,11 @@ struct MarchParams {
   uint32_t seed;         // bitcast<u32>(randSeed)
   float blur;
   float extinction;
+  float rcp_extinction;  // RN(1/extinction): exponential.wgsl's division
   uint32_t max_bounces;
   uint32_t steps;
   uint32_t nb;           // u32(spectrum[0] + 0.5)
+  uint32_t bins_sorted;  // lam[1..nb-1] non-decreasing: branchless bin search valid
   float lam[13];         // spectrum[1 .. 13]: bin boundaries
   float min_lam, max_lam; // spectrum[1], spectrum[nb + 1] (wgsl:262-263)
   float xb[kMaxBins], yb[kMaxBins], zb[kMaxBins];  // CMF bin means (0 past nb)
@@ -70,8 +76,8 @@ __device__ __forceinline__ f3 sample_hg(uint32_t& st, float g, f3 dir) {
   f3 u = rnd_sphere(st);
   if (__builtin_fabsf(g) < kEps) return u;
   float g2 = g * g;
-  float c = (1.0f - g2) / ((1.0f - g) + (2.0f * g) * rnd_uniform(st));
-  float hgcos = ((1.0f + g2) - c * c) / (2.0f * g);
+  float c = (1.0f - g2) * rcp((1.0f - g) + (2.0f * g) * rnd_uniform(st));
+  float hgcos = ((1.0f + g2) - c * c) * rcp(2.0f * g);
   float ud = dot3(u, dir);
   f3 circle = norm3(f3{u.x - ud * dir.x, u.y - ud * dir.y, u.z - ud * dir.z});
   float sn = __builtin_sqrtf(1.0f - hgcos * hgcos);
@@ -87,7 +93,7 @@ struct WaveConst {
   float intensity;
 };
 __device__ __forceinline__ WaveConst wave_const(float lambda, const float* s_light) {
-  float t = (lambda - 400.0f) / (700.0f - 400.0f);  // wgsl:64 == wgsl:77
+  float t = (lambda - 400.0f) * rcp(700.0f - 400.0f);  // wgsl:64 == wgsl:77
   WaveConst w;
   int ic = axis_floor(t, 256.0f, &w.fc);
   w.c0 = clampi(ic, 255);
@@ -96,12 +102,25 @@ __device__ __forceinline__ WaveConst wave_const(float lambda, const float* s_lig
   return w;
 }
 
-// PhotonSpectral_set_wavelength, wgsl:276-290 (bin search over lam[])
+// PhotonSpectral_set_wavelength, wgsl:276-290. For non-decreasing boundaries
+// the first i with lambda < lam[i] is 1 + #{i : !(lambda < lam[i])}, so the
+// search is a branchless count; otherwise the sequential first-match search.
 __device__ __forceinline__ uint32_t bin_of(const MarchParams& P, float lambda) {
-  uint32_t bin = P.nb - 1u;
+  if (P.nb == 0u) return 0xffffffffu;  // nb - 1 wraps (first-reset quirk)
+  uint32_t bin;
+  if (P.bins_sorted) {
+    bin = 0u;
 #pragma unroll
-  for (uint32_t i = 1u; i < (uint32_t)kMaxBins; i++) {
-    if (i < P.nb && bin == P.nb - 1u && lambda < P.lam[i]) bin = i - 1u;
+    for (uint32_t i = 1u; i < (uint32_t)kMaxBins; i++)
+      bin += (i < P.nb && !(lambda < P.lam[i])) ? 1u : 0u;
+  } else {
+    bin = P.nb - 1u;
+    for (uint32_t i = 1u; i < P.nb; i++) {
+      if (lambda < P.lam[i]) {
+        bin = i - 1u;
+        break;
+      }
+    }
   }
   return bin;
 }
@@ -113,31 +132,39 @@ struct Photon {
   float rad[kMaxBins];
 };
 
-// PhotonSpectral_reset, wgsl:249-266 (+ unprojectRand.wgsl, intersectCube.wgsl)
+// near point of the camera ray: M * (screen + disk*blur, -1, 1), divided by w
+__device__ __forceinline__ f3 unproject(const float* m, float a, float b, float z) {
+  float d[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) d[r] = ((m[r] * a + m[4 + r] * b) + m[8 + r] * z) + m[12 + r] * 1.0f;
+  float iw = rcp(d[3]);
+  return f3{d[0] * iw, d[1] * iw, d[2] * iw};
+}
+
+// PhotonSpectral_reset, wgsl:249-266 (+ unprojectRand.wgsl, intersectCube.wgsl).
+// fixed_from: blur == 0 and the screen position has no zero coordinate, so
+// screen + disk*0 == screen exactly and the near point is the per-pixel
+// constant `from`; the two disk draws are still consumed.
 __device__ __forceinline__ void photon_reset(const MarchParams& P, Photon& p, float sx, float sy,
-                                             uint32_t& st) {
-  float dx, dy;
-  rnd_disk(st, dx, dy);
-  float n0 = sx + dx * P.blur, n1 = sy + dy * P.blur;
+                                             bool fixed_from, f3 from, uint32_t& st) {
+  if (fixed_from) {
+    st = pcg_hash(pcg_hash(st));
+  } else {
+    float dx, dy;
+    rnd_disk(st, dx, dy);
+    from = unproject(P.m, sx + dx * P.blur, sy + dy * P.blur, -1.0f);
+  }
   float q0 = rnd_uniform(st);
   float q1 = rnd_uniform(st);
-  float f0 = sx + (q0 * 2.0f - 1.0f) * P.inv_res[0];
-  float f1 = sy + (q1 * 2.0f - 1.0f) * P.inv_res[1];
-  const float* m = P.m;
-  float fd[4], td[4];
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    fd[r] = ((m[r] * n0 + m[4 + r] * n1) + m[8 + r] * -1.0f) + m[12 + r] * 1.0f;
-    td[r] = ((m[r] * f0 + m[4 + r] * f1) + m[8 + r] * 1.0f) + m[12 + r] * 1.0f;
-  }
-  f3 from{fd[0] / fd[3], fd[1] / fd[3], fd[2] / fd[3]};
-  f3 to{td[0] / td[3], td[1] / td[3], td[2] / td[3]};
+  f3 to = unproject(P.m, sx + (q0 * 2.0f - 1.0f) * P.inv_res[0],
+                    sy + (q1 * 2.0f - 1.0f) * P.inv_res[1], 1.0f);
   f3 dir = norm3(f3{to.x - from.x, to.y - from.y, to.z - from.z});
   p.dir = dir;
   p.bounces = 0u;
-  float t1x = smin((0.0f - from.x) / dir.x, (1.0f - from.x) / dir.x);
-  float t1y = smin((0.0f - from.y) / dir.y, (1.0f - from.y) / dir.y);
-  float t1z = smin((0.0f - from.z) / dir.z, (1.0f - from.z) / dir.z);
+  float rx = rcp(dir.x), ry = rcp(dir.y), rz = rcp(dir.z);
+  float t1x = smin((0.0f - from.x) * rx, (1.0f - from.x) * rx);
+  float t1y = smin((0.0f - from.y) * ry, (1.0f - from.y) * ry);
+  float t1z = smin((0.0f - from.z) * rz, (1.0f - from.z) * rz);
   float tn = smax(smax(smax(t1x, t1y), t1z), 0.0f);
   p.pos = f3{from.x + tn * dir.x, from.y + tn * dir.y, from.z + tn * dir.z};
   float lambda = rnd_uniform(st) * (P.max_lam - P.min_lam) + P.min_lam;

@@ -101,10 +101,14 @@ __device__ __forceinline__ float rnd_uniform(uint32_t& st) {
   return (float)st * 2.3283064365386963e-10f;
 }
 
+// The spec's division: WGSL `a / b` (2.5 ULP allowed) is a * rcp(b) with
+// rcp(b) = RN(1/b), one correctly rounded reciprocal per divisor value.
+__device__ __forceinline__ float rcp(float x) { return 1.0f / x; }
+
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 __device__ __forceinline__ f3 norm3(f3 a) {
-  float l = __builtin_sqrtf(dot3(a, a));
-  return f3{a.x / l, a.y / l, a.z / l};
+  float il = rcp(__builtin_sqrtf(dot3(a, a)));
+  return f3{a.x * il, a.y * il, a.z * il};
 }
 
 // float -> half, round to nearest even (v_cvt_f16_f32 under the default mode).

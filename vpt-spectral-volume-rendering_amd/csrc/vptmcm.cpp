@@ -104,6 +104,7 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
   P.seed = seed;
   P.blur = h->params.blur;
   P.extinction = h->params.extinction;
+  P.rcp_extinction = 1.0f / h->params.extinction;  // RN(1/x), the spec's division
   P.max_bounces = h->params.max_bounces;
   P.steps = h->params.steps;
   const float* s = h->spectrum;
@@ -111,6 +112,9 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
   uint32_t nb = (nbf > 0.0f) ? (uint32_t)nbf : 0u;
   P.nb = nb;
   for (int i = 0; i < 13; i++) P.lam[i] = s[1 + i];
+  P.bins_sorted = 1u;
+  for (uint32_t i = 1; i + 1 < nb; i++)
+    if (!(s[1 + i] <= s[2 + i])) P.bins_sorted = 0u;  // lam[i] <= lam[i+1], NaN-safe
   P.min_lam = s[1];
   P.max_lam = s[nb + 1];
   for (uint32_t i = 0; i < nb && i < (uint32_t)kMaxBins; i++) {
@@ -122,10 +126,11 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
   float dd = (ld[0] * ld[0] + ld[1] * ld[1]) + ld[2] * ld[2];
   float len = sqrtf(dd);
   P.light_iso = len < kEps ? 1u : 0u;
-  if (!P.light_iso) {
-    P.light_dir[0] = ld[0] / len;
-    P.light_dir[1] = ld[1] / len;
-    P.light_dir[2] = ld[2] / len;
+  if (!P.light_iso) {  // normalize = v * RN(1/length)
+    float il = 1.0f / len;
+    P.light_dir[0] = ld[0] * il;
+    P.light_dir[1] = ld[1] * il;
+    P.light_dir[2] = ld[2] * il;
   }
   P.R = h->R;
   P.tiles_x = h->tiles_x;
