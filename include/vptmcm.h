@@ -196,6 +196,12 @@ int vptmcm_comm_allreduce_host(vptmcm* h, double* vals, int n, int op);
  * 2 = cos, 3 = hash (u32 bits in/out), 4 = float->half (u16 in low bits). */
 int vptmcm_debug_eval(vptmcm* h, int fn, const uint32_t* in, uint32_t* out, uint32_t n);
 
+/* Exhaustive device check of a fast arithmetic sequence against the correctly
+ * rounded reference over the u32 bit patterns [lo, lo + count) (count <= 2^32):
+ * returns the number of mismatches and up to nfirst mismatching inputs. */
+int vptmcm_debug_verify(vptmcm* h, int fn, uint32_t lo, uint64_t count, uint64_t* mismatches,
+                        uint32_t* first_bad, uint32_t nfirst);
+
 /* Library version string. */
 const char* vptmcm_version(void);
 

@@ -48,3 +48,10 @@ def test_tables():
 
 
 FBM32_HASH = "c4c7a0a97a586e75"
+
+
+def test_tf_materials_row_structure():
+    t = cf.tf_materials(True)
+    assert (t[180, :, 2] != t[180, 0, 2]).any()          # wavelength-varying anisotropy
+    t2 = cf.tf_materials(False)
+    assert all((t2[r, :, 2] == t2[r, 0, 2]).all() for r in range(256))

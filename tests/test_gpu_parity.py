@@ -101,6 +101,22 @@ def test_c1_sphere_in_cube(layout, tfname, ext):
     gpu.close()
 
 
+@pytest.mark.parametrize("variant", ["0", "1"])
+@pytest.mark.parametrize("layout", LAYOUTS)
+@pytest.mark.parametrize("tfname", ["spectral", "materials", "materials_const_b"])
+def test_march_variants_bitexact(variant, layout, tfname, monkeypatch):
+    """Every step-loop variant (speculative / plain) is bit-exact, with a
+    row-invariant anisotropy channel (LDS row table) and a wavelength-varying one
+    (4-corner gather)."""
+    monkeypatch.setenv("VPTMCM_MARCH_VARIANT", variant)
+    tf = {"spectral": cf.tf_spectral(), "materials": cf.tf_materials(True),
+          "materials_const_b": cf.tf_materials(False)}[tfname]
+    gpu, cpu = make_pair(64, cf.fbm_volume(64, 3, nthreads=8), tf, ext=24.0, layout=layout)
+    run_and_compare(gpu, cpu, cf.golden_mvp("orbit"), cf.seed_stream(5, start=0),
+                    f"variant {variant} layout {layout} tf {tfname}")
+    gpu.close()
+
+
 @pytest.mark.parametrize("camera", ["near", "orbit", "orbit_tilted"])
 def test_cameras_and_bins(camera):
     for spec in ("6", "3", "8_uneven", "12_wide"):

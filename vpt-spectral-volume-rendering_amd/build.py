@@ -54,6 +54,17 @@ def build_hip(force: bool = False) -> Path:
     return out
 
 
+def build_experiments() -> Path:
+    """Cost-attribution build (knock-out switches via VPTMCM_MARCH_VARIANT bits 1..4);
+    results are NOT valid from this library. Selected with VPTMCM_LIB=exp."""
+    out = LIB / "libvptmcm_exp.so"
+    srcs = [CSRC / "kernels.hip", CSRC / "vptmcm.cpp"]
+    hipcc = shutil.which("hipcc") or str(ROCM / "bin" / "hipcc")
+    _run([hipcc, *HIP_FLAGS, "-DVPT_EXPERIMENTS", "-shared", f"-I{REPO / 'include'}", *srcs, "-o",
+          out, "-lrccl", f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}"])
+    return out
+
+
 def build_napi(force: bool = False) -> Path | None:
     out = LIB / "vptmcm_napi.node"
     src = PKG / "napi" / "vptmcm_napi.c"

@@ -6,19 +6,34 @@
 
 namespace vpt {
 
-constexpr uint32_t kBlock = 256;  // 4 waves, each one 8x8 pixel tile
+constexpr uint32_t kBlock = 256;        // reset/pack: 4 waves, each one 8x8 pixel tile
+constexpr uint32_t kMarchBlock = 1024;  // march: 16 waves share the LDS copy of the TF
 
-inline uint32_t march_blocks(const MarchParams& P) {
-  return (P.n_tiles + (kBlock / 64) - 1) / (kBlock / 64);
+inline uint32_t tile_blocks(const MarchParams& P, uint32_t block) {
+  return (P.n_tiles + (block / 64) - 1) / (block / 64);
 }
+inline uint32_t march_blocks(const MarchParams& P) { return tile_blocks(P, kBlock); }
+
+// TF re-layouts (built on the host by vptmcm_set_material_tf):
+//   tf_rg  u16[256*256]: (albedo | alpha << 8) per texel — staged in LDS (128 KB)
+//   tf_b4  u32[257*257]: the 4 anisotropy corners of each bilinear cell
+//   tf_brow u8[256]: anisotropy per row when it does not vary with wavelength
+constexpr uint32_t kTfCells = 257;
 
 hipError_t launch_reset(const MarchParams& P, float* ph, hipStream_t s);
-hipError_t launch_march(uint32_t layout, const MarchParams& P, float* ph, const uint8_t* vol,
-                        const uint32_t* tf, const uint8_t* light, uint16_t* rgba, hipStream_t s);
+// variant: tuning bits (bit 0 = plain step loop instead of the speculative one)
+hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P, float* ph,
+                        const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
+                        const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba,
+                        hipStream_t s);
 hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, void* out,
                           hipStream_t s);
 hipError_t launch_pack(const MarchParams& P, const float* ph, const uint16_t* rgba, float4* out,
                        hipStream_t s);
+// experiment build only: read and clear the per-segment stamp sums (8 counters)
+hipError_t read_stamps(unsigned long long* out8);
+hipError_t launch_verify(int fn, uint32_t lo, uint32_t n, unsigned long long* bad, uint32_t* first,
+                         uint32_t nfirst, hipStream_t s);
 hipError_t launch_debug_eval(int fn, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s);
 
 }  // namespace vpt

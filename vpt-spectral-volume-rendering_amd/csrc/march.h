@@ -49,13 +49,14 @@ struct MarchParams {
   float xb[kMaxBins], yb[kMaxBins], zb[kMaxBins];  // CMF bin means (0 past nb)
   float light_dir[3];    // normalize(light_direction) (host-computed, IEEE)
   uint32_t light_iso;    // length(light_direction) < EPS
+  uint32_t b_rows;       // TF blue channel column-invariant: use the LDS row table
   uint32_t R, tiles_x, n_tiles, npad;
   uint32_t W, H, D;
 };
 
 // ---------------------------------------------------------------- RNG draws
 __device__ __forceinline__ void rnd_disk(uint32_t& st, float& dx, float& dy) {  // disk.wgsl
-  float radius = __builtin_sqrtf(rnd_uniform(st));
+  float radius = sqrt_cr(rnd_uniform(st));
   float angle = kTwoPi * rnd_uniform(st);
   float s, c;
   spec_sincos(angle, &s, &c);
@@ -66,7 +67,7 @@ __device__ __forceinline__ f3 rnd_sphere(uint32_t& st) {  // sphere.wgsl:4-10
   float dx, dy;
   rnd_disk(st, dx, dy);
   float nrm = dx * dx + dy * dy;
-  float radius = 2.0f * __builtin_sqrtf(1.0f - nrm);
+  float radius = 2.0f * sqrt_cr(1.0f - nrm);
   float z = 1.0f - 2.0f * nrm;
   return f3{radius * dx, radius * dy, z};
 }
@@ -80,7 +81,7 @@ __device__ __forceinline__ f3 sample_hg(uint32_t& st, float g, f3 dir) {
   float hgcos = ((1.0f + g2) - c * c) * rcp(2.0f * g);
   float ud = dot3(u, dir);
   f3 circle = norm3(f3{u.x - ud * dir.x, u.y - ud * dir.y, u.z - ud * dir.z});
-  float sn = __builtin_sqrtf(1.0f - hgcos * hgcos);
+  float sn = sqrt_cr(1.0f - hgcos * hgcos);
   return f3{sn * circle.x + hgcos * dir.x, sn * circle.y + hgcos * dir.y,
             sn * circle.z + hgcos * dir.z};
 }
@@ -88,7 +89,8 @@ __device__ __forceinline__ f3 sample_hg(uint32_t& st, float g, f3 dir) {
 // Per-photon wavelength constants: TF column taps + weight, and the light
 // intensity textureSampleLevel(uLightSpectrum, (t, .5)).r * 5 (wgsl:64-65).
 struct WaveConst {
-  int c0, c1;
+  int c0, c1;     // clamped column taps
+  int cc;         // column cell of the 4-corner b table: clamp(ic, -1, 255) + 1
   float fc;
   float intensity;
 };
@@ -98,6 +100,7 @@ __device__ __forceinline__ WaveConst wave_const(float lambda, const float* s_lig
   int ic = axis_floor(t, 256.0f, &w.fc);
   w.c0 = clampi(ic, 255);
   w.c1 = clampi(ic + 1, 255);
+  w.cc = clampi(ic + 1, 256);
   w.intensity = lerp(s_light[w.c0], s_light[w.c1], w.fc) * kInv255 * 5.0f;
   return w;
 }
@@ -168,6 +171,29 @@ __device__ __forceinline__ void photon_reset(const MarchParams& P, Photon& p, fl
   float tn = smax(smax(smax(t1x, t1y), t1z), 0.0f);
   p.pos = f3{from.x + tn * dir.x, from.y + tn * dir.y, from.z + tn * dir.z};
   float lambda = rnd_uniform(st) * (P.max_lam - P.min_lam) + P.min_lam;
+  p.lambda = lambda;
+  p.bin = bin_of(P, lambda);
+}
+
+// The same reset computed from pre-drawn hashes: h1,h2 are the disk draws
+// (already turned into dx, dy), h3,h4 the square, h5 the wavelength.
+__device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p, float sx, float sy,
+                                                 bool fixed_from, f3 from, float dx, float dy,
+                                                 uint32_t h3, uint32_t h4, uint32_t h5) {
+  if (!fixed_from) from = unproject(P.m, sx + dx * P.blur, sy + dy * P.blur, -1.0f);
+  float q0 = (float)h3 * 2.3283064365386963e-10f;
+  float q1 = (float)h4 * 2.3283064365386963e-10f;
+  f3 to = unproject(P.m, sx + (q0 * 2.0f - 1.0f) * P.inv_res[0],
+                    sy + (q1 * 2.0f - 1.0f) * P.inv_res[1], 1.0f);
+  f3 dir = norm3(f3{to.x - from.x, to.y - from.y, to.z - from.z});
+  p.dir = dir;
+  float rx = rcp(dir.x), ry = rcp(dir.y), rz = rcp(dir.z);
+  float t1x = smin((0.0f - from.x) * rx, (1.0f - from.x) * rx);
+  float t1y = smin((0.0f - from.y) * ry, (1.0f - from.y) * ry);
+  float t1z = smin((0.0f - from.z) * rz, (1.0f - from.z) * rz);
+  float tn = smax(smax(smax(t1x, t1y), t1z), 0.0f);
+  p.pos = f3{from.x + tn * dir.x, from.y + tn * dir.y, from.z + tn * dir.z};
+  float lambda = ((float)h5 * 2.3283064365386963e-10f) * (P.max_lam - P.min_lam) + P.min_lam;
   p.lambda = lambda;
   p.bin = bin_of(P, lambda);
 }

@@ -36,6 +36,51 @@ __device__ __forceinline__ float smax(float a, float b) {
   return b > a ? b : a;
 }
 
+// ---- correctly rounded reciprocal / sqrt / log division, fast -------------
+// The arithmetic spec needs RN(1/x), RN(sqrt x) and RN(a/b). hipcc's default
+// IEEE sequences are ~12 dependent instructions plus denorm-mode switches; the
+// sequences below use the hardware estimate + one FMA correction and are
+// PROVEN equal to the correctly rounded result for every u32 input by
+// tests/test_gpu_fastmath.py (exhaustive, on the GPU, through
+// vptmcm_debug_verify). Inputs outside the proven-exact ranges take the
+// default IEEE path.
+__device__ __noinline__ float rcp_slow(float x) { return 1.0f / x; }
+__device__ __noinline__ float sqrt_slow(float x) { return __builtin_sqrtf(x); }
+
+// RN(1/x): v_rcp_f32 + one Newton step is exact for biased exponent 1..252.
+__device__ __forceinline__ float rcp_cr(float x) {
+  float y = __builtin_amdgcn_rcpf(x);
+  float e = __builtin_fmaf(-x, y, 1.0f);
+  y = __builtin_fmaf(e, y, y);
+  uint32_t ex = (__float_as_uint(x) >> 23) & 0xffu;
+  if (__builtin_expect(ex - 1u >= 252u, 0)) y = rcp_slow(x);
+  return y;
+}
+
+// RN(sqrt x): v_sqrt_f32 + one Newton step (rsq estimate) is exact for
+// positive x with biased exponent 32..254.
+__device__ __forceinline__ float sqrt_cr(float x) {
+  float s = __builtin_amdgcn_sqrtf(x);
+  float e = __builtin_fmaf(-s, s, x);
+  float h = 0.5f * __builtin_amdgcn_rsqf(x);
+  s = __builtin_fmaf(e, h, s);
+  uint32_t ex = __float_as_uint(x) >> 23;  // sign bit included: negatives excluded
+  if (__builtin_expect(ex - 32u > 222u, 0)) s = sqrt_slow(x);
+  return s;
+}
+
+// RN(f / (2 + f)) for f = m - 1, m in [sqrt(.5), sqrt(2)] (spec_log's only
+// division): exact over that whole domain (proven exhaustively).
+__device__ __forceinline__ float log_div(float f) {
+  float d = 2.0f + f;
+  float y = __builtin_amdgcn_rcpf(d);
+  float e = __builtin_fmaf(-d, y, 1.0f);
+  y = __builtin_fmaf(e, y, y);
+  float q = f * y;
+  float r = __builtin_fmaf(-q, d, f);
+  return __builtin_fmaf(r, y, q);
+}
+
 // log(x) = e*ln2 + 2*atanh(s), s = (m-1)/(m+1), m in [sqrt(.5), sqrt(2)).
 __device__ __forceinline__ float spec_log(float x) {
   uint32_t b = as_u(x);
@@ -54,7 +99,7 @@ __device__ __forceinline__ float spec_log(float x) {
     e = e + 1;
   }
   float f = m - 1.0f;
-  float s = f / (2.0f + f);
+  float s = log_div(f);
   float z = s * s;
   float R = z * (0.6666666865348816f +
                  z * (0.4000000059604645f +
@@ -103,11 +148,11 @@ __device__ __forceinline__ float rnd_uniform(uint32_t& st) {
 
 // The spec's division: WGSL `a / b` (2.5 ULP allowed) is a * rcp(b) with
 // rcp(b) = RN(1/b), one correctly rounded reciprocal per divisor value.
-__device__ __forceinline__ float rcp(float x) { return 1.0f / x; }
+__device__ __forceinline__ float rcp(float x) { return rcp_cr(x); }
 
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 __device__ __forceinline__ f3 norm3(f3 a) {
-  float il = rcp(__builtin_sqrtf(dot3(a, a)));
+  float il = rcp(sqrt_cr(dot3(a, a)));
   return f3{a.x * il, a.y * il, a.z * il};
 }
 

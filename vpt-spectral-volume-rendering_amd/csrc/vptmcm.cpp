@@ -10,6 +10,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -34,6 +35,7 @@ struct vptmcm {
   hipStream_t stream = nullptr;
   uint32_t R = 0, tiles_x = 0, n_tiles = 0, npad = 0;
   uint32_t layout = kLayoutLinear;
+  uint32_t variant = 0;  // tuning knob (VPTMCM_MARCH_VARIANT), results identical
 
   float* photons = nullptr;    // kNumPlanes * npad words
   uint16_t* rgba = nullptr;    // R*R*4 halfs
@@ -41,7 +43,10 @@ struct vptmcm {
   void* vol_c8 = nullptr;      // (W+1)(H+1)(D+1) u64
   uint32_t W = 0, H = 0, D = 0;
   bool volume_ready = false;
-  uint32_t* tf = nullptr;      // 65536 rgba8 texels
+  uint16_t* tf_rg = nullptr;   // 65536 (albedo | alpha << 8) texels
+  uint32_t* tf_b4 = nullptr;   // 257*257 anisotropy corner cells
+  uint8_t* tf_brow = nullptr;  // 256 anisotropy rows (valid when b_rows)
+  uint32_t b_rows = 1;         // zero TF: column-invariant
   uint8_t* light = nullptr;    // 256 bytes
 
   float spectrum[VPTMCM_SPECTRUM_FLOATS] = {};
@@ -132,6 +137,7 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
     P.light_dir[1] = ld[1] * il;
     P.light_dir[2] = ld[2] * il;
   }
+  P.b_rows = h->b_rows;
   P.R = h->R;
   P.tiles_x = h->tiles_x;
   P.n_tiles = h->n_tiles;
@@ -165,7 +171,8 @@ int do_march(vptmcm* h, const float* mvp, uint32_t seed) {
   int rc = time_begin(h, &ep);
   if (rc) return rc;
   const uint8_t* vol = h->layout == kLayoutCorner8 ? (const uint8_t*)h->vol_c8 : h->vol_lin;
-  HIPCHK(h, launch_march(h->layout, P, h->photons, vol, h->tf, h->light, h->rgba, h->stream));
+  HIPCHK(h, launch_march(h->layout, h->variant, P, h->photons, vol, h->tf_rg, h->tf_b4, h->tf_brow,
+                         h->light, h->rgba, h->stream));
   if (ep) HIPCHK(h, hipEventRecord(ep->end, h->stream));
   return VPTMCM_OK;
 }
@@ -233,6 +240,7 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
     (void)hipGetDevice(&h->device);
   }
   h->layout = cfg->volume_layout;
+  if (const char* v = getenv("VPTMCM_MARCH_VARIANT")) h->variant = (uint32_t)strtoul(v, nullptr, 0);
   h->R = cfg->resolution;
   h->tiles_x = (h->R + 7) / 8;
   h->n_tiles = h->tiles_x * h->tiles_x;
@@ -251,8 +259,12 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   CK(hipMemsetAsync(h->photons, 0, (size_t)kNumPlanes * h->npad * sizeof(float), h->stream));
   CK(hipMalloc(&h->rgba, (size_t)h->R * h->R * 4 * sizeof(uint16_t)));
   CK(hipMemsetAsync(h->rgba, 0, (size_t)h->R * h->R * 4 * sizeof(uint16_t), h->stream));
-  CK(hipMalloc(&h->tf, VPTMCM_TF_BYTES));
-  CK(hipMemsetAsync(h->tf, 0, VPTMCM_TF_BYTES, h->stream));  // zero texture, js:85
+  CK(hipMalloc(&h->tf_rg, 65536 * sizeof(uint16_t)));
+  CK(hipMemsetAsync(h->tf_rg, 0, 65536 * sizeof(uint16_t), h->stream));  // zero texture, js:85
+  CK(hipMalloc(&h->tf_b4, kTfCells * kTfCells * sizeof(uint32_t)));
+  CK(hipMemsetAsync(h->tf_b4, 0, kTfCells * kTfCells * sizeof(uint32_t), h->stream));
+  CK(hipMalloc(&h->tf_brow, 256));
+  CK(hipMemsetAsync(h->tf_brow, 0, 256, h->stream));
   CK(hipMalloc(&h->light, 256));
   CK(hipMemsetAsync(h->light, 0, 256, h->stream));
   CK(hipStreamSynchronize(h->stream));
@@ -279,7 +291,9 @@ void vptmcm_destroy(vptmcm* h) {
   free_volume(h);
   if (h->photons) (void)hipFree(h->photons);
   if (h->rgba) (void)hipFree(h->rgba);
-  if (h->tf) (void)hipFree(h->tf);
+  if (h->tf_rg) (void)hipFree(h->tf_rg);
+  if (h->tf_b4) (void)hipFree(h->tf_b4);
+  if (h->tf_brow) (void)hipFree(h->tf_brow);
   if (h->light) (void)hipFree(h->light);
   if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -368,8 +382,33 @@ int vptmcm_set_material_tf(vptmcm* h, const uint8_t* rgba) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (!rgba) FAIL(h, VPTMCM_EINVAL, "set_material_tf: null data");
   HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipMemcpyAsync(h->tf, rgba, VPTMCM_TF_BYTES, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));  // the caller may reuse its buffer
+  // Re-layout for the march: (albedo, alpha) u16 texels (LDS-staged) and the
+  // 4-corner anisotropy cells; texel (row, col) = rgba[(row*256 + col)*4 + ch].
+  std::vector<uint16_t> rg(65536);
+  std::vector<uint32_t> b4((size_t)kTfCells * kTfCells);
+  for (int t = 0; t < 65536; t++)
+    rg[t] = (uint16_t)(rgba[t * 4 + 0] | (rgba[t * 4 + 1] << 8));
+  auto bch = [&](int r, int c) { return (uint32_t)rgba[(r * 256 + c) * 4 + 2]; };
+  for (int cr = 0; cr < (int)kTfCells; cr++)
+    for (int cc = 0; cc < (int)kTfCells; cc++) {
+      int r0 = cr - 1 < 0 ? 0 : cr - 1, r1 = cr > 255 ? 255 : cr;
+      int c0 = cc - 1 < 0 ? 0 : cc - 1, c1 = cc > 255 ? 255 : cc;
+      b4[(size_t)cr * kTfCells + cc] =
+          bch(r0, c0) | (bch(r0, c1) << 8) | (bch(r1, c0) << 16) | (bch(r1, c1) << 24);
+    }
+  HIPCHK(h, hipMemcpyAsync(h->tf_rg, rg.data(), rg.size() * 2, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->tf_b4, b4.data(), b4.size() * 4, hipMemcpyHostToDevice, h->stream));
+  // column-invariant anisotropy (the UI's per-material constant case): exact row table
+  uint8_t brow[256];
+  uint32_t inv = 1;
+  for (int r = 0; r < 256; r++) {
+    brow[r] = (uint8_t)bch(r, 0);
+    for (int c = 1; c < 256 && inv; c++)
+      if (bch(r, c) != brow[r]) inv = 0;
+  }
+  HIPCHK(h, hipMemcpyAsync(h->tf_brow, brow, 256, hipMemcpyHostToDevice, h->stream));
+  h->b_rows = inv;
+  HIPCHK(h, hipStreamSynchronize(h->stream));  // the host copies are freed on return
   return VPTMCM_OK;
 }
 
@@ -525,6 +564,18 @@ int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
   }
   *total_ms = sum;
   *launches = h->events_used;
+#ifdef VPT_EXPERIMENTS
+  unsigned long long st[8];
+  if (read_stamps(st) == hipSuccess) {
+    unsigned long long tot = 0;
+    for (int k = 0; k < 8; k++) tot += st[k];
+    const char* names[8] = {"prologue", "head", "reset", "scatter", "sample+tf", "decide", "epilogue", "-"};
+    fprintf(stderr, "stamps:");
+    for (int k = 0; k < 7; k++) fprintf(stderr, " %s=%.1f%%", names[k], tot ? 100.0 * st[k] / tot : 0.0);
+    fprintf(stderr, " (wave-cycles/launch/wave %.0f)\n",
+            h->events_used ? (double)tot / h->events_used / (h->npad / 64) : 0.0);
+  }
+#endif
   return VPTMCM_OK;
 }
 
@@ -644,6 +695,35 @@ int vptmcm_debug_eval(vptmcm* h, int fn, const uint32_t* in, uint32_t* out, uint
   (void)hipFree(din);
   (void)hipFree(dout);
   if (e != hipSuccess) FAIL(h, VPTMCM_EHIP, "debug_eval: %s", hipGetErrorString(e));
+  return VPTMCM_OK;
+}
+
+int vptmcm_debug_verify(vptmcm* h, int fn, uint32_t lo, uint64_t count, uint64_t* mismatches,
+                        uint32_t* first_bad, uint32_t nfirst) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!mismatches || (nfirst && !first_bad)) FAIL(h, VPTMCM_EINVAL, "debug_verify: bad args");
+  HIPCHK(h, hipSetDevice(h->device));
+  unsigned long long* dbad = nullptr;
+  uint32_t* dfirst = nullptr;
+  HIPCHK(h, hipMalloc(&dbad, sizeof(unsigned long long)));
+  HIPCHK(h, hipMalloc(&dfirst, (nfirst ? nfirst : 1) * sizeof(uint32_t)));
+  HIPCHK(h, hipMemsetAsync(dbad, 0, sizeof(unsigned long long), h->stream));
+  uint64_t done = 0;
+  hipError_t e = hipSuccess;
+  while (done < count && e == hipSuccess) {  // chunks of 2^31 (u32 range)
+    uint64_t chunk = count - done < (1ull << 31) ? count - done : (1ull << 31);
+    e = launch_verify(fn, (uint32_t)(lo + done), (uint32_t)chunk, dbad, dfirst, nfirst, h->stream);
+    done += chunk;
+  }
+  unsigned long long nb = 0;
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e == hipSuccess) e = hipMemcpy(&nb, dbad, sizeof nb, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && nfirst)
+    e = hipMemcpy(first_bad, dfirst, (size_t)nfirst * sizeof(uint32_t), hipMemcpyDeviceToHost);
+  (void)hipFree(dbad);
+  (void)hipFree(dfirst);
+  if (e != hipSuccess) FAIL(h, VPTMCM_EHIP, "debug_verify: %s", hipGetErrorString(e));
+  *mismatches = nb;
   return VPTMCM_OK;
 }
 

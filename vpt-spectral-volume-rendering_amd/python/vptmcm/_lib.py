@@ -7,6 +7,7 @@ fallback: if the HIP library is missing, loading fails loudly.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 import numpy as np
@@ -28,7 +29,8 @@ EXPORTS = [
     "vptmcm_read_rgba16f", "vptmcm_read_photons", "vptmcm_write_photons",
     "vptmcm_enable_kernel_timing", "vptmcm_kernel_time", "vptmcm_comm_unique_id",
     "vptmcm_comm_init", "vptmcm_comm_allreduce_radiance", "vptmcm_comm_read_composite",
-    "vptmcm_comm_barrier", "vptmcm_comm_allreduce_host", "vptmcm_debug_eval", "vptmcm_version",
+    "vptmcm_comm_barrier", "vptmcm_comm_allreduce_host", "vptmcm_debug_eval",
+    "vptmcm_debug_verify", "vptmcm_version",
 ]
 
 
@@ -52,6 +54,9 @@ _lib = None
 
 
 def lib_path() -> Path:
+    # VPTMCM_LIB=exp selects the cost-attribution build (tools only; results invalid)
+    if os.environ.get("VPTMCM_LIB") == "exp":
+        return LIB_DIR / "libvptmcm_exp.so"
     return LIB_DIR / "libvptmcm.so"
 
 
@@ -93,6 +98,8 @@ def load() -> C.CDLL:
         "vptmcm_comm_barrier": (C.c_int, [vp]),
         "vptmcm_comm_allreduce_host": (C.c_int, [vp, C.POINTER(C.c_double), C.c_int, C.c_int]),
         "vptmcm_debug_eval": (C.c_int, [vp, C.c_int, u32p, u32p, C.c_uint32]),
+        "vptmcm_debug_verify": (C.c_int, [vp, C.c_int, C.c_uint32, C.c_uint64,
+                                          C.POINTER(C.c_uint64), u32p, C.c_uint32]),
         "vptmcm_version": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
@@ -267,6 +274,14 @@ class Renderer:
         o = np.empty_like(i)
         self._ck(self.L.vptmcm_debug_eval(self.h, fn, _u32p(i), _u32p(o), i.size))
         return o
+
+
+    def debug_verify(self, fn: int, lo: int = 0, count: int = 1 << 32, nfirst: int = 16):
+        bad = C.c_uint64()
+        first = np.zeros(max(nfirst, 1), np.uint32)
+        self._ck(self.L.vptmcm_debug_verify(self.h, fn, lo, count, C.byref(bad), _u32p(first),
+                                            nfirst))
+        return bad.value, first[: min(nfirst, bad.value)]
 
 
 def unique_id() -> bytes:

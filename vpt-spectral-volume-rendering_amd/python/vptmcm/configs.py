@@ -153,6 +153,27 @@ def tf_spectral() -> np.ndarray:
     return t
 
 
+def tf_materials(varying_anisotropy: bool = True) -> np.ndarray:
+    """A UI-like TF (MaterialTransferFunction.js:56-75 paints one material's
+    256-entry albedo/alpha/anisotropy arrays into every density row of a range):
+    three materials over density ranges; with varying_anisotropy the third
+    material's anisotropy depends on wavelength (the general, non-row-invariant
+    blue channel)."""
+    t = np.zeros((256, 256, 4), dtype=np.uint8)
+    col = np.arange(256)
+    mats = [
+        (slice(20, 90), 180, 60, np.full(256, 127)),
+        (slice(90, 170), (150 + 80 * np.cos(col / 40.0)).astype(int), 140, np.full(256, 200)),
+        (slice(170, 256), 230, 230,
+         (60 + col * 0.7).astype(int) if varying_anisotropy else np.full(256, 30)),
+    ]
+    for rows, alb, alpha, aniso in mats:
+        t[rows, :, 0] = alb
+        t[rows, :, 1] = alpha
+        t[rows, :, 2] = aniso
+    return t
+
+
 def light_default():
     """js:82-83: SPD 100 everywhere, direction [1, 0, 0]."""
     return np.full(256, 100, dtype=np.uint8), np.array([1.0, 0.0, 0.0], dtype=np.float32)
