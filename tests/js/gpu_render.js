@@ -1,0 +1,45 @@
+// GPU driver for tests/test_js_gpu.py: renders through the JavaScript renderer
+// (N-API -> C-ABI -> HIP) exactly as the reference application would drive
+// WebGPUMCMSpectralComputeRenderer, and dumps photons + image for comparison
+// with the CPU oracle. Usage: node gpu_render.js <case.json> <outdir>
+'use strict';
+const fs = require('fs');
+const path = require('path');
+
+const ROOT = path.resolve(__dirname, '..', '..');
+const V = require(path.join(ROOT, 'vpt-spectral-volume-rendering_amd', 'js'));
+
+(async () => {
+  const c = JSON.parse(fs.readFileSync(process.argv[2]));
+  const out = process.argv[3];
+  const cie = JSON.parse(fs.readFileSync(path.join(ROOT, 'tests', 'golden', 'cie1931.json')));
+  let k = 0;
+  const random = () => c.seeds[k++];  // Math.random() stand-in: exact f32 values
+
+  const renderer = new (V.RendererFactory('mcm-spectral-compute'))(
+    V.createDevice(0, c.layout), null, new V.Camera(c.camera || {}), null,
+    { resolution: c.R, cie, random });
+  renderer.extinction = c.extinction;
+  renderer.bounces = c.bounces;
+  renderer.steps = c.steps;
+  renderer.setMaterialTransferFunction(new Uint8Array(fs.readFileSync(c.tf_path)), false);
+
+  const reader = new V.RAWReader(new V.FileLoader(c.volume_path),
+    { width: c.W, height: c.H, depth: c.D });
+  const volume = new V.Volume(reader);
+  if (c.stream_volume) {
+    await renderer.loadVolume(volume);        // block-wise HBM ingest, then reset() (seed 0)
+  } else {
+    await volume.load();
+    renderer.setVolume(volume);               // host copy upload, then reset() (seed 0)
+  }
+  for (let p = 0; p < c.passes; p++) renderer.render();
+  if (c.change_event) {                       // UI property edit -> reset (js:116-125)
+    renderer.setProperty('extinction', c.extinction);
+  }
+  const tex = renderer.getTexture();
+  fs.writeFileSync(path.join(out, 'photons.bin'), Buffer.from(renderer.readPhotons().buffer));
+  fs.writeFileSync(path.join(out, 'rgba.bin'), Buffer.from(tex.data.buffer));
+  fs.writeFileSync(path.join(out, 'meta.json'), JSON.stringify({ seeds_used: k }));
+  renderer.destroy();
+})().catch(e => { console.error(e.stack); process.exit(1); });

@@ -1,0 +1,82 @@
+"""The JavaScript renderer (N-API -> C-ABI -> HIP) against the CPU oracle.
+
+Node drives MCMSpectralComputeRenderer as the reference application drives
+WebGPUMCMSpectralComputeRenderer: construct, set the TF, load the volume
+through RAWReader/Volume (which resets: first reset sees the all-zero spectrum
+buffer, as in the reference), render K passes with Math.random()-style seeds.
+The oracle replays the same call sequence; photons and image must be bit-exact.
+"""
+import json
+import shutil
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from vptmcm import configs as cf
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def run_case(tmp_path, vol, tf, R=64, passes=3, ext=32.0, layout="corner8", stream=True,
+             change_event=False):
+    D, H, W = vol.shape
+    (tmp_path / "vol.raw").write_bytes(np.ascontiguousarray(vol).tobytes())
+    (tmp_path / "tf.bin").write_bytes(np.ascontiguousarray(tf).tobytes())
+    seeds = [float(np.uint32(cf.seed_bits(k)).view(np.float32)) for k in range(passes + 2)]
+    case = dict(R=R, passes=passes, extinction=ext, bounces=8, steps=8, layout=layout,
+                W=W, H=H, D=D, volume_path=str(tmp_path / "vol.raw"), tf_path=str(tmp_path / "tf.bin"),
+                seeds=seeds, stream_volume=stream, change_event=change_event)
+    (tmp_path / "case.json").write_text(json.dumps(case))
+    r = subprocess.run(["node", str(ROOT / "tests" / "js" / "gpu_render.js"), str(tmp_path / "case.json"),
+                        str(tmp_path)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    ph = np.frombuffer((tmp_path / "photons.bin").read_bytes(), np.uint32).reshape(R * R, 36)
+    rgba = np.frombuffer((tmp_path / "rgba.bin").read_bytes(), np.uint16).reshape(R, R, 4)
+    used = json.loads((tmp_path / "meta.json").read_text())["seeds_used"]
+    return ph, rgba, seeds, used
+
+
+def oracle_replay(vol, tf, R, seeds, passes, ext, change_event=False):
+    o = orc.Oracle(R)
+    o.volume, o.tf, o.light = vol, tf, np.full(256, 100, np.uint8)
+    o.params.update(extinction=ext, bounces=8, steps=8)
+    mvp = cf.default_mvp_inverse()
+    bits = lambda s: int(np.float32(s).view(np.uint32))  # noqa: E731
+    o.reset(mvp, bits(seeds[0]))                 # spectrum still all zero here
+    o.set_spectrum(cf.spectrum_buffer("12"))     # uploaded by the first render
+    rgba = None
+    for k in range(passes):
+        _, rgba = o.render(mvp, bits(seeds[1 + k]))
+    if change_event:
+        o.reset(mvp, bits(seeds[1 + passes]))
+    return o.photons, rgba
+
+
+def same(a, b):
+    fa, fb = a.view(np.float32), b.view(np.float32)
+    return ((a == b) | (np.isnan(fa) & np.isnan(fb))).all()
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+@pytest.mark.parametrize("layout,stream", [("corner8", True), ("linear", False)])
+def test_js_renderer_bitexact(tmp_path, layout, stream):
+    vol, tf = cf.sphere_in_cube(64), cf.tf_spectral()
+    ph, rgba, seeds, used = run_case(tmp_path, vol, tf, layout=layout, stream=stream)
+    assert used == 4  # one seed per reset/render, like Math.random() in js:231/298
+    want_ph, want_rgba = oracle_replay(vol, tf, 64, seeds, 3, 32.0)
+    assert same(ph[:, :34], want_ph[:, :34])
+    assert np.array_equal(rgba, want_rgba)
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+def test_js_property_change_resets(tmp_path):
+    vol, tf = cf.two_spheres(48), cf.tf_materials(True)
+    ph, _, seeds, used = run_case(tmp_path, vol, tf, R=48, passes=2, ext=16.0, change_event=True)
+    assert used == 4
+    want_ph, _ = oracle_replay(vol, tf, 48, seeds, 2, 16.0, change_event=True)
+    assert same(ph[:, :34], want_ph[:, :34])
+    assert (ph[:, 7] == 0).all()  # samples cleared by the reset

@@ -44,8 +44,8 @@ __device__ __forceinline__ float smax(float a, float b) {
 // tests/test_gpu_fastmath.py (exhaustive, on the GPU, through
 // vptmcm_debug_verify). Inputs outside the proven-exact ranges take the
 // default IEEE path.
-__device__ __noinline__ float rcp_slow(float x) { return 1.0f / x; }
-__device__ __noinline__ float sqrt_slow(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ float rcp_slow(float x) { return 1.0f / x; }
+__device__ __forceinline__ float sqrt_slow(float x) { return __builtin_sqrtf(x); }
 
 // RN(1/x): v_rcp_f32 + one Newton step is exact for biased exponent 1..252.
 __device__ __forceinline__ float rcp_cr(float x) {

@@ -1,0 +1,19 @@
+'use strict';
+// Public JS surface of the MI355X spectral MCM renderer.
+const { MCMSpectralComputeRenderer, native } = require('./MCMSpectralComputeRenderer');
+const { RendererFactory } = require('./RendererFactory');
+const { Camera, Transform, PerspectiveCamera, mvpInverse } = require('./Camera');
+const { PropertyBag } = require('./PropertyBag');
+const { BufferLoader, FileLoader, RAWReader, Volume } = require('./readers');
+const spectrum = require('./spectrum');
+const mat4 = require('./mat4');
+
+// A HIP device descriptor in place of the reference's GPUDevice.
+function createDevice(ordinal = 0, layout = 'corner8') {
+  return { ordinal, layout };
+}
+
+module.exports = {
+  MCMSpectralComputeRenderer, RendererFactory, Camera, Transform, PerspectiveCamera, mvpInverse,
+  PropertyBag, BufferLoader, FileLoader, RAWReader, Volume, spectrum, mat4, createDevice, native,
+};
