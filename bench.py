@@ -48,7 +48,11 @@ def parse():
     ap.add_argument("--extinction", type=float, default=32.0)
     ap.add_argument("--layout", choices=["corner8", "linear"], default="corner8")
     ap.add_argument("--tf", choices=["spectral", "grey", "zero"], default="spectral")
-    ap.add_argument("--allreduce-every", type=int, default=1,
+    ap.add_argument("--fuse", type=int, default=16,
+                    help="passes per march launch (render_passes; photon state stays in "
+                         "registers between them, every pass stores its image); 1 = one launch "
+                         "per render() call")
+    ap.add_argument("--allreduce-every", type=int, default=16,
                     help="passes between radiance all-reduces (N > 1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="budget of the CPU-oracle baseline (0 = skip)")
@@ -119,11 +123,27 @@ def main():
             rendezvous.cleanup(key)
 
     seeds = cf.seed_stream(a.warmup + a.steps + 1, start=0, rank=rank)
+    F = max(1, min(a.fuse, 32))
+    every = max(1, a.allreduce_every)
+
+    def passes(first: int, count: int) -> list:
+        """Enqueue `count` passes from seeds[first:] in launches of <= F passes,
+        compositing across ranks whenever `every` passes have completed.
+        Returns the pass count of every march launch."""
+        launches, done = [], 0
+        while done < count:
+            n = min(F, count - done)
+            if multi:  # never fuse across a composite
+                n = min(n, every - (first - 1 + done) % every)
+            r.render_passes(mvp, seeds[first + done:first + done + n])
+            launches.append(n)
+            done += n
+            if multi and (first - 1 + done) % every == 0:
+                r.allreduce_radiance()
+        return launches
+
     r.reset(mvp, seeds[0])
-    for k in range(a.warmup):
-        r.render(mvp, seeds[1 + k])
-        if multi and (k + 1) % a.allreduce_every == 0:
-            r.allreduce_radiance()
+    passes(1, a.warmup)
     r.synchronize()
     if multi:
         r.barrier()
@@ -131,33 +151,37 @@ def main():
     # ---- timed region: K passes (+ composites), bracketed by barrier + sync
     r.enable_kernel_timing(True)
     t0 = time.perf_counter()
-    for k in range(a.steps):
-        r.render(mvp, seeds[1 + a.warmup + k])
-        if multi and (k + 1) % a.allreduce_every == 0:
-            r.allreduce_radiance()
+    launches = passes(1 + a.warmup, a.steps)
     r.synchronize()
     if multi:
         r.read_composite()  # waits for the last all-reduce
     el = time.perf_counter() - t0
     if multi:
         r.barrier()
-    kern_ms, launches = r.kernel_time()
-    vals = np.array([el, kern_ms / max(launches, 1)])
+    kern_ms, n_launch = r.kernel_time()
+    assert n_launch == len(launches), (n_launch, len(launches))
+    vals = np.array([el, kern_ms])
     if multi:
         vals = r.allreduce_host(vals, op="max")
-    el_max, kern_avg_ms = float(vals[0]), float(vals[1])
+    el_max, kern_ms_max = float(vals[0]), float(vals[1])
 
     photon_steps = world * R * R * S * a.steps
     value = photon_steps / el_max / 1e6
-    bytes_per_launch = cf.algorithmic_bytes_per_pass(R, S)
-    achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
+    # roofline of the march kernel: the algorithmic bytes its launches
+    # materialise over their summed duration (= bytes per launch / average
+    # launch duration for equal launches)
+    alg_bytes = sum(cf.algorithmic_bytes_per_launch(R, S, n) for n in launches)
+    achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
+    kern_avg_ms = kern_ms_max / len(launches)
+    bytes_per_launch = alg_bytes // len(launches)
 
     traffic = None
     tp = Path(a.traffic_json)
     if tp.exists():
         try:
             t = json.loads(tp.read_text())
-            if t.get("resolution") == R and t.get("steps") == S and t.get("layout") == a.layout:
+            if (t.get("resolution") == R and t.get("steps") == S and t.get("layout") == a.layout
+                    and t.get("passes_per_launch", 1) == F):
                 traffic = t.get("hbm_bytes_per_launch")
         except (ValueError, OSError):
             traffic = None
@@ -173,15 +197,17 @@ def main():
                             f"(HG g=0.702), R={R}, S={S}, 12 bins, extinction {a.extinction}, "
                             "default camera",
                 "resolution": R, "photon_steps_per_pass": S, "volume": a.volume,
-                "volume_layout": a.layout,
+                "volume_layout": a.layout, "passes_per_launch": F,
                 "parallelism": (f"photon-parallel replicas x{world}, RCCL all-reduce of (rgb*n, n) "
-                                f"every {a.allreduce_every} pass(es)") if multi else "single GPU",
+                                f"every {every} pass(es)") if multi else "single GPU",
             },
             "hbm_gbps_algorithmic": round(achieved, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic,
                          "kernel": "k_march", "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
+                         "passes_per_launch": F,
+                         "kernel_us_per_pass": round(kern_ms_max * 1e3 / a.steps, 3),
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "cpu_baseline": None,
             "volume_gen_s": round(gen_s, 2),

@@ -18,6 +18,7 @@ ALL = (0, 1 << 32)
     (6, "rcp_cr: RN(1/x)", *ALL),
     (7, "sqrt_cr: RN(sqrt x)", *ALL),
     (8, "log_div: RN(f/(2+f)) on m in [sqrt(.5), sqrt(2)]", 0x3F3504F3, 0x3FB504F4 - 0x3F3504F3),
+    (9, "spec_log_unit(h) == spec_log(f32(h) * 2^-32)", *ALL),
 ])
 def test_fast_sequences_are_correctly_rounded(fn, name, lo, n):
     with vptmcm.Renderer(8, device=0) as g:

@@ -256,14 +256,55 @@ def test_composite_single_rank():
 
 
 def test_kernel_timing_counts_launches():
+    """render_passes fuses up to 32 passes per march launch."""
     gpu, _ = make_pair(64, cf.sphere_in_cube(64), cf.tf_spectral())
     mvp = cf.default_mvp_inverse()
     gpu.reset(mvp, 1)
     gpu.enable_kernel_timing(True)
     gpu.render_passes(mvp, cf.seed_stream(5))
+    gpu.render_passes(mvp, cf.seed_stream(40, start=5))
     ms, n = gpu.kernel_time()
-    assert n == 5 and ms > 0
+    assert n == 3 and ms > 0  # 5 | 32 + 8
     gpu.close()
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+@pytest.mark.parametrize("R", [64, 72])
+def test_fused_passes_bitexact(layout, R):
+    """render_passes keeps the photon state in registers across the passes of
+    one launch (32 per launch here: 37 = 32 + 5); photon state and the last
+    pass's image equal the oracle's after the same passes one by one."""
+    gpu, cpu = make_pair(R, cf.two_spheres(48), cf.tf_materials(True), ext=24.0, layout=layout)
+    mvp = cf.golden_mvp("orbit")
+    seeds = cf.seed_stream(38, start=3)
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0])
+    gpu.render_passes(mvp, seeds[1:])
+    for s in seeds[1:]:
+        _, want = cpu.render(mvp, s)
+    assert_photons_equal(gpu.read_photons(), cpu.photons, f"fused R={R}")
+    assert_rgba_equal(gpu.read_rgba16f(), want, f"fused R={R}")
+    gpu.close()
+
+
+def test_schedule_and_fusion_knobs_agree(monkeypatch):
+    """The tile schedule (variant bit 1 = raster mapping) and pass fusion
+    (variant bit 2 = one launch per pass) only change which wave runs a tile and
+    how launches are cut: all four combinations give identical bits."""
+    vol, tf = cf.fbm_volume(64, 9), cf.tf_spectral()
+    mvp = cf.default_mvp_inverse()
+    seeds = cf.seed_stream(12, start=50)
+    out = []
+    for variant in (0, 2, 4, 6):
+        monkeypatch.setenv("VPTMCM_MARCH_VARIANT", str(variant))
+        gpu, _ = make_pair(128, vol, tf, ext=32.0)
+        gpu.reset(mvp, seeds[0])
+        gpu.render_passes(mvp, seeds[1:6])
+        gpu.render_passes(mvp, seeds[6:])
+        out.append((gpu.read_photons(), gpu.read_rgba16f()))
+        gpu.close()
+    for ph, img in out[1:]:
+        assert np.array_equal(ph, out[0][0]) and np.array_equal(img, out[0][1])
 
 
 def test_render_without_volume_fails_loudly():

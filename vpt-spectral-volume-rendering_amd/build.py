@@ -54,15 +54,22 @@ def build_hip(force: bool = False) -> Path:
     return out
 
 
-def build_experiments() -> Path:
-    """Cost-attribution build (knock-out switches via VPTMCM_MARCH_VARIANT bits 1..4);
-    results are NOT valid from this library. Selected with VPTMCM_LIB=exp."""
-    out = LIB / "libvptmcm_exp.so"
+def build_experiments() -> list[Path]:
+    """Cost-attribution builds, selected with VPTMCM_LIB=exp / exp_stamps:
+    libvptmcm_exp.so — knock-out switches (VPTMCM_MARCH_VARIANT bits 8+; they
+    change results) and per-wave records (VPTMCM_WAVE_DUMP=<file>);
+    libvptmcm_exp_stamps.so — additionally s_memtime segment stamps, which
+    serialise the waves and inflate kernel time (shares only)."""
     srcs = [CSRC / "kernels.hip", CSRC / "vptmcm.cpp"]
     hipcc = shutil.which("hipcc") or str(ROCM / "bin" / "hipcc")
-    _run([hipcc, *HIP_FLAGS, "-DVPT_EXPERIMENTS", "-shared", f"-I{REPO / 'include'}", *srcs, "-o",
-          out, "-lrccl", f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}"])
-    return out
+    outs = []
+    for name, defs in (("libvptmcm_exp.so", ["-DVPT_EXPERIMENTS"]),
+                       ("libvptmcm_exp_stamps.so", ["-DVPT_EXPERIMENTS", "-DVPT_STAMPS"])):
+        out = LIB / name
+        _run([hipcc, *HIP_FLAGS, *defs, "-shared", f"-I{REPO / 'include'}", *srcs, "-o", out,
+              "-lrccl", f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}"])
+        outs.append(out)
+    return outs
 
 
 def build_napi(force: bool = False) -> Path | None:

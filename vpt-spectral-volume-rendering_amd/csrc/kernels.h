@@ -2,6 +2,8 @@
 // the C-ABI implementation (vptmcm.cpp).
 #pragma once
 
+#include <cstddef>
+
 #include "march.h"
 
 namespace vpt {
@@ -20,9 +22,37 @@ inline uint32_t march_blocks(const MarchParams& P) { return tile_blocks(P, kBloc
 //   tf_brow u8[256]: anisotropy per row when it does not vary with wavelength
 constexpr uint32_t kTfCells = 257;
 
+// Per-pass tile schedule of the march (see schedule_tile in kernels.hip): one
+// byte per tile, written by the pass ("its wave entered the volume") and read
+// by the next pass to deal volume tiles evenly over the SIMDs.
+struct TileSched {
+  const uint8_t* flags_in;
+  uint8_t* flags_out;
+};
+constexpr uint32_t kSchedChunk = 4 * kMarchBlock;  // tiles scanned per block-wide round
+constexpr uint32_t kSchedMaxTiles = 16384;         // larger frames use the raster mapping
+// Seeds of the passes one march launch runs back to back (render_passes): the
+// photon state stays in registers between them; every pass reseeds the RNG
+// from its own seed (wgsl:122) and stores its full image.
+constexpr uint32_t kMaxFusedPasses = 32;
+struct PassSeeds {
+  uint32_t n;
+  uint32_t seed[kMaxFusedPasses];
+};
+static_assert(offsetof(PassSeeds, seed) == 4, "pass_seed() reads seed[] at kernarg byte 4");
+// k_march(PassSeeds, MarchParams, ...): MarchParams starts right after PassSeeds
+static_assert(sizeof(PassSeeds) % alignof(MarchParams) == 0, "MarchParams kernarg offset");
+static_assert(offsetof(MarchParams, yb) == offsetof(MarchParams, xb) + 4 * kMaxBins &&
+                  offsetof(MarchParams, zb) == offsetof(MarchParams, yb) + 4 * kMaxBins,
+              "cmf_table() reads xb, yb, zb contiguously");
+inline uint32_t sched_flag_bytes(uint32_t n_tiles) {
+  return (n_tiles + kSchedChunk - 1) / kSchedChunk * kSchedChunk;
+}
+
 hipError_t launch_reset(const MarchParams& P, float* ph, hipStream_t s);
 // variant: tuning bits (bit 0 = plain step loop instead of the speculative one)
-hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P, float* ph,
+hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P, const PassSeeds& PS,
+                        const TileSched& T, float* ph,
                         const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba,
                         hipStream_t s);
@@ -32,6 +62,8 @@ hipError_t launch_pack(const MarchParams& P, const float* ph, const uint16_t* rg
                        hipStream_t s);
 // experiment build only: read and clear the per-segment stamp sums (8 counters)
 hipError_t read_stamps(unsigned long long* out8);
+// experiment build only: per-wave records of the last march launch (32 B each)
+hipError_t read_wave_records(void* out, size_t bytes);
 hipError_t launch_verify(int fn, uint32_t lo, uint32_t n, unsigned long long* bad, uint32_t* first,
                          uint32_t nfirst, hipStream_t s);
 hipError_t launch_debug_eval(int fn, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s);

@@ -148,6 +148,33 @@ __device__ __forceinline__ unsigned long long stamp_now() {
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
+// per-wave record of the last launch: HW_ID, XCC_ID, realtime start/end
+// (100 MHz), shader-clock duration, tile, entered flag
+struct WaveRec {
+  uint32_t hwid, xcc, rt0, rt1, cycles, tile, entered, block_wave;
+};
+__device__ WaveRec g_wrec[1 << 16];
+__device__ __forceinline__ unsigned long long realtime_now() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+__device__ __forceinline__ void wave_record(uint32_t tile, bool entered, unsigned long long rt0,
+                                            unsigned long long c0) {
+  unsigned long long rt1 = realtime_now(), c1 = stamp_now();
+  uint32_t hwid, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63u) == 0u) {
+    WaveRec r{hwid, xcc, (uint32_t)rt0, (uint32_t)rt1, (uint32_t)(c1 - c0), tile, entered ? 1u : 0u,
+              blockIdx.x * 16u + w};
+    g_wrec[(blockIdx.x * 16u + w) & 0xffffu] = r;
+  }
+}
+#define WAVE_T0 unsigned long long _rt0 = realtime_now(), _c0 = stamp_now();
+#define WAVE_RECORD(tile, entered) wave_record(tile, entered, _rt0, _c0)
+#ifdef VPT_STAMPS
 #define STAMP_DECL unsigned long long _tp = stamp_now(), _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define STAMP(k)                          \
   do {                                    \
@@ -161,7 +188,20 @@ __device__ __forceinline__ unsigned long long stamp_now() {
       for (int _k = 0; _k < 8; _k++) atomicAdd(&g_stamp[_k], _acc[_k]);     \
   } while (0)
 #else
+#define STAMP_DECL
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#define STAMP_FLUSH() \
+  do {                \
+  } while (0)
+#endif
+#else
 #define KO(bit) 0u
+#define WAVE_T0
+#define WAVE_RECORD(tile, entered) \
+  do {                             \
+  } while (0)
 #define STAMP_DECL
 #define STAMP(k) \
   do {           \
@@ -171,8 +211,146 @@ __device__ __forceinline__ unsigned long long stamp_now() {
   } while (0)
 #endif
 
-template <uint32_t L, bool SPEC>
-__global__ __launch_bounds__(kMarchBlock) void k_march(const MarchParams P, float* __restrict__ ph,
+// sample_light (wgsl:62-73) for a leaving photon; light_dir is pre-normalised
+__device__ __forceinline__ float exit_radiance(const MarchParams& P, f3 dir, const WaveConst& wc) {
+  float rad = wc.intensity;
+  if (!P.light_iso) {
+    float cosl = (dir.x * P.light_dir[0] + dir.y * P.light_dir[1]) + dir.z * P.light_dir[2];
+    rad = smax(cosl * wc.intensity, 0.0f);
+  }
+  return rad;
+}
+
+// PhotonSpectral_add_radiance (wgsl:292-302) with 1/samples precomputed:
+// rad[b] += (target - rad[b]) * inv_n over the first nb bins. NBF (nb >= 12)
+// drops the per-bin guards and pairs the bins into packed f32 operations
+// (v_pk_add/v_pk_mul round each half exactly like the scalar forms).
+template <bool NBF>
+__device__ __forceinline__ void add_radiance(const MarchParams& P, float* rad, float inv_n,
+                                             uint32_t bin, float l) {
+  if constexpr (NBF) {
+    typedef float v2f __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int b = 0; b < kMaxBins; b += 2) {
+      v2f r = {rad[b], rad[b + 1]};
+      v2f t = {((uint32_t)b == bin) ? l : 0.0f, ((uint32_t)b + 1u == bin) ? l : 0.0f};
+      v2f n = {inv_n, inv_n};
+      r = r + (t - r) * n;
+      rad[b] = r.x;
+      rad[b + 1] = r.y;
+    }
+  } else {
+#pragma unroll
+    for (int b = 0; b < kMaxBins; b++) {
+      if ((uint32_t)b < P.nb) {
+        float tgt = ((uint32_t)b == bin) ? l : 0.0f;
+        rad[b] = rad[b] + (tgt - rad[b]) * inv_n;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------- tile schedule
+// With one 1024-thread block per CU and four waves per SIMD, a pass lasts as
+// long as its busiest SIMD. A tile whose rays never enter the volume costs
+// about half of one that does (its waves take the all-exit path), and the two
+// kinds form large screen regions, so the raster mapping can hand one SIMD
+// four volume tiles while another idles. Each pass therefore records, per
+// tile, whether its wave entered the volume, and the next pass orders the
+// tiles as [volume tiles, background tiles] (raster order inside each class,
+// for cache locality) and deals that list over wave slots numbered so that
+// every 4*gridDim.x consecutive slots put one wave on each SIMD of every CU:
+//   slot = k * 4G + lb * 4 + j,  wave w = 4j + ((k + j) & 3)
+// (a Latin square over w: group k holds one wave per SIMD whether the
+// hardware deals a block's waves to SIMDs by w%4 or by w/4; lb is the
+// XCD-swizzled block). The schedule only changes which wave runs a tile,
+// never a photon's arithmetic. All threads of the block must call this.
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane) {
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  return x - v;
+}
+
+__device__ uint32_t schedule_tile(const MarchParams& P, const uint8_t* __restrict__ flags,
+                                  uint32_t* s_red, uint32_t* s_tile) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  const uint32_t n = P.n_tiles, G = gridDim.x;
+  const uint32_t lb = xcd_swizzle(blockIdx.x, G);
+  const uint32_t* f4 = reinterpret_cast<const uint32_t*>(flags);
+  if (tid < 16u) s_tile[tid] = 0xffffffffu;  // idle unless a tile is dealt to it
+  if (tid < 17u) s_red[tid] = 0u;
+  __syncthreads();
+  uint32_t mine = 0u;  // number of volume tiles (flags are 0/1 bytes)
+  for (uint32_t base = 0; base < n; base += kSchedChunk) mine += __popc(f4[(base >> 2) + tid]);
+  mine = wave_sum(mine);
+  if (lane == 0u) atomicAdd(&s_red[16], mine);
+  __syncthreads();
+  const uint32_t nv = s_red[16];
+  uint32_t run = 0u;  // volume tiles before this chunk
+  for (uint32_t base = 0; base < n; base += kSchedChunk) {
+    const uint32_t f = f4[(base >> 2) + tid];
+    const uint32_t c = __popc(f);
+    const uint32_t pre = wave_excl_scan(c, lane);
+    if (lane == 63u) s_red[w] = pre + c;
+    __syncthreads();
+    uint32_t before = run, total = 0u;
+    for (uint32_t k = 0; k < 16u; k++) {
+      uint32_t t = s_red[k];
+      before += (k < w) ? t : 0u;
+      total += t;
+    }
+    uint32_t ones = before + pre;  // volume tiles before tile base + 4*tid
+#pragma unroll
+    for (uint32_t q = 0; q < 4u; q++) {
+      const uint32_t t = base + 4u * tid + q;
+      const uint32_t fl = (f >> (8u * q)) & 1u;
+      if (t < n) {
+        const uint32_t slot = fl ? ones : nv + (t - ones);
+        const uint32_t k = slot / (4u * G), rem = slot - k * 4u * G;
+        if ((rem >> 2) == lb) {
+          const uint32_t j = rem & 3u;
+          s_tile[4u * j + ((k + j) & 3u)] = t;
+        }
+      }
+      ones += fl;
+    }
+    run += total;
+    __syncthreads();  // s_red reused by the next chunk; s_tile complete after the last
+  }
+  return s_tile[w];
+}
+
+// PassSeeds is k_march's first kernel argument: seed[pass] is read straight
+// from the kernarg segment (one scalar load per pass) instead of keeping all
+// kMaxFusedPasses seeds live in SGPRs.
+typedef const __attribute__((address_space(4))) uint32_t* karg_u32;
+__device__ __forceinline__ uint32_t pass_seed(uint32_t pass) {
+  karg_u32 k = (karg_u32)__builtin_amdgcn_kernarg_segment_ptr();
+  return k[1u + pass];  // offsetof(PassSeeds, seed) == 4
+}
+// The CMF bin means of MarchParams (the second kernel argument), re-read from
+// the kernarg segment at every pass's radiance_to_rgb through a pointer the
+// compiler cannot prove invariant, so the 36 values are not hoisted out of the
+// pass loop and kept live in SGPRs across the whole march.
+__device__ __forceinline__ const __attribute__((address_space(4))) float* cmf_table() {
+  karg_u32 k = (karg_u32)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(k));
+  return (const __attribute__((address_space(4))) float*)(k + (sizeof(PassSeeds) +
+                                                               offsetof(MarchParams, xb)) / 4);
+}
+
+template <uint32_t L, bool SPEC, bool NBF>
+__global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const MarchParams P,
+                                                       const TileSched T, float* __restrict__ ph,
                                                        const uint8_t* __restrict__ vol,
                                                        const uint16_t* __restrict__ tf_rg,
                                                        const uint32_t* __restrict__ tf_b4,
@@ -188,11 +366,25 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const MarchParams P, floa
   __shared__ float s_light[256];
   __shared__ float s_brow[256];
 
+  __shared__ uint32_t s_red[17];
+  __shared__ uint32_t s_tile[16];
+
+  WAVE_T0
   STAMP_DECL
-  uint32_t x, y;
-  size_t i;
-  const bool live = tile_pixel<kMarchBlock>(P, x, y, i);
+  uint32_t tile;
+  if (P.sched == 0u) {
+    tile = __builtin_amdgcn_readfirstlane(schedule_tile(P, T.flags_in, s_red, s_tile));
+  } else {  // raster: the block's 16 consecutive tiles
+    tile = xcd_swizzle(blockIdx.x, gridDim.x) * 16u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (tile >= P.n_tiles) tile = 0xffffffffu;
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
+  const uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
+  const size_t i = (size_t)tile * 64u + lane;
+  const bool live = tile != 0xffffffffu && x < P.R && y < P.R;
   const size_t S = P.npad;
+  bool entered = false;  // wave-uniform: some lane of this wave was inside the volume
   Photon p;
   if (live) load_photon(ph, S, i, p);  // issue the state loads before the LDS fill
 
@@ -214,7 +406,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const MarchParams P, floa
   f3 from{0.0f, 0.0f, 0.0f};
   bool fixed = near_fixed(P, sx, sy, from);
   WaveConst wc = wave_const(p.lambda, s_light);
-  uint32_t st = hash3(x, y, P.seed);  // wgsl:122 (state is not carried across passes)
+
+  const uint32_t n_passes = PS.n;
+  for (uint32_t pass = 0; pass < n_passes; pass++) {
+  uint32_t st = hash3(x, y, pass_seed(pass));  // wgsl:122 (state is not carried across passes)
 
   if constexpr (SPEC) {
     // add_radiance of a termination is deferred into the next step's gather
@@ -223,21 +418,27 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const MarchParams P, floa
     uint32_t pend_bin = 0u;
     auto apply_pending = [&]() {
       if (pend_n != 0.0f) {
-        float inv_n = rcp(pend_n);
-#pragma unroll
-        for (int b = 0; b < kMaxBins; b++) {  // PhotonSpectral_add_radiance, wgsl:292-302
-          if ((uint32_t)b < P.nb) {
-            float tgt = ((uint32_t)b == pend_bin) ? pend_l : 0.0f;
-            p.rad[b] = p.rad[b] + (tgt - p.rad[b]) * inv_n;
-          }
-        }
+        add_radiance<NBF>(P, p.rad, rcp(pend_n), pend_bin, pend_l);
         pend_n = 0.0f;
       }
+    };
+    // exit or absorption: count the sample, defer its radiance, adopt the
+    // reset candidate (drawn from h1..h5) and continue from state h5
+    auto terminate = [&](float rad, const Photon& rc) {
+      p.samples++;
+      pend_n = (float)p.samples;
+      pend_l = rad;
+      pend_bin = p.bin;
+      p.pos = rc.pos;
+      p.dir = rc.dir;
+      p.bounces = 0u;
+      p.lambda = rc.lambda;
+      p.bin = rc.bin;
     };
     for (uint32_t step = 0; step < P.steps; step++) {
       // distance + wheel draws (exponential.wgsl, wgsl:124-125, :141)
       uint32_t s1 = pcg_hash(st);
-      float dist = -spec_log((float)s1 * 2.3283064365386963e-10f) * P.rcp_extinction;
+      float dist = -spec_log_unit(s1) * P.rcp_extinction;
       p.pos.x = p.pos.x + dist * p.dir.x;
       p.pos.y = p.pos.y + dist * p.dir.y;
       p.pos.z = p.pos.z + dist * p.dir.z;
@@ -245,7 +446,27 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const MarchParams P, floa
       float wheel = (float)sw * 2.3283064365386963e-10f;
       bool oob = p.pos.x > 1.0f || p.pos.y > 1.0f || p.pos.z > 1.0f || p.pos.x < 0.0f ||
                  p.pos.y < 0.0f || p.pos.z < 0.0f;
-      VolTap vt;
+
+      if (__builtin_amdgcn_ballot_w64(!oob) == 0ull) {
+        // Every lane of the wave leaves the volume this step (background tiles:
+        // ~60% of wave-steps on the benchmark). The volume/TF samples, whose
+        // values are unused on exit (wgsl:142), and the scatter half are skipped.
+        apply_pending();
+        uint32_t h1 = pcg_hash(sw), h2 = pcg_hash(h1), h3 = pcg_hash(h2);
+        uint32_t h4 = pcg_hash(h3), h5 = pcg_hash(h4);
+        float dx = 0.0f, dy = 0.0f;
+        if (!fixed) disk_of(h1, h2, dx, dy);
+        Photon rc;
+        reset_from_draws(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5);
+        terminate(exit_radiance(P, p.dir, wc), rc);
+        wc = wave_const(rc.lambda, s_light);
+        st = h5;
+        STAMP(1);
+        continue;
+      }
+
+      entered = true;
+      VolTap vt{0.0f, 0.0f, 0.0f, 0u, 0u};
       if (KO(1)) {
         vt.fx = vt.fy = vt.fz = 0.5f;
         vt.lo = vt.hi = 0x80808080u;
@@ -261,14 +482,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const MarchParams P, floa
       uint32_t h1 = pcg_hash(sw), h2 = pcg_hash(h1), h3 = pcg_hash(h2);
       uint32_t h4 = pcg_hash(h3), h5 = pcg_hash(h4);
       float dx, dy;
-      {
-        float radius = sqrt_cr((float)h1 * 2.3283064365386963e-10f);
-        float angle = kTwoPi * ((float)h2 * 2.3283064365386963e-10f);
-        float sn, cs;
-        spec_sincos(angle, &sn, &cs);
-        dx = radius * cs;
-        dy = radius * sn;
-      }
+      disk_of(h1, h2, dx, dy);
       Photon rc;
       WaveConst wcr = wc;
       if (KO(3)) {
@@ -317,23 +531,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const MarchParams P, floa
 
       if (oob || wheel < pabs) {
         // exit (wgsl:142-150) or absorption (wgsl:151-155): adopt the candidate
-        float rad = 0.0f;
-        if (oob) {
-          rad = wc.intensity;
-          if (!P.light_iso) {
-            float cosl = (p.dir.x * P.light_dir[0] + p.dir.y * P.light_dir[1]) + p.dir.z * P.light_dir[2];
-            rad = smax(cosl * wc.intensity, 0.0f);
-          }
-        }
-        p.samples++;
-        pend_n = (float)p.samples;
-        pend_l = rad;
-        pend_bin = p.bin;
-        p.pos = rc.pos;
-        p.dir = rc.dir;
-        p.bounces = 0u;
-        p.lambda = rc.lambda;
-        p.bin = rc.bin;
+        terminate(oob ? exit_radiance(P, p.dir, wc) : 0.0f, rc);
         wc = wcr;
         st = h5;
       } else if (wheel < pabs + pscat) {
@@ -370,6 +568,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const MarchParams P, floa
       float wheel = rnd_uniform(st);  // wgsl:141 (drawn before the branch either way)
       bool oob = p.pos.x > 1.0f || p.pos.y > 1.0f || p.pos.z > 1.0f || p.pos.x < 0.0f ||
                  p.pos.y < 0.0f || p.pos.z < 0.0f;
+      entered = entered || __builtin_amdgcn_ballot_w64(!oob) != 0ull;
 
       // sample_volume_color (wgsl:75-80); its value is unused when out of bounds.
       float pabs = 0.0f, pscat = 0.0f, fr = 0.0f;
@@ -391,23 +590,9 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const MarchParams P, floa
 
       if (oob || wheel < pabs) {
         // exit (wgsl:142-150) or absorption (wgsl:151-155)
-        float rad = 0.0f;
-        if (oob) {  // sample_light, wgsl:62-73
-          rad = wc.intensity;
-          if (!P.light_iso) {
-            float cosl = (p.dir.x * P.light_dir[0] + p.dir.y * P.light_dir[1]) + p.dir.z * P.light_dir[2];
-            rad = smax(cosl * wc.intensity, 0.0f);
-          }
-        }
+        float rad = oob ? exit_radiance(P, p.dir, wc) : 0.0f;  // sample_light, wgsl:62-73
         p.samples++;
-        float inv_n = rcp((float)p.samples);
-  #pragma unroll
-        for (int b = 0; b < kMaxBins; b++) {  // PhotonSpectral_add_radiance, wgsl:292-302
-          if ((uint32_t)b < P.nb) {
-            float tgt = ((uint32_t)b == p.bin) ? rad : 0.0f;
-            p.rad[b] = p.rad[b] + (tgt - p.rad[b]) * inv_n;
-          }
-        }
+        add_radiance<NBF>(P, p.rad, rcp((float)p.samples), p.bin, rad);
         photon_reset(P, p, sx, sy, fixed, from, st);
         wc = wave_const(p.lambda, s_light);
       } else if (wheel < pabs + pscat) {
@@ -426,18 +611,17 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const MarchParams P, floa
     }
   }
 
-  store_state(ph, S, i, p);
-#pragma unroll
-  for (int b = 0; b < kMaxBins; b++) ph[(kRad0 + b) * S + i] = p.rad[b];
-
   // PhotonSpectral_radiance_to_rgb (wgsl:304-326) + textureStore (wgsl:168)
   float X = 0.0f, Y = 0.0f, Z = 0.0f;
+  {
+    const auto cmf = cmf_table();  // xb[12], yb[12], zb[12]
 #pragma unroll
-  for (int b = 0; b < kMaxBins; b++) {
-    if ((uint32_t)b < P.nb) {
-      X = X + p.rad[b] * P.xb[b];
-      Y = Y + p.rad[b] * P.yb[b];
-      Z = Z + p.rad[b] * P.zb[b];
+    for (int b = 0; b < kMaxBins; b++) {
+      if ((uint32_t)b < P.nb) {
+        X = X + p.rad[b] * cmf[b];
+        Y = Y + p.rad[b] * cmf[kMaxBins + b];
+        Z = Z + p.rad[b] * cmf[2 * kMaxBins + b];
+      }
     }
   }
   float r = (3.240479f * X - 1.537150f * Y) - 0.498536f * Z;
@@ -447,6 +631,14 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const MarchParams P, floa
   px.x = (uint32_t)f2h(r) | ((uint32_t)f2h(g) << 16);
   px.y = (uint32_t)f2h(bl) | (0x3c00u << 16);
   reinterpret_cast<uint2*>(rgba)[(size_t)y * P.R + x] = px;
+  }  // pass
+
+  store_state(ph, S, i, p);  // uPhotons[globalIndex] = p (wgsl:165), once per launch
+#pragma unroll
+  for (int b = 0; b < kMaxBins; b++) ph[(kRad0 + b) * S + i] = p.rad[b];
+
+  if (lane == 0u) T.flags_out[tile] = entered ? 1u : 0u;  // the next pass's schedule
+  WAVE_RECORD(tile, entered);
   STAMP(6);  // epilogue: state + image stores issued
   STAMP_FLUSH();
 }
@@ -524,15 +716,15 @@ hipError_t launch_reset(const MarchParams& P, float* ph, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P, float* ph,
-                        const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
+hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P, const PassSeeds& PS,
+                        const TileSched& T, float* ph, const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba,
                         hipStream_t s) {
   dim3 grid(tile_blocks(P, kMarchBlock));
 #ifdef VPT_EXPERIMENTS
   {
     static uint32_t last = 0xffffffffu;
-    uint32_t ko = variant & ~1u;
+    uint32_t ko = variant >> 8;  // knock-out bits live above the tuning bits
     if (ko != last) {
       hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_ko), &ko, sizeof ko);
       if (e != hipSuccess) return e;
@@ -541,14 +733,23 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   }
 #endif
   const bool spec = (variant & 1u) == 0u;  // variant bit 0: plain (non-speculative) step
-#define VPT_LAUNCH(LAY, SP)                                                                     \
-  hipLaunchKernelGGL((k_march<LAY, SP>), grid, dim3(kMarchBlock), 0, s, P, ph, vol, tf_rg, tf_b4, \
-                     tf_brow, light, rgba)
+  const bool nbf = P.nb >= (uint32_t)kMaxBins;  // every radiance bin in use
+#define VPT_LAUNCH(LAY, SP, NB)                                                                  \
+  hipLaunchKernelGGL((k_march<LAY, SP, NB>), grid, dim3(kMarchBlock), 0, s, PS, P, T, ph, vol, tf_rg, \
+                     tf_b4, tf_brow, light, rgba)
+#define VPT_LAUNCH_NB(LAY, SP) \
+  do {                         \
+    if (nbf)                   \
+      VPT_LAUNCH(LAY, SP, true); \
+    else                       \
+      VPT_LAUNCH(LAY, SP, false); \
+  } while (0)
   if (layout == kLayoutCorner8) {
-    if (spec) VPT_LAUNCH(kLayoutCorner8, true); else VPT_LAUNCH(kLayoutCorner8, false);
+    if (spec) VPT_LAUNCH_NB(kLayoutCorner8, true); else VPT_LAUNCH_NB(kLayoutCorner8, false);
   } else {
-    if (spec) VPT_LAUNCH(kLayoutLinear, true); else VPT_LAUNCH(kLayoutLinear, false);
+    if (spec) VPT_LAUNCH_NB(kLayoutLinear, true); else VPT_LAUNCH_NB(kLayoutLinear, false);
   }
+#undef VPT_LAUNCH_NB
 #undef VPT_LAUNCH
   return hipGetLastError();
 }
@@ -639,6 +840,11 @@ __device__ __forceinline__ float cand_eval(int fn, float x, float* ref) {
       *ref = f / (2.0f + f);
       return log_div(f);
     }
+    case 9: {  // the march's distance log: spec_log_unit(h) vs spec_log(f32(h) * 2^-32)
+      uint32_t h = __float_as_uint(x);
+      *ref = spec_log((float)h * 2.3283064365386963e-10f);
+      return spec_log_unit(h);
+    }
     case 5: {  // v_sqrt_f32 + one Newton correction using the rsq estimate
       *ref = __builtin_sqrtf(x);
       float s0 = __builtin_amdgcn_sqrtf(x);
@@ -663,6 +869,17 @@ __global__ void k_verify(int fn, uint32_t lo, uint32_t n, unsigned long long* ba
       if (idx < nfirst) first[idx] = lo + k;
     }
   }
+}
+
+hipError_t read_wave_records(void* out, size_t bytes) {
+#ifdef VPT_EXPERIMENTS
+  if (bytes > sizeof(g_wrec)) bytes = sizeof(g_wrec);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wrec), bytes);
+#else
+  (void)out;
+  (void)bytes;
+  return hipErrorNotSupported;
+#endif
 }
 
 hipError_t read_stamps(unsigned long long* out8) {

@@ -50,18 +50,25 @@ struct MarchParams {
   float light_dir[3];    // normalize(light_direction) (host-computed, IEEE)
   uint32_t light_iso;    // length(light_direction) < EPS
   uint32_t b_rows;       // TF blue channel column-invariant: use the LDS row table
+  uint32_t sched;        // march tile mapping: 0 scheduled (TileSched flags), 1 raster
   uint32_t R, tiles_x, n_tiles, npad;
   uint32_t W, H, D;
 };
 
 // ---------------------------------------------------------------- RNG draws
-__device__ __forceinline__ void rnd_disk(uint32_t& st, float& dx, float& dy) {  // disk.wgsl
-  float radius = sqrt_cr(rnd_uniform(st));
-  float angle = kTwoPi * rnd_uniform(st);
+// disk.wgsl from its two hash draws
+__device__ __forceinline__ void disk_of(uint32_t h1, uint32_t h2, float& dx, float& dy) {
+  float radius = sqrt_cr((float)h1 * 2.3283064365386963e-10f);
+  float angle = kTwoPi * ((float)h2 * 2.3283064365386963e-10f);
   float s, c;
   spec_sincos(angle, &s, &c);
   dx = radius * c;
   dy = radius * s;
+}
+__device__ __forceinline__ void rnd_disk(uint32_t& st, float& dx, float& dy) {  // disk.wgsl
+  uint32_t h1 = pcg_hash(st);
+  st = pcg_hash(h1);
+  disk_of(h1, st, dx, dy);
 }
 __device__ __forceinline__ f3 rnd_sphere(uint32_t& st) {  // sphere.wgsl:4-10
   float dx, dy;

@@ -24,17 +24,11 @@ struct f3 { float x, y, z; };
 __device__ __forceinline__ float as_f(uint32_t u) { return __uint_as_float(u); }
 __device__ __forceinline__ uint32_t as_u(float f) { return __float_as_uint(f); }
 
-// IEEE minNum/maxNum with explicit compares; ties keep the first operand.
-__device__ __forceinline__ float smin(float a, float b) {
-  if (a != a) return b;
-  if (b != b) return a;
-  return b < a ? b : a;
-}
-__device__ __forceinline__ float smax(float a, float b) {
-  if (a != a) return b;
-  if (b != b) return a;
-  return b > a ? b : a;
-}
+// IEEE minNum/maxNum with explicit compares; ties keep the first operand:
+// a NaN -> b; b NaN -> a; else (b < a ? b : a). Written as one select so it
+// stays branch-free (the if-chain form compiles to exec-mask branches).
+__device__ __forceinline__ float smin(float a, float b) { return (b < a || a != a) ? b : a; }
+__device__ __forceinline__ float smax(float a, float b) { return (b > a || a != a) ? b : a; }
 
 // ---- correctly rounded reciprocal / sqrt / log division, fast -------------
 // The arithmetic spec needs RN(1/x), RN(sqrt x) and RN(a/b). hipcc's default
@@ -82,17 +76,9 @@ __device__ __forceinline__ float log_div(float f) {
 }
 
 // log(x) = e*ln2 + 2*atanh(s), s = (m-1)/(m+1), m in [sqrt(.5), sqrt(2)).
-__device__ __forceinline__ float spec_log(float x) {
-  uint32_t b = as_u(x);
-  if (!(x > 0.0f)) return (x == 0.0f) ? -__builtin_inff() : __builtin_nanf("");
-  if (b == 0x7f800000u) return x;
-  int e = 0;
-  if (b < 0x00800000u) {
-    x = x * 33554432.0f;
-    b = as_u(x);
-    e = -25;
-  }
-  e += (int)(b >> 23) - 127;
+// Core for a normal positive x given as bit pattern b plus extra exponent e0.
+__device__ __forceinline__ float spec_log_normal(uint32_t b, int e0) {
+  int e = e0 + (int)(b >> 23) - 127;
   float m = as_f((b & 0x007fffffu) | 0x3f800000u);
   if (m > 1.41421353816986083984375f) {
     m = m * 0.5f;
@@ -108,6 +94,27 @@ __device__ __forceinline__ float spec_log(float x) {
   float lm = (s + s) + s * R;
   float ef = (float)e;
   return (ef * 3.194618329871446e-05f + lm) + ef * 0.693115234375f;
+}
+
+__device__ __forceinline__ float spec_log(float x) {
+  uint32_t b = as_u(x);
+  if (!(x > 0.0f)) return (x == 0.0f) ? -__builtin_inff() : __builtin_nanf("");
+  if (b == 0x7f800000u) return x;
+  int e = 0;
+  if (b < 0x00800000u) {
+    x = x * 33554432.0f;
+    b = as_u(x);
+    e = -25;
+  }
+  return spec_log_normal(b, e);
+}
+
+// spec_log(f32(h) * 2^-32): the argument is 0 or a normal number in
+// [2^-32, 1], so the zero/denormal/inf/NaN paths reduce to one select.
+// Equal to spec_log on all 2^32 h (tests/test_gpu_fastmath.py, fn 9).
+__device__ __forceinline__ float spec_log_unit(uint32_t h) {
+  float r = spec_log_normal(as_u((float)h * 2.3283064365386963e-10f), 0);
+  return h == 0u ? -__builtin_inff() : r;
 }
 
 // sin/cos: 3-part Cody-Waite reduction by pi/2, Taylor on |r| <= pi/4.

@@ -48,6 +48,8 @@ struct vptmcm {
   uint8_t* tf_brow = nullptr;  // 256 anisotropy rows (valid when b_rows)
   uint32_t b_rows = 1;         // zero TF: column-invariant
   uint8_t* light = nullptr;    // 256 bytes
+  uint8_t* sched = nullptr;    // tile schedule flags: [2][sched_flag_bytes(n_tiles)]
+  uint32_t sched_cur = 0;      // which flag row the next march reads
 
   float spectrum[VPTMCM_SPECTRUM_FLOATS] = {};
   uint8_t light_host[256];
@@ -164,15 +166,24 @@ int time_begin(vptmcm* h, EventPair** ep) {
   return VPTMCM_OK;
 }
 
-int do_march(vptmcm* h, const float* mvp, uint32_t seed) {
+// One march launch running n <= kMaxFusedPasses passes back to back.
+int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   if (!h->volume_ready) FAIL(h, VPTMCM_ESTATE, "render: no volume set (setVolume first)");
-  MarchParams P = make_params(h, mvp, seed);
+  MarchParams P = make_params(h, mvp, seeds[0]);
+  PassSeeds PS;
+  memset(&PS, 0, sizeof PS);
+  PS.n = n;
+  memcpy(PS.seed, seeds, n * sizeof(uint32_t));
   EventPair* ep = nullptr;
   int rc = time_begin(h, &ep);
   if (rc) return rc;
   const uint8_t* vol = h->layout == kLayoutCorner8 ? (const uint8_t*)h->vol_c8 : h->vol_lin;
-  HIPCHK(h, launch_march(h->layout, h->variant, P, h->photons, vol, h->tf_rg, h->tf_b4, h->tf_brow,
-                         h->light, h->rgba, h->stream));
+  const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
+  TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf};
+  P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : 0u;
+  HIPCHK(h, launch_march(h->layout, h->variant, P, PS, T, h->photons, vol, h->tf_rg, h->tf_b4,
+                         h->tf_brow, h->light, h->rgba, h->stream));
+  h->sched_cur = c ^ 1u;
   if (ep) HIPCHK(h, hipEventRecord(ep->end, h->stream));
   return VPTMCM_OK;
 }
@@ -267,6 +278,8 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   CK(hipMemsetAsync(h->tf_brow, 0, 256, h->stream));
   CK(hipMalloc(&h->light, 256));
   CK(hipMemsetAsync(h->light, 0, 256, h->stream));
+  CK(hipMalloc(&h->sched, 2 * (size_t)sched_flag_bytes(h->n_tiles)));
+  CK(hipMemsetAsync(h->sched, 0, 2 * (size_t)sched_flag_bytes(h->n_tiles), h->stream));
   CK(hipStreamSynchronize(h->stream));
 #undef CK
   *out = h;
@@ -295,6 +308,7 @@ void vptmcm_destroy(vptmcm* h) {
   if (h->tf_b4) (void)hipFree(h->tf_b4);
   if (h->tf_brow) (void)hipFree(h->tf_brow);
   if (h->light) (void)hipFree(h->light);
+  if (h->sched) (void)hipFree(h->sched);
   if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -455,15 +469,16 @@ int vptmcm_render(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (!mvp) FAIL(h, VPTMCM_EINVAL, "render: null matrix");
   HIPCHK(h, hipSetDevice(h->device));
-  return do_march(h, mvp, seed_bits);
+  return do_march(h, mvp, &seed_bits, 1u);
 }
 
 int vptmcm_render_passes(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (!mvp || (!seeds && n)) FAIL(h, VPTMCM_EINVAL, "render_passes: null argument");
   HIPCHK(h, hipSetDevice(h->device));
-  for (uint32_t k = 0; k < n; k++) {
-    int rc = do_march(h, mvp, seeds[k]);
+  const uint32_t fuse = (h->variant & 4u) ? 1u : kMaxFusedPasses;  // variant bit 2: one pass per launch
+  for (uint32_t k = 0; k < n; k += fuse) {
+    int rc = do_march(h, mvp, seeds + k, n - k < fuse ? n - k : fuse);
     if (rc) return rc;
   }
   return VPTMCM_OK;
@@ -574,6 +589,15 @@ int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
     for (int k = 0; k < 7; k++) fprintf(stderr, " %s=%.1f%%", names[k], tot ? 100.0 * st[k] / tot : 0.0);
     fprintf(stderr, " (wave-cycles/launch/wave %.0f)\n",
             h->events_used ? (double)tot / h->events_used / (h->npad / 64) : 0.0);
+  }
+  if (const char* path = getenv("VPTMCM_WAVE_DUMP")) {
+    std::vector<uint8_t> buf((size_t)32 << 16);
+    if (read_wave_records(buf.data(), buf.size()) == hipSuccess) {
+      if (FILE* f = fopen(path, "wb")) {
+        fwrite(buf.data(), 1, buf.size(), f);
+        fclose(f);
+      }
+    }
   }
 #endif
   return VPTMCM_OK;

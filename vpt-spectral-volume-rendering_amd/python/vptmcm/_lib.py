@@ -55,8 +55,8 @@ _lib = None
 
 def lib_path() -> Path:
     # VPTMCM_LIB=exp selects the cost-attribution build (tools only; results invalid)
-    if os.environ.get("VPTMCM_LIB") == "exp":
-        return LIB_DIR / "libvptmcm_exp.so"
+    if os.environ.get("VPTMCM_LIB") in ("exp", "exp_stamps"):
+        return LIB_DIR / f"libvptmcm_{os.environ['VPTMCM_LIB']}.so"
     return LIB_DIR / "libvptmcm.so"
 
 
