@@ -40,8 +40,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200, help="timed passes")
-    ap.add_argument("--warmup", type=int, default=20, help="untimed passes")
+    ap.add_argument("--steps", type=int, default=192, help="timed passes")
+    ap.add_argument("--warmup", type=int, default=16, help="untimed passes")
     ap.add_argument("--resolution", type=int, default=512)
     ap.add_argument("--volume", type=int, default=512)
     ap.add_argument("--photon-steps", type=int, default=8, help="S: steps per pass")
@@ -54,6 +54,9 @@ def parse():
                          "per render() call")
     ap.add_argument("--allreduce-every", type=int, default=16,
                     help="passes between radiance all-reduces (N > 1)")
+    ap.add_argument("--unfused-steps", type=int, default=64,
+                    help="passes of a second timed region at one launch per pass (reported "
+                         "as 'unfused'; 0 = skip; N = 1 only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="budget of the CPU-oracle baseline (0 = skip)")
     ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "pmc_traffic.json"),
@@ -106,7 +109,10 @@ def main():
     spec = cf.spectrum_buffer("12")
     mvp = cf.default_mvp_inverse()
 
-    r = vptmcm.Renderer(R, device=local, layout=layout)
+    # VPTMCM_BENCH_DEVICE pins every rank to one ordinal (rehearsing the N > 1
+    # path on a one-GPU box); the default is one GPU per local rank
+    device = int(os.environ.get("VPTMCM_BENCH_DEVICE", local))
+    r = vptmcm.Renderer(R, device=device, layout=layout)
     r.set_volume(vol)
     r.set_material_tf(tf)
     r.set_light(spd, ldir)
@@ -122,11 +128,12 @@ def main():
         if rank == 0:
             rendezvous.cleanup(key)
 
-    seeds = cf.seed_stream(a.warmup + a.steps + 1, start=0, rank=rank)
+    n_unfused = a.unfused_steps if not multi else 0
+    seeds = cf.seed_stream(a.warmup + a.steps + n_unfused + 1, start=0, rank=rank)
     F = max(1, min(a.fuse, 32))
     every = max(1, a.allreduce_every)
 
-    def passes(first: int, count: int) -> list:
+    def passes(first: int, count: int, F: int = F) -> list:
         """Enqueue `count` passes from seeds[first:] in launches of <= F passes,
         compositing across ranks whenever `every` passes have completed.
         Returns the pass count of every march launch."""
@@ -175,6 +182,26 @@ def main():
     kern_avg_ms = kern_ms_max / len(launches)
     bytes_per_launch = alg_bytes // len(launches)
 
+    # the same workload at one launch per render() call (photon state stored and
+    # reloaded every pass), continuing the pass sequence; N = 1 only
+    unfused = None
+    if n_unfused > 0:
+        r.synchronize()
+        r.enable_kernel_timing(True)  # restart the launch timings
+        t1 = time.perf_counter()
+        ul = passes(1 + a.warmup + a.steps, n_unfused, F=1)
+        r.synchronize()
+        el1 = time.perf_counter() - t1
+        uk_ms, un = r.kernel_time()
+        assert un == len(ul)
+        ub = cf.algorithmic_bytes_per_launch(R, S, 1)
+        ua = ub * un / (uk_ms * 1e-3) / 1e9
+        unfused = {"value": round(R * R * S * n_unfused / el1 / 1e6, 3),
+                   "ms_per_step": round(el1 * 1e3 / n_unfused, 5), "steps": n_unfused,
+                   "kernel_avg_us": round(uk_ms * 1e3 / un, 3),
+                   "achieved": round(ua, 1), "frac": round(ua / HBM_PEAK_GBPS, 4),
+                   "algorithmic_bytes_per_launch": ub}
+
     traffic = None
     tp = Path(a.traffic_json)
     if tp.exists():
@@ -209,6 +236,7 @@ def main():
                          "passes_per_launch": F,
                          "kernel_us_per_pass": round(kern_ms_max * 1e3 / a.steps, 3),
                          "algorithmic_bytes_per_launch": bytes_per_launch},
+            "unfused": unfused,
             "cpu_baseline": None,
             "volume_gen_s": round(gen_s, 2),
         }

@@ -412,6 +412,12 @@ static inline v2 screen_pos(uint32_t x, uint32_t y, const float* inv_res) { /* w
     return s;
 }
 
+/* Analysis hook (tools/march_stats.c): per-step outcome of a photon,
+ * 0 null collision, 1 scatter, 2 absorption, 3 exit. No-op in the oracle. */
+#ifndef ORC_EVENT
+#define ORC_EVENT(x, y, step, kind) ((void)0)
+#endif
+
 /* render compute_main body for one pixel, wgsl:118-168 */
 static void render_pixel(const ctx* c, uint32_t R, uint32_t x, uint32_t y, orc_photon* photons,
                          float* rgb32, uint16_t* rgba16) {
@@ -438,6 +444,7 @@ static void render_pixel(const ctx* c, uint32_t R, uint32_t x, uint32_t y, orc_p
         float wheel = rnd_uniform(&st);
         int oob = p.position[0] > 1.0f || p.position[1] > 1.0f || p.position[2] > 1.0f ||
                   p.position[0] < 0.0f || p.position[1] < 0.0f || p.position[2] < 0.0f;
+        ORC_EVENT(x, y, i, oob ? 3 : wheel < pabs ? 2 : wheel < pabs + pscat ? 1 : 0);
         if (oob) {
             v3 d = {p.direction[0], p.direction[1], p.direction[2]};
             float rad = sample_light(c, d, p.wavelength);

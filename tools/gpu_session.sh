@@ -21,11 +21,11 @@ for s in $STEPS; do
     timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err
     rc=$?; echo "bench rc=$rc" | tee -a $OUT/status.txt; cat $OUT/bench.json; fault $rc && exit $rc ;;
   prof)
-    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 100 --warmup 10 --cpu-seconds 0 ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err")
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 96 --warmup 16 --unfused-steps 0 --cpu-seconds 0 ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err")
     rc=$?; echo "prof rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc ;;
   pmc)
     for c in FETCH_SIZE WRITE_SIZE; do
-      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --pmc $c -d "$GRAFT_REPO_ROOT/$OUT/pmc_$c" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 2 --cpu-seconds 0 ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/$OUT/pmc_$c.json" 2> "$GRAFT_REPO_ROOT/$OUT/pmc_$c.err")
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --pmc $c -d "$GRAFT_REPO_ROOT/$OUT/pmc_$c" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 32 --warmup 16 --unfused-steps 0 --cpu-seconds 0 ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/$OUT/pmc_$c.json" 2> "$GRAFT_REPO_ROOT/$OUT/pmc_$c.err")
       rc=$?; echo "pmc $c rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
     done ;;
   esac

@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Build tuning variants of the HIP library for A/B sweeps on the GPU box.
+
+    python tools/variants.py name1='-DFOO=1' name2='-fno-slp-vectorize' ...
+
+Each variant is lib/libvptmcm_<name>.so, compiled from the same sources as the
+product with the extra flags appended; bench.py / tests select one with
+VPTMCM_LIB=<name> (tools/sweep.sh lines 'VPTMCM_LIB=<name>;<bench args>').
+Variants are experiments only: the product library is always libvptmcm.so.
+"""
+import shlex
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "vpt-spectral-volume-rendering_amd"))
+import build as B  # noqa: E402
+
+
+def one(spec: str) -> Path:
+    name, _, flags = spec.partition("=")
+    out = B.LIB / f"libvptmcm_{name}.so"
+    srcs = [B.CSRC / "kernels.hip", B.CSRC / "vptmcm.cpp"]
+    B._run(["/opt/rocm/bin/hipcc", *B.HIP_FLAGS, *shlex.split(flags), "-shared",
+            f"-I{REPO / 'include'}", *srcs, "-o", out, "-lrccl", f"-L{B.ROCM / 'lib'}",
+            f"-Wl,-rpath,{B.ROCM / 'lib'}"])
+    return out
+
+
+if __name__ == "__main__":
+    B.LIB.mkdir(parents=True, exist_ok=True)
+    with ThreadPoolExecutor(4) as ex:
+        for p in ex.map(one, sys.argv[1:]):
+            print(p)

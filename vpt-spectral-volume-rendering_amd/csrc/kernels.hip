@@ -9,6 +9,13 @@
 //   k_debug_eval  spec-math primitives, for device-vs-oracle parity tests
 #include "kernels.h"
 
+#ifndef VPT_PK_RAD
+#define VPT_PK_RAD 0  // 1: packed (v_pk_*) 12-bin radiance update (measured 5 % slower)
+#endif
+#ifndef VPT_PRIO
+#define VPT_PRIO 1  // s_setprio level of volume waves (0 = off); 11 % faster passes
+#endif
+
 namespace vpt {
 
 // ------------------------------------------------------------- photon I/O
@@ -228,7 +235,13 @@ __device__ __forceinline__ float exit_radiance(const MarchParams& P, f3 dir, con
 template <bool NBF>
 __device__ __forceinline__ void add_radiance(const MarchParams& P, float* rad, float inv_n,
                                              uint32_t bin, float l) {
-  if constexpr (NBF) {
+  if constexpr (NBF && !VPT_PK_RAD) {
+#pragma unroll
+    for (int b = 0; b < kMaxBins; b++) {
+      float tgt = ((uint32_t)b == bin) ? l : 0.0f;
+      rad[b] = rad[b] + (tgt - rad[b]) * inv_n;
+    }
+  } else if constexpr (NBF) {
     typedef float v2f __attribute__((ext_vector_type(2)));
 #pragma unroll
     for (int b = 0; b < kMaxBins; b += 2) {
@@ -407,8 +420,19 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   bool fixed = near_fixed(P, sx, sy, from);
   WaveConst wc = wave_const(p.lambda, s_light);
 
+#if VPT_PRIO
+  // Waves whose tile entered the volume last pass are the long ones; they win
+  // VALU issue arbitration over background waves, which have slack.
+  bool hot = (P.sched == 0u) ? (T.flags_in[tile] != 0u) : true;
+#endif
   const uint32_t n_passes = PS.n;
   for (uint32_t pass = 0; pass < n_passes; pass++) {
+#if VPT_PRIO
+  if (pass > 0u) hot = entered;
+  if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) __builtin_amdgcn_s_setprio(VPT_PRIO);
+  else __builtin_amdgcn_s_setprio(0);
+  entered = false;
+#endif
   uint32_t st = hash3(x, y, pass_seed(pass));  // wgsl:122 (state is not carried across passes)
 
   if constexpr (SPEC) {

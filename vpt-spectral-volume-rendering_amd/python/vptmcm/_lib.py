@@ -54,9 +54,14 @@ _lib = None
 
 
 def lib_path() -> Path:
-    # VPTMCM_LIB=exp selects the cost-attribution build (tools only; results invalid)
-    if os.environ.get("VPTMCM_LIB") in ("exp", "exp_stamps"):
-        return LIB_DIR / f"libvptmcm_{os.environ['VPTMCM_LIB']}.so"
+    # VPTMCM_LIB=<name> selects lib/libvptmcm_<name>.so: the cost-attribution
+    # builds (exp, exp_stamps; results invalid) and tuning variants built by
+    # tools/variants.py for A/B sweeps (tools only; never the product default)
+    name = os.environ.get("VPTMCM_LIB", "")
+    if name:
+        if not name.replace("_", "").isalnum():
+            raise ValueError(f"VPTMCM_LIB={name!r}: expected an alphanumeric variant name")
+        return LIB_DIR / f"libvptmcm_{name}.so"
     return LIB_DIR / "libvptmcm.so"
 
 
