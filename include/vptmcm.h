@@ -198,7 +198,12 @@ int vptmcm_debug_eval(vptmcm* h, int fn, const uint32_t* in, uint32_t* out, uint
 
 /* Exhaustive device check of a fast arithmetic sequence against the correctly
  * rounded reference over the u32 bit patterns [lo, lo + count) (count <= 2^32):
- * returns the number of mismatches and up to nfirst mismatching inputs. */
+ * returns the number of mismatches and up to nfirst mismatching inputs.
+ * fn 6/7 rcp/sqrt, 8 log division, 9 unit log, 10 rcp_small, 11 sqrt_z,
+ * 12 rcp_in_range (each on its documented domain), 13 the arithmetic bin
+ * search vs the sequential one for lambda(h5) of every h5 on the current
+ * spectrum, 14 (count 1) reports 1 mismatch unless that arithmetic search is
+ * selected for the current spectrum. */
 int vptmcm_debug_verify(vptmcm* h, int fn, uint32_t lo, uint64_t count, uint64_t* mismatches,
                         uint32_t* first_bad, uint32_t nfirst);
 

@@ -64,8 +64,9 @@ hipError_t launch_pack(const MarchParams& P, const float* ph, const uint16_t* rg
 hipError_t read_stamps(unsigned long long* out8);
 // experiment build only: per-wave records of the last march launch (32 B each)
 hipError_t read_wave_records(void* out, size_t bytes);
-hipError_t launch_verify(int fn, uint32_t lo, uint32_t n, unsigned long long* bad, uint32_t* first,
-                         uint32_t nfirst, hipStream_t s);
+// fn 13 checks bin_of's arithmetic path against the count on the spectrum in P
+hipError_t launch_verify(int fn, const MarchParams& P, uint32_t lo, uint32_t n,
+                         unsigned long long* bad, uint32_t* first, uint32_t nfirst, hipStream_t s);
 hipError_t launch_debug_eval(int fn, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s);
 
 }  // namespace vpt

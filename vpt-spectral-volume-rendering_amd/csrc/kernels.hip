@@ -12,6 +12,9 @@
 #ifndef VPT_PK_RAD
 #define VPT_PK_RAD 0  // 1: packed (v_pk_*) 12-bin radiance update (measured 5 % slower)
 #endif
+#ifndef VPT_BF_PEND
+#define VPT_BF_PEND 1  // branch-free deferred radiance update
+#endif
 #ifndef VPT_PRIO
 #define VPT_PRIO 1  // s_setprio level of volume waves (0 = off); 11 % faster passes
 #endif
@@ -441,10 +444,28 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     float pend_n = 0.0f, pend_l = 0.0f;
     uint32_t pend_bin = 0u;
     auto apply_pending = [&]() {
+#if VPT_BF_PEND
+      // Branch-free: every lane runs the update and lanes without a pending
+      // sample keep their old bins through one shared select per bin (no
+      // exec-mask split, no phi copies). pend_n is a sample count >= 1, so
+      // the guard-free reciprocal is exact (rcp_in_range).
+      const bool on = pend_n != 0.0f;
+      const float inv = rcp_in_range(on ? pend_n : 1.0f);
+#pragma unroll
+      for (int b = 0; b < kMaxBins; b++) {
+        if (NBF || (uint32_t)b < P.nb) {
+          float tgt = ((uint32_t)b == pend_bin) ? pend_l : 0.0f;
+          float nv = p.rad[b] + (tgt - p.rad[b]) * inv;
+          p.rad[b] = on ? nv : p.rad[b];
+        }
+      }
+      pend_n = 0.0f;
+#else
       if (pend_n != 0.0f) {
         add_radiance<NBF>(P, p.rad, rcp(pend_n), pend_bin, pend_l);
         pend_n = 0.0f;
       }
+#endif
     };
     // exit or absorption: count the sample, defer its radiance, adopt the
     // reset candidate (drawn from h1..h5) and continue from state h5
@@ -869,6 +890,24 @@ __device__ __forceinline__ float cand_eval(int fn, float x, float* ref) {
       *ref = spec_log((float)h * 2.3283064365386963e-10f);
       return spec_log_unit(h);
     }
+    case 10: {  // rcp_small on its domain: every x but biased exponent 253..254 and +-inf
+      *ref = 1.0f / x;
+      uint32_t ex = (__float_as_uint(x) >> 23) & 0xffu;
+      bool out = ex == 253u || ex == 254u || (__float_as_uint(x) & 0x7fffffffu) == 0x7f800000u;
+      return out ? *ref : rcp_small(x);
+    }
+    case 11: {  // sqrt_z on its domain: +-0, NaN, |x| with exponent 32..254 and non-denormal negatives
+      *ref = __builtin_sqrtf(x);
+      uint32_t b = __float_as_uint(x), a = b & 0x7fffffffu;
+      bool in = a == 0u || a > 0x7f800000u || ((b & 0x80000000u) ? a >= 0x00800000u
+                                                                  : ((a >> 23) >= 32u && (a >> 23) <= 254u));
+      return in ? sqrt_z(x) : *ref;
+    }
+    case 12: {  // rcp_in_range on its domain: biased exponent 1..252
+      *ref = 1.0f / x;
+      uint32_t ex = (__float_as_uint(x) >> 23) & 0xffu;
+      return (ex >= 1u && ex <= 252u) ? rcp_in_range(x) : *ref;
+    }
     case 5: {  // v_sqrt_f32 + one Newton correction using the rsq estimate
       *ref = __builtin_sqrtf(x);
       float s0 = __builtin_amdgcn_sqrtf(x);
@@ -882,13 +921,24 @@ __device__ __forceinline__ float cand_eval(int fn, float x, float* ref) {
   }
 }
 
-__global__ void k_verify(int fn, uint32_t lo, uint32_t n, unsigned long long* bad, uint32_t* first,
-                         uint32_t nfirst) {
+__global__ void k_verify(int fn, const MarchParams P, uint32_t lo, uint32_t n,
+                         unsigned long long* bad, uint32_t* first, uint32_t nfirst) {
   uint32_t stride = gridDim.x * blockDim.x;
+  MarchParams Pc = P;  // fn 13: the sequential-count bin search as the reference
+  Pc.bins_uniform = 0u;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
-    float x = __uint_as_float(lo + k), ref;
-    float got = cand_eval(fn, x, &ref);
-    if (!same_bits(got, ref)) {
+    bool ok;
+    if (fn == 14) {  // query: is the arithmetic bin path selected for this spectrum?
+      ok = P.bins_uniform != 0u;
+    } else if (fn == 13) {  // bin_of's arithmetic path vs the count, for lambda of every h5
+      float lambda = ((float)(lo + k) * 2.3283064365386963e-10f) * (P.max_lam - P.min_lam) + P.min_lam;
+      ok = bin_of(P, lambda) == bin_of(Pc, lambda);
+    } else {
+      float x = __uint_as_float(lo + k), ref;
+      float got = cand_eval(fn, x, &ref);
+      ok = same_bits(got, ref);
+    }
+    if (!ok) {
       unsigned long long idx = atomicAdd(bad, 1ull);
       if (idx < nfirst) first[idx] = lo + k;
     }
@@ -918,9 +968,9 @@ hipError_t read_stamps(unsigned long long* out8) {
 #endif
 }
 
-hipError_t launch_verify(int fn, uint32_t lo, uint32_t n, unsigned long long* bad, uint32_t* first,
-                         uint32_t nfirst, hipStream_t s) {
-  hipLaunchKernelGGL(k_verify, dim3(8192), dim3(256), 0, s, fn, lo, n, bad, first, nfirst);
+hipError_t launch_verify(int fn, const MarchParams& P, uint32_t lo, uint32_t n,
+                         unsigned long long* bad, uint32_t* first, uint32_t nfirst, hipStream_t s) {
+  hipLaunchKernelGGL(k_verify, dim3(8192), dim3(256), 0, s, fn, P, lo, n, bad, first, nfirst);
   return hipGetLastError();
 }
 

@@ -44,6 +44,8 @@ struct MarchParams {
   uint32_t steps;
   uint32_t nb;           // u32(spectrum[0] + 0.5)
   uint32_t bins_sorted;  // lam[1..nb-1] non-decreasing: branchless bin search valid
+  uint32_t bins_uniform; // lam[i] == lam[0] + f32(i) * bin_w exactly: arithmetic bin
+  float bin_w, rcp_bin_w;
   float lam[13];         // spectrum[1 .. 13]: bin boundaries
   float min_lam, max_lam; // spectrum[1], spectrum[nb + 1] (wgsl:262-263)
   float xb[kMaxBins], yb[kMaxBins], zb[kMaxBins];  // CMF bin means (0 past nb)
@@ -58,7 +60,7 @@ struct MarchParams {
 // ---------------------------------------------------------------- RNG draws
 // disk.wgsl from its two hash draws
 __device__ __forceinline__ void disk_of(uint32_t h1, uint32_t h2, float& dx, float& dy) {
-  float radius = sqrt_cr((float)h1 * 2.3283064365386963e-10f);
+  float radius = sqrt_z((float)h1 * 2.3283064365386963e-10f);
   float angle = kTwoPi * ((float)h2 * 2.3283064365386963e-10f);
   float s, c;
   spec_sincos(angle, &s, &c);
@@ -74,7 +76,7 @@ __device__ __forceinline__ f3 rnd_sphere(uint32_t& st) {  // sphere.wgsl:4-10
   float dx, dy;
   rnd_disk(st, dx, dy);
   float nrm = dx * dx + dy * dy;
-  float radius = 2.0f * sqrt_cr(1.0f - nrm);
+  float radius = 2.0f * sqrt_z(1.0f - nrm);
   float z = 1.0f - 2.0f * nrm;
   return f3{radius * dx, radius * dy, z};
 }
@@ -84,11 +86,11 @@ __device__ __forceinline__ f3 sample_hg(uint32_t& st, float g, f3 dir) {
   f3 u = rnd_sphere(st);
   if (__builtin_fabsf(g) < kEps) return u;
   float g2 = g * g;
-  float c = (1.0f - g2) * rcp((1.0f - g) + (2.0f * g) * rnd_uniform(st));
-  float hgcos = ((1.0f + g2) - c * c) * rcp(2.0f * g);
+  float c = (1.0f - g2) * rcp_small((1.0f - g) + (2.0f * g) * rnd_uniform(st));
+  float hgcos = ((1.0f + g2) - c * c) * rcp_small(2.0f * g);
   float ud = dot3(u, dir);
   f3 circle = norm3(f3{u.x - ud * dir.x, u.y - ud * dir.y, u.z - ud * dir.z});
-  float sn = sqrt_cr(1.0f - hgcos * hgcos);
+  float sn = sqrt_z(1.0f - hgcos * hgcos);
   return f3{sn * circle.x + hgcos * dir.x, sn * circle.y + hgcos * dir.y,
             sn * circle.z + hgcos * dir.z};
 }
@@ -118,6 +120,20 @@ __device__ __forceinline__ WaveConst wave_const(float lambda, const float* s_lig
 __device__ __forceinline__ uint32_t bin_of(const MarchParams& P, float lambda) {
   if (P.nb == 0u) return 0xffffffffu;  // nb - 1 wraps (first-reset quirk)
   uint32_t bin;
+  if (P.bins_uniform) {
+    // Host-verified: lam[i] == lam0 + f32(i) * w for i <= nb, lam0 > 0,
+    // lam[nb] <= 2 lam0 (so lambda - lam0 is exact). The candidate
+    // floor((lambda - lam0) * RN(1/w)) is within one bin of the count, and
+    // two exact comparisons against the boundaries fix it.
+    float q = (lambda - P.lam[0]) * P.rcp_bin_w;
+    int k = (int)__builtin_floorf(q);
+    k = k < 0 ? 0 : (k > (int)P.nb - 1 ? (int)P.nb - 1 : k);
+    float kf = (float)k;
+    float lo = P.lam[0] + kf * P.bin_w;
+    float hi = P.lam[0] + (kf + 1.0f) * P.bin_w;
+    k = (lambda < lo) ? k - 1 : ((!(lambda < hi) && k + 1 < (int)P.nb) ? k + 1 : k);
+    return (uint32_t)k;
+  }
   if (P.bins_sorted) {
     bin = 0u;
 #pragma unroll
@@ -171,7 +187,7 @@ __device__ __forceinline__ void photon_reset(const MarchParams& P, Photon& p, fl
   f3 dir = norm3(f3{to.x - from.x, to.y - from.y, to.z - from.z});
   p.dir = dir;
   p.bounces = 0u;
-  float rx = rcp(dir.x), ry = rcp(dir.y), rz = rcp(dir.z);
+  float rx = rcp_small(dir.x), ry = rcp_small(dir.y), rz = rcp_small(dir.z);
   float t1x = smin((0.0f - from.x) * rx, (1.0f - from.x) * rx);
   float t1y = smin((0.0f - from.y) * ry, (1.0f - from.y) * ry);
   float t1z = smin((0.0f - from.z) * rz, (1.0f - from.z) * rz);
@@ -194,7 +210,7 @@ __device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p
                     sy + (q1 * 2.0f - 1.0f) * P.inv_res[1], 1.0f);
   f3 dir = norm3(f3{to.x - from.x, to.y - from.y, to.z - from.z});
   p.dir = dir;
-  float rx = rcp(dir.x), ry = rcp(dir.y), rz = rcp(dir.z);
+  float rx = rcp_small(dir.x), ry = rcp_small(dir.y), rz = rcp_small(dir.z);
   float t1x = smin((0.0f - from.x) * rx, (1.0f - from.x) * rx);
   float t1y = smin((0.0f - from.y) * ry, (1.0f - from.y) * ry);
   float t1z = smin((0.0f - from.z) * rz, (1.0f - from.z) * rz);

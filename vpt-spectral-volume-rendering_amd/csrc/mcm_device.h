@@ -51,6 +51,24 @@ __device__ __forceinline__ float rcp_cr(float x) {
   return y;
 }
 
+// RN(1/x) for x known to have biased exponent 1..252 (e.g. a sample count
+// converted to f32): the proven fast path without the range guard.
+__device__ __forceinline__ float rcp_in_range(float x) {
+  float y = __builtin_amdgcn_rcpf(x);
+  float e = __builtin_fmaf(-x, y, 1.0f);
+  return __builtin_fmaf(e, y, y);
+}
+
+// RN(1/x) for finite |x| < 2^126 or NaN (e.g. a unit-vector component or a
+// HG denominator in [0, 2]): the only inputs outside the fast path's proven
+// range are then zero and denormals (and NaN, harmlessly), which one compare
+// with an abs modifier detects (vs the 3-instruction exponent range test).
+__device__ __forceinline__ float rcp_small(float x) {
+  float y = rcp_in_range(x);
+  if (__builtin_expect(!(__builtin_fabsf(x) >= 1.17549435e-38f), 0)) y = rcp_slow(x);
+  return y;
+}
+
 // RN(sqrt x): v_sqrt_f32 + one Newton step (rsq estimate) is exact for
 // positive x with biased exponent 32..254.
 __device__ __forceinline__ float sqrt_cr(float x) {
@@ -61,6 +79,19 @@ __device__ __forceinline__ float sqrt_cr(float x) {
   uint32_t ex = __float_as_uint(x) >> 23;  // sign bit included: negatives excluded
   if (__builtin_expect(ex - 32u > 222u, 0)) s = sqrt_slow(x);
   return s;
+}
+
+// RN(sqrt x) for x that is +-0, NaN, a normal negative, or positive with
+// biased exponent 32..254 (e.g. 1 - y for y in [0, 1] (0 or >= 2^-24 by
+// Sterbenz), or f32(h) * 2^-32 (0 or >= 2^-32)): the fast path is exact there
+// for everything but +-0 (where the Newton step makes 0 * inf), which one
+// select returns as is.
+__device__ __forceinline__ float sqrt_z(float x) {
+  float s = __builtin_amdgcn_sqrtf(x);
+  float e = __builtin_fmaf(-s, s, x);
+  float h = 0.5f * __builtin_amdgcn_rsqf(x);
+  s = __builtin_fmaf(e, h, s);
+  return x == 0.0f ? x : s;
 }
 
 // RN(f / (2 + f)) for f = m - 1, m in [sqrt(.5), sqrt(2)] (spec_log's only

@@ -99,6 +99,8 @@ struct vptmcm {
 
 namespace {
 
+const float kNoMatrix[16] = {};  // for launches that only read the non-camera fields
+
 // Uniform preparation shared by render and reset (wgsl:8-18, js:295-312).
 // Everything derived here is computed in IEEE f32 exactly as the kernel
 // would compute it per lane (host SSE arithmetic, no contraction).
@@ -124,6 +126,23 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
     if (!(s[1 + i] <= s[2 + i])) P.bins_sorted = 0u;  // lam[i] <= lam[i+1], NaN-safe
   P.min_lam = s[1];
   P.max_lam = s[nb + 1];
+  // Equal-width bins (the reference default, 12 x 25 nm from 400 nm) take the
+  // arithmetic bin search of bin_of(); see its comment for the conditions.
+  P.bins_uniform = 0u;
+  if (nb >= 1u && nb <= (uint32_t)kMaxBins && P.bins_sorted) {
+    const float l0 = s[1], w = s[2] - s[1];
+    bool ok = std::isfinite(l0) && std::isfinite(w) && l0 > 0.0f && w > 0.0f &&
+              std::isfinite(s[nb + 1]) && s[nb + 1] <= 2.0f * l0;
+    for (uint32_t i = 0; ok && i <= nb; i++) {
+      volatile float iw = (float)i * w;  // f32 rounding, no contraction
+      if (!(s[1 + i] == l0 + iw)) ok = false;
+    }
+    if (ok) {
+      P.bins_uniform = 1u;
+      P.bin_w = w;
+      P.rcp_bin_w = 1.0f / w;
+    }
+  }
   for (uint32_t i = 0; i < nb && i < (uint32_t)kMaxBins; i++) {
     P.xb[i] = s[2 + nb + i];
     P.yb[i] = s[2 + 2 * nb + i];
@@ -647,7 +666,6 @@ int vptmcm_comm_allreduce_radiance(vptmcm* h) {
   int k = h->comp_next;
   // the buffer must be free of the all-reduce issued two passes ago
   HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[k], 0));
-  static const float kNoMatrix[16] = {};  // k_pack only reads the geometry fields
   MarchParams P = make_params(h, kNoMatrix, 0);
   HIPCHK(h, launch_pack(P, h->photons, h->rgba, h->comp[k], h->stream));
   HIPCHK(h, hipEventRecord(h->comp_ready[k], h->stream));
@@ -734,9 +752,10 @@ int vptmcm_debug_verify(vptmcm* h, int fn, uint32_t lo, uint64_t count, uint64_t
   HIPCHK(h, hipMemsetAsync(dbad, 0, sizeof(unsigned long long), h->stream));
   uint64_t done = 0;
   hipError_t e = hipSuccess;
+  const MarchParams P = make_params(h, kNoMatrix, 0);  // fn 13 uses the current spectrum
   while (done < count && e == hipSuccess) {  // chunks of 2^31 (u32 range)
     uint64_t chunk = count - done < (1ull << 31) ? count - done : (1ull << 31);
-    e = launch_verify(fn, (uint32_t)(lo + done), (uint32_t)chunk, dbad, dfirst, nfirst, h->stream);
+    e = launch_verify(fn, P, (uint32_t)(lo + done), (uint32_t)chunk, dbad, dfirst, nfirst, h->stream);
     done += chunk;
   }
   unsigned long long nb = 0;

@@ -281,6 +281,10 @@ class Renderer:
         return o
 
 
+    def uniform_bins(self) -> bool:
+        """True when the current spectrum takes the arithmetic bin search."""
+        return self.debug_verify(14, 0, 1, 0)[0] == 0
+
     def debug_verify(self, fn: int, lo: int = 0, count: int = 1 << 32, nfirst: int = 16):
         bad = C.c_uint64()
         first = np.zeros(max(nfirst, 1), np.uint32)
