@@ -314,3 +314,45 @@ def test_render_without_volume_fails_loudly():
     with pytest.raises(vptmcm.VptError, match="n_bins"):
         gpu.set_spectrum(np.float32([13.0] + [0] * 63))
     gpu.close()
+
+
+def _poses():
+    import json
+    return list(json.loads((cf.GOLDEN / "mvp_inverse.json").read_text())["cameras"])
+
+
+@pytest.mark.parametrize("camera", _poses())
+def test_fused_full_size_robust_background(camera):
+    """R = 512 with 16 fused passes: background tiles run the robust-miss path
+    (no distance/advance/bounds/slab per step, start point materialised once
+    per launch); photon state and image equal the oracle's pass-by-pass run."""
+    mvp = cf.golden_mvp(camera)
+    gpu, cpu = make_pair(512, cf.fbm_volume(128, 77), cf.tf_spectral(), ext=32.0)
+    seeds = cf.seed_stream(17, start=100)
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0], nthreads=16)
+    gpu.render_passes(mvp, seeds[1:])
+    for s in seeds[1:]:
+        _, want = cpu.render(mvp, s, nthreads=16)
+    assert_photons_equal(gpu.read_photons(), cpu.photons, f"fused R=512 {camera}")
+    assert_rgba_equal(gpu.read_rgba16f(), want, f"fused R=512 {camera}")
+    gpu.close()
+
+
+def test_camera_change_without_reset():
+    """Photons carried into a launch from another camera (no reset between):
+    the robust path only engages after a lane's first reset under the current
+    matrix, so the result still equals the oracle's."""
+    other = [n for n in _poses() if n != "default"]
+    mvps = [cf.default_mvp_inverse(), cf.golden_mvp(other[0])]
+    gpu, cpu = make_pair(256, cf.fbm_volume(64, 5), cf.tf_spectral(), ext=8.0)
+    seeds = cf.seed_stream(13, start=7)
+    gpu.reset(mvps[0], seeds[0])
+    cpu.reset(mvps[0], seeds[0], nthreads=16)
+    gpu.render_passes(mvps[0], seeds[1:7])
+    gpu.render_passes(mvps[-1], seeds[7:])
+    for k, s in enumerate(seeds[1:], 1):
+        _, want = cpu.render(mvps[0] if k < 7 else mvps[-1], s, nthreads=16)
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "camera change")
+    assert_rgba_equal(gpu.read_rgba16f(), want, "camera change")
+    gpu.close()

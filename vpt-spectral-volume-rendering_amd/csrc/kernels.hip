@@ -15,6 +15,9 @@
 #ifndef VPT_BF_PEND
 #define VPT_BF_PEND 1  // branch-free deferred radiance update
 #endif
+#ifndef VPT_ROBUST
+#define VPT_ROBUST 1  // robust-miss background path
+#endif
 #ifndef VPT_PRIO
 #define VPT_PRIO 1  // s_setprio level of volume waves (0 = off); 11 % faster passes
 #endif
@@ -428,6 +431,17 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   // VALU issue arbitration over background waves, which have slack.
   bool hot = (P.sched == 0u) ? (T.flags_in[tile] != 0u) : true;
 #endif
+#if VPT_ROBUST
+  // Robust-miss pixels (MarchParams::robust): once such a lane has been reset
+  // with this launch's matrix its ray misses the cube by a margin, so every
+  // later step of the launch is an exit whatever the distance drawn; a wave
+  // whose lanes are all in that state (background tiles) skips the distance
+  // log, the advance, the bounds test and the ray-start slab test, and
+  // materialises the start point once, at the end of the launch.
+  const bool rbpix = P.robust != 0u && fixed &&
+                     (sx < P.rb_x0 || sx > P.rb_x1 || sy < P.rb_y0 || sy > P.rb_y1);
+  bool rb = false, stale = false;
+#endif
   const uint32_t n_passes = PS.n;
   for (uint32_t pass = 0; pass < n_passes; pass++) {
 #if VPT_PRIO
@@ -479,8 +493,35 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       p.bounces = 0u;
       p.lambda = rc.lambda;
       p.bin = rc.bin;
+#if VPT_ROBUST
+      rb = rbpix;
+#endif
     };
     for (uint32_t step = 0; step < P.steps; step++) {
+#if VPT_ROBUST
+      if (__builtin_amdgcn_ballot_w64(!rb) == 0ull) {
+        // Robust path: the exit of wgsl:142-150 and the reset, minus what a
+        // certain exit does not need (the distance only moves the photon
+        // further along a ray that misses the cube).
+        uint32_t s1 = pcg_hash(st);
+        uint32_t sw = pcg_hash(s1);
+        apply_pending();
+        uint32_t h1 = pcg_hash(sw), h2 = pcg_hash(h1), h3 = pcg_hash(h2);
+        uint32_t h4 = pcg_hash(h3), h5 = pcg_hash(h4);
+        p.samples++;
+        pend_n = (float)p.samples;
+        pend_l = exit_radiance(P, p.dir, wc);
+        pend_bin = p.bin;
+        p.dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
+        p.bounces = 0u;
+        p.lambda = lambda_of(P, h5);
+        p.bin = bin_of(P, p.lambda);
+        wc = wave_const(p.lambda, s_light);
+        st = h5;
+        stale = true;
+        continue;
+      }
+#endif
       // distance + wheel draws (exponential.wgsl, wgsl:124-125, :141)
       uint32_t s1 = pcg_hash(st);
       float dist = -spec_log_unit(s1) * P.rcp_extinction;
@@ -678,6 +719,9 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   reinterpret_cast<uint2*>(rgba)[(size_t)y * P.R + x] = px;
   }  // pass
 
+#if VPT_ROBUST
+  if (stale) p.pos = ray_start(from, p.dir);  // the last robust reset's start point
+#endif
   store_state(ph, S, i, p);  // uPhotons[globalIndex] = p (wgsl:165), once per launch
 #pragma unroll
   for (int b = 0; b < kMaxBins; b++) ph[(kRad0 + b) * S + i] = p.rad[b];

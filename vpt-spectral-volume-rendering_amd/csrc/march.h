@@ -53,6 +53,12 @@ struct MarchParams {
   uint32_t light_iso;    // length(light_direction) < EPS
   uint32_t b_rows;       // TF blue channel column-invariant: use the LDS row table
   uint32_t sched;        // march tile mapping: 0 scheduled (TileSched flags), 1 raster
+  // Robust-miss screen region (NDC, host-derived from the forward matrix):
+  // with blur 0, every ray of a pixel whose centre lies outside
+  // [rb_x0, rb_x1] x [rb_y0, rb_y1] misses the unit cube by a margin, so each
+  // of its steps is an exit (see k_march's robust path).
+  uint32_t robust;
+  float rb_x0, rb_x1, rb_y0, rb_y1;
   uint32_t R, tiles_x, n_tiles, npad;
   uint32_t W, H, D;
 };
@@ -198,27 +204,40 @@ __device__ __forceinline__ void photon_reset(const MarchParams& P, Photon& p, fl
   p.bin = bin_of(P, lambda);
 }
 
-// The same reset computed from pre-drawn hashes: h1,h2 are the disk draws
-// (already turned into dx, dy), h3,h4 the square, h5 the wavelength.
-__device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p, float sx, float sy,
-                                                 bool fixed_from, f3 from, float dx, float dy,
-                                                 uint32_t h3, uint32_t h4, uint32_t h5) {
-  if (!fixed_from) from = unproject(P.m, sx + dx * P.blur, sy + dy * P.blur, -1.0f);
+// The pieces of PhotonSpectral_reset (wgsl:249-266) from pre-drawn hashes:
+// h1,h2 are the disk draws (already turned into dx, dy), h3,h4 the square,
+// h5 the wavelength.
+// Direction of the new camera ray: normalize(far - near) (unprojectRand.wgsl).
+__device__ __forceinline__ f3 ray_dir_from_draws(const MarchParams& P, float sx, float sy, f3 from,
+                                                 uint32_t h3, uint32_t h4) {
   float q0 = (float)h3 * 2.3283064365386963e-10f;
   float q1 = (float)h4 * 2.3283064365386963e-10f;
   f3 to = unproject(P.m, sx + (q0 * 2.0f - 1.0f) * P.inv_res[0],
                     sy + (q1 * 2.0f - 1.0f) * P.inv_res[1], 1.0f);
-  f3 dir = norm3(f3{to.x - from.x, to.y - from.y, to.z - from.z});
-  p.dir = dir;
+  return norm3(f3{to.x - from.x, to.y - from.y, to.z - from.z});
+}
+// Start point on the ray: from + max(tnear, 0) * dir (intersectCube.wgsl, wgsl:254-256).
+__device__ __forceinline__ f3 ray_start(f3 from, f3 dir) {
   float rx = rcp_small(dir.x), ry = rcp_small(dir.y), rz = rcp_small(dir.z);
   float t1x = smin((0.0f - from.x) * rx, (1.0f - from.x) * rx);
   float t1y = smin((0.0f - from.y) * ry, (1.0f - from.y) * ry);
   float t1z = smin((0.0f - from.z) * rz, (1.0f - from.z) * rz);
   float tn = smax(smax(smax(t1x, t1y), t1z), 0.0f);
-  p.pos = f3{from.x + tn * dir.x, from.y + tn * dir.y, from.z + tn * dir.z};
-  float lambda = ((float)h5 * 2.3283064365386963e-10f) * (P.max_lam - P.min_lam) + P.min_lam;
-  p.lambda = lambda;
-  p.bin = bin_of(P, lambda);
+  return f3{from.x + tn * dir.x, from.y + tn * dir.y, from.z + tn * dir.z};
+}
+// Wavelength and bin (PhotonSpectral_set_wavelength, wgsl:276-290).
+__device__ __forceinline__ float lambda_of(const MarchParams& P, uint32_t h5) {
+  return ((float)h5 * 2.3283064365386963e-10f) * (P.max_lam - P.min_lam) + P.min_lam;
+}
+
+__device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p, float sx, float sy,
+                                                 bool fixed_from, f3 from, float dx, float dy,
+                                                 uint32_t h3, uint32_t h4, uint32_t h5) {
+  if (!fixed_from) from = unproject(P.m, sx + dx * P.blur, sy + dy * P.blur, -1.0f);
+  p.dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
+  p.pos = ray_start(from, p.dir);
+  p.lambda = lambda_of(P, h5);
+  p.bin = bin_of(P, p.lambda);
 }
 
 __device__ __forceinline__ void screen_of(const MarchParams& P, uint32_t x, uint32_t y, float& sx,

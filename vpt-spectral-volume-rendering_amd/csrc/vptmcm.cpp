@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/vptmcm.h"
@@ -101,6 +102,79 @@ namespace {
 
 const float kNoMatrix[16] = {};  // for launches that only read the non-camera fields
 
+// Robust-miss region of the march (MarchParams::robust, k_march's robust
+// path). In exact arithmetic a camera ray of pixel (sx, sy) runs from the
+// near point NDC (sx, sy, -1) to the far point (sx', sy', 1) with
+// |sx' - sx|, |sy' - sy| <= invRes, and every point of it beyond the far
+// point has NDC z > 1. So if (a) the projective map is regular on the NDC
+// box (world w > 0 at its 8 corners), (b) the unit cube, expanded by a
+// world-space margin delta that dominates the f32 rounding of the ray, lies
+// in front of the camera with NDC z in (-1, 1), and (c) the pixel's jitter
+// footprint misses the NDC bounding box of that expanded cube, then every
+// computed photon position on the ray is outside [0,1]^3: each step is an
+// exit. Computed in double from the f32 matrix; returns the screen bounds
+// outside of which pixel centres qualify, or false (no robust pixels).
+bool robust_region(const float* m32, float ir, float rb[4]) {
+  double M[16], F[16];
+  for (int i = 0; i < 16; i++) M[i] = m32[i];  // column-major: M[col * 4 + row]
+  auto mul = [](const double* A, double x, double y, double z, double o[4]) {
+    for (int r = 0; r < 4; r++) o[r] = A[r] * x + A[4 + r] * y + A[8 + r] * z + A[12 + r];
+  };
+  double maxnear = 0.0, maxfar = 0.0, o[4];
+  for (int c = 0; c < 8; c++) {
+    mul(M, (c & 1) ? 1.0 : -1.0, (c & 2) ? 1.0 : -1.0, (c & 4) ? 1.0 : -1.0, o);
+    if (!(o[3] > 0.0)) return false;
+    for (int k = 0; k < 3; k++) {
+      double v = std::fabs(o[k] / o[3]);
+      if (!std::isfinite(v)) return false;
+      double& mx = (c & 4) ? maxfar : maxnear;
+      mx = v > mx ? v : mx;
+    }
+  }
+  // F = M^-1 by Gauss-Jordan with partial pivoting (row-major work copy)
+  double A[4][8];
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++) {
+      A[r][c] = M[c * 4 + r];
+      A[r][4 + c] = (r == c) ? 1.0 : 0.0;
+    }
+  for (int c = 0; c < 4; c++) {
+    int piv = c;
+    for (int r = c + 1; r < 4; r++)
+      if (std::fabs(A[r][c]) > std::fabs(A[piv][c])) piv = r;
+    if (!(std::fabs(A[piv][c]) > 1e-300)) return false;
+    for (int k = 0; k < 8; k++) std::swap(A[c][k], A[piv][k]);
+    double d = A[c][c];
+    for (int k = 0; k < 8; k++) A[c][k] /= d;
+    for (int r = 0; r < 4; r++) {
+      if (r == c) continue;
+      double f = A[r][c];
+      for (int k = 0; k < 8; k++) A[r][k] -= f * A[c][k];
+    }
+  }
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++) F[c * 4 + r] = A[r][4 + c];
+  const double delta = 1e-3 * (1.0 + maxnear) + 1e-6 * maxfar;
+  double x0 = 1e300, x1 = -1e300, y0 = 1e300, y1 = -1e300;
+  for (int c = 0; c < 8; c++) {
+    mul(F, (c & 1) ? 1.0 + delta : -delta, (c & 2) ? 1.0 + delta : -delta,
+        (c & 4) ? 1.0 + delta : -delta, o);
+    if (!(o[3] > 0.0)) return false;
+    double nx = o[0] / o[3], ny = o[1] / o[3], nz = o[2] / o[3];
+    if (!(nz > -1.0 + 1e-6 && nz < 1.0 - 1e-6) || !std::isfinite(nx) || !std::isfinite(ny)) return false;
+    x0 = nx < x0 ? nx : x0;
+    x1 = nx > x1 ? nx : x1;
+    y0 = ny < y0 ? ny : y0;
+    y1 = ny > y1 ? ny : y1;
+  }
+  const double pad = (double)ir + 1e-4;
+  rb[0] = std::nextafter((float)(x0 - pad), -INFINITY);
+  rb[1] = std::nextafter((float)(x1 + pad), INFINITY);
+  rb[2] = std::nextafter((float)(y0 - pad), -INFINITY);
+  rb[3] = std::nextafter((float)(y1 + pad), INFINITY);
+  return true;
+}
+
 // Uniform preparation shared by render and reset (wgsl:8-18, js:295-312).
 // Everything derived here is computed in IEEE f32 exactly as the kernel
 // would compute it per lane (host SSE arithmetic, no contraction).
@@ -159,6 +233,15 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
     P.light_dir[2] = ld[2] * il;
   }
   P.b_rows = h->b_rows;
+  float rb[4];
+  P.robust = (P.blur == 0.0f && P.rcp_extinction > 0.0f && std::isfinite(P.rcp_extinction) &&
+              robust_region(mvp, P.inv_res[0], rb)) ? 1u : 0u;
+  if (P.robust) {
+    P.rb_x0 = rb[0];
+    P.rb_x1 = rb[1];
+    P.rb_y0 = rb[2];
+    P.rb_y1 = rb[3];
+  }
   P.R = h->R;
   P.tiles_x = h->tiles_x;
   P.n_tiles = h->n_tiles;
