@@ -15,19 +15,23 @@
  *   - log/sin/cos: WGSL allows 3 ULP / 2^-11 abs error. Here they are
  *     defined as explicit f32 polynomials built only from +,-,*,/ (below),
  *     so CPU and GPU agree to the bit.
- *   - no FMA contraction anywhere (-ffp-contract=off); expressions are
- *     evaluated left to right as written in the WGSL.
+ *   - FMA: WGSL lets implementations fuse a*b + c. Here exactly the
+ *     products listed in DESIGN.md ("Arithmetic specification") are fused,
+ *     written as explicit fmaf() calls (correctly rounded in glibc); nothing
+ *     else is contracted (-ffp-contract=off). Everything else is evaluated
+ *     left to right as written in the WGSL.
  *   - division: WGSL's f32 `/` is only 2.5-ULP accurate; here a / b is
  *     defined as a * rcp(b) with rcp(b) = RN(1/b), the correctly rounded
  *     reciprocal (<= 1.5 ULP), one reciprocal per divisor value.
  *   - min/max: IEEE minNum/maxNum written with explicit compares; ties keep
  *     the first operand.
- *   - normalize(v) = v / sqrt(dot(v,v)); length = sqrt(dot); dot = (x*x+y*y)+z*z.
- *   - mat4 * vec4 = ((c0*v.x + c1*v.y) + c2*v.z) + c3*v.w.
+ *   - normalize(v) = v / sqrt(dot(v,v)); length = sqrt(dot);
+ *     dot = fma(z, z', fma(y, y', x*x')).
+ *   - mat4 * vec4 = fma(c3, v.w, fma(c2, v.z, fma(c1, v.y, c0*v.x))).
  *   - sampler (linear, clamp-to-edge; WebGPUVolume.js:61-64,
  *     WebGPUMCMSpectralComputeRenderer.js:150-169): per axis
- *     x = clampc(u)*N - 0.5, i0 = floor(x), f = x - i0, indices clamped to
- *     [0,N-1]; lerp(a,b,f) = a + f*(b-a) on the raw byte values, x then y
+ *     x = fma(clampc(u), N, -0.5), i0 = floor(x), f = x - i0, indices clamped to
+ *     [0,N-1]; lerp(a,b,f) = fma(f, b-a, a) on the raw byte values, x then y
  *     then z; result * f32(1/255). clampc maps NaN to -1 and limits u to
  *     [-1,2] (outside [0,1] only the clamped edge texel is ever read).
  *   - f32 -> f16 for the rgba16float store: round to nearest even.
@@ -98,31 +102,28 @@ float orc_log(float x) {
     float f = m - 1.0f;
     float s = f / (2.0f + f);
     float z = s * s;
-    float R = z * (0.6666666865348816f +
-                   z * (0.4000000059604645f +
-                        z * (0.2857142984867096f +
-                             z * (0.2222222238779068f + z * 0.1818181872367859f))));
-    float lm = (s + s) + s * R;
+    float P = fmaf(z, fmaf(z, fmaf(z, fmaf(z, 0.1818181872367859f, 0.2222222238779068f),
+                                   0.2857142984867096f), 0.4000000059604645f), 0.6666666865348816f);
+    float R = z * P;
+    float lm = fmaf(s, R, s + s);
     float ef = (float)e;
-    return (ef * 3.194618329871446e-05f + lm) + ef * 0.693115234375f;
+    return fmaf(ef, 0.693115234375f, fmaf(ef, 3.194618329871446e-05f, lm));
 }
 
 /* sin/cos: k = nearest(x * 2/pi); r = x - k*pi/2 (3-part Cody-Waite);
  * Taylor polynomials on |r| <= pi/4; quadrant select. */
 static void spec_sincos(float x, float* so, float* co) {
-    float kf = floorf(x * 0.6366197466850281f + 0.5f);
-    float r = ((x - kf * 1.5703125f) - kf * 0.0004837512969970703f) -
-              kf * 7.549790126404332e-08f;
+    float kf = floorf(fmaf(x, 0.6366197466850281f, 0.5f));
+    float r = fmaf(-kf, 7.549790126404332e-08f,
+                   fmaf(-kf, 0.0004837512969970703f, fmaf(-kf, 1.5703125f, x)));
     float z = r * r;
-    float s = r + r * z * (-0.1666666716337204f +
-                           z * (0.008333333767950535f +
-                                z * (-0.00019841270113829523f +
-                                     z * (2.7557318844628753e-06f +
-                                          z * -2.5052107943679403e-08f))));
-    float c = (1.0f - 0.5f * z) +
-              z * z * (0.0416666679084301f +
-                       z * (-0.0013888889225199819f +
-                            z * (2.4801587642286904e-05f + z * -2.755731998149713e-07f)));
+    float ps = fmaf(z, fmaf(z, fmaf(z, fmaf(z, -2.5052107943679403e-08f, 2.7557318844628753e-06f),
+                                    -0.00019841270113829523f), 0.008333333767950535f),
+                    -0.1666666716337204f);
+    float s = fmaf(r * z, ps, r);
+    float pc = fmaf(z, fmaf(z, fmaf(z, -2.755731998149713e-07f, 2.4801587642286904e-05f),
+                            -0.0013888889225199819f), 0.0416666679084301f);
+    float c = fmaf(z * z, pc, fmaf(-0.5f, z, 1.0f));
     int k = ((int)kf) & 3;
     switch (k) {
         case 0: *so = s; *co = c; break;
@@ -150,7 +151,7 @@ uint16_t orc_f2h(float f) {
     return sign | (uint16_t)h;
 }
 
-static inline float dot3(v3 a, v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+static inline float dot3(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 static inline float len3(v3 a) { return sqrtf(dot3(a, a)); }
 static inline v3 norm3(v3 a) {
     float il = rcp(len3(a));
@@ -198,7 +199,7 @@ static inline v2 rnd_square(uint32_t* st) {
 /* sphere.wgsl:4-10 (Marsaglia) */
 static inline v3 rnd_sphere(uint32_t* st) {
     v2 d = rnd_disk(st);
-    float nrm = d.x * d.x + d.y * d.y;
+    float nrm = fmaf(d.y, d.y, d.x * d.x);
     float radius = 2.0f * sqrtf(1.0f - nrm);
     float z = 1.0f - 2.0f * nrm;
     v3 r = {radius * d.x, radius * d.y, z};
@@ -209,7 +210,7 @@ static inline v3 rnd_sphere(uint32_t* st) {
 
 static inline float clampc(float u) { return u >= -1.0f ? (u <= 2.0f ? u : 2.0f) : -1.0f; }
 static inline void axis(float u, uint32_t n, uint32_t* i0, uint32_t* i1, float* f) {
-    float x = clampc(u) * (float)n - 0.5f;
+    float x = fmaf(clampc(u), (float)n, -0.5f);
     float fl = floorf(x);
     *f = x - fl;
     int i = (int)fl;
@@ -218,7 +219,7 @@ static inline void axis(float u, uint32_t n, uint32_t* i0, uint32_t* i1, float* 
     *i0 = (uint32_t)a;
     *i1 = (uint32_t)b;
 }
-static inline float lerp(float a, float b, float f) { return a + f * (b - a); }
+static inline float lerp(float a, float b, float f) { return fmaf(f, b - a, a); }
 #define INV255 0.003921568859368563f
 
 /* textureSampleLevel(uVolume, linear, clamp-to-edge, p).r — wgsl:76 */
@@ -291,32 +292,31 @@ static v3 sample_hg(uint32_t* st, float g, v3 dir) {
     v3 u = rnd_sphere(st);
     if (fabsf(g) < EPS) return u;
     float g2 = g * g;
-    float c = (1.0f - g2) * rcp((1.0f - g) + (2.0f * g) * rnd_uniform(st));
-    float hgcos = ((1.0f + g2) - c * c) * rcp(2.0f * g);
+    float c = (1.0f - g2) * rcp(fmaf(2.0f * g, rnd_uniform(st), 1.0f - g));
+    float hgcos = fmaf(-c, c, 1.0f + g2) * rcp(2.0f * g);
     float ud = dot3(u, dir);
-    v3 w = {u.x - ud * dir.x, u.y - ud * dir.y, u.z - ud * dir.z};
+    v3 w = {fmaf(-ud, dir.x, u.x), fmaf(-ud, dir.y, u.y), fmaf(-ud, dir.z, u.z)};
     v3 circle = norm3(w);
-    float sn = sqrtf(1.0f - hgcos * hgcos);
-    v3 r = {sn * circle.x + hgcos * dir.x, sn * circle.y + hgcos * dir.y,
-            sn * circle.z + hgcos * dir.z};
+    float sn = sqrtf(fmaf(-hgcos, hgcos, 1.0f));
+    v3 r = {fmaf(sn, circle.x, hgcos * dir.x), fmaf(sn, circle.y, hgcos * dir.y),
+            fmaf(sn, circle.z, hgcos * dir.z)};
     return r;
 }
 
 /* mat4x4f * vec4f, column-major */
 static inline void mat_vec(const float* m, const float v[4], float o[4]) {
     for (int r = 0; r < 4; r++)
-        o[r] = ((m[0 + r] * v[0] + m[4 + r] * v[1]) + m[8 + r] * v[2]) + m[12 + r] * v[3];
+        o[r] = fmaf(m[12 + r], v[3], fmaf(m[8 + r], v[2], fmaf(m[4 + r], v[1], m[0 + r] * v[0])));
 }
 
 /* unprojectRand.wgsl:3-25 */
 static void unproject_rand(uint32_t* st, v2 screen, const float* m, const float* inv_res,
                            float blur, v3* from, v3* to) {
     v2 disk = rnd_disk(st);
-    float nearp[4] = {screen.x + disk.x * blur, screen.y + disk.y * blur, -1.0f, 1.0f};
+    float nearp[4] = {fmaf(disk.x, blur, screen.x), fmaf(disk.y, blur, screen.y), -1.0f, 1.0f};
     v2 sq = rnd_square(st);
-    float aax = (sq.x * 2.0f - 1.0f) * inv_res[0];
-    float aay = (sq.y * 2.0f - 1.0f) * inv_res[1];
-    float farp[4] = {screen.x + aax, screen.y + aay, 1.0f, 1.0f};
+    float farp[4] = {fmaf(fmaf(sq.x, 2.0f, -1.0f), inv_res[0], screen.x),
+                     fmaf(fmaf(sq.y, 2.0f, -1.0f), inv_res[1], screen.y), 1.0f, 1.0f};
     float fd[4], td[4];
     mat_vec(m, nearp, fd);
     mat_vec(m, farp, td);
@@ -363,14 +363,14 @@ static void photon_reset(const ctx* c, orc_photon* p, v2 screen, uint32_t* st) {
     p->direction[0] = dir.x; p->direction[1] = dir.y; p->direction[2] = dir.z;
     p->bounces = 0u;
     float tn = smax(intersect_cube_near(from, dir), 0.0f);
-    p->position[0] = from.x + tn * dir.x;
-    p->position[1] = from.y + tn * dir.y;
-    p->position[2] = from.z + tn * dir.z;
+    p->position[0] = fmaf(tn, dir.x, from.x);
+    p->position[1] = fmaf(tn, dir.y, from.y);
+    p->position[2] = fmaf(tn, dir.z, from.z);
     for (int i = 0; i < MAX_N_BINS; i++) p->transmittance[i] = 1.0f;
     uint32_t nb = n_bins_of(c->spec);
     float min_lam = c->spec[1];
     float max_lam = c->spec[nb + 1];
-    set_wavelength(p, c->spec, rnd_uniform(st) * (max_lam - min_lam) + min_lam);
+    set_wavelength(p, c->spec, fmaf(rnd_uniform(st), max_lam - min_lam, min_lam));
 }
 
 /* PhotonSpectral_full_reset, wgsl:268-274 */
@@ -385,10 +385,8 @@ static void add_radiance(const ctx* c, orc_photon* p, float radiance) {
     uint32_t nb = n_bins_of(c->spec);
     float in = rcp((float)p->samples);
     for (uint32_t i = 0u; i < nb && i < MAX_N_BINS; i++) {
-        if (i == p->bin)
-            p->radiance[i] += (radiance - p->radiance[i]) * in;
-        else
-            p->radiance[i] += (0.0f - p->radiance[i]) * in;
+        float tgt = (i == p->bin) ? radiance : 0.0f;
+        p->radiance[i] = fmaf(tgt - p->radiance[i], in, p->radiance[i]);
     }
 }
 
@@ -397,18 +395,18 @@ static void radiance_to_rgb(const ctx* c, const orc_photon* p, float rgb[3]) {
     uint32_t nb = n_bins_of(c->spec);
     float X = 0.0f, Y = 0.0f, Z = 0.0f;
     for (uint32_t i = 0u; i < nb && i < MAX_N_BINS; i++) {
-        X = X + p->radiance[i] * c->spec[2 + nb + i];
-        Y = Y + p->radiance[i] * c->spec[2 + 2 * nb + i];
-        Z = Z + p->radiance[i] * c->spec[2 + 3 * nb + i];
+        X = fmaf(p->radiance[i], c->spec[2 + nb + i], X);
+        Y = fmaf(p->radiance[i], c->spec[2 + 2 * nb + i], Y);
+        Z = fmaf(p->radiance[i], c->spec[2 + 3 * nb + i], Z);
     }
-    rgb[0] = (3.240479f * X - 1.537150f * Y) - 0.498536f * Z;
-    rgb[1] = (-0.969255f * X + 1.875990f * Y) + 0.041556f * Z;
-    rgb[2] = (0.055647f * X - 0.204041f * Y) + 1.057311f * Z;
+    rgb[0] = fmaf(-0.498536f, Z, fmaf(-1.537150f, Y, 3.240479f * X));
+    rgb[1] = fmaf(0.041556f, Z, fmaf(1.875990f, Y, -0.969255f * X));
+    rgb[2] = fmaf(1.057311f, Z, fmaf(-0.204041f, Y, 0.055647f * X));
 }
 
 static inline v2 screen_pos(uint32_t x, uint32_t y, const float* inv_res) { /* wgsl:118 */
-    v2 s = {(((float)x + 0.5f) * inv_res[0] - 0.5f) * 2.0f,
-            (((float)y + 0.5f) * inv_res[1] - 0.5f) * -2.0f};
+    v2 s = {fmaf((float)x + 0.5f, inv_res[0], -0.5f) * 2.0f,
+            fmaf((float)y + 0.5f, inv_res[1], -0.5f) * -2.0f};
     return s;
 }
 
@@ -427,9 +425,9 @@ static void render_pixel(const ctx* c, uint32_t R, uint32_t x, uint32_t y, orc_p
     uint32_t st = orc_hash3(x, y, u->seed_bits);
     for (uint32_t i = 0u; i < u->steps; i++) {
         float dist = rnd_exponential(&st, u->extinction);
-        p.position[0] = p.position[0] + dist * p.direction[0];
-        p.position[1] = p.position[1] + dist * p.direction[1];
-        p.position[2] = p.position[2] + dist * p.direction[2];
+        p.position[0] = fmaf(dist, p.direction[0], p.position[0]);
+        p.position[1] = fmaf(dist, p.direction[1], p.position[1]);
+        p.position[2] = fmaf(dist, p.direction[2], p.position[2]);
 
         float dens = orc_sample_volume(c->vol, c->W, c->H, c->D, p.position);
         float smp[3];

@@ -3,11 +3,15 @@
 A second, independent restatement (numpy float32 scalars, Python-int u32
 arithmetic), written directly from MCMSpectralComputeRenderer.wgsl and its
 mixins, used only to cross-check the C oracle on small cases (a few pixels).
-It follows the same arithmetic specification: unfused f32 ops in
-WGSL evaluation order, the spec log/sin/cos polynomials, explicit min/max,
-the software linear/clamp sampler.
+It follows the same arithmetic specification: f32 ops in WGSL
+evaluation order with exactly the spec's listed products fused (fma32, an
+exact rational fma rounded once to f32), the spec log/sin/cos polynomials,
+explicit min/max, the software linear/clamp sampler.
 """
 from __future__ import annotations
+
+import math
+from fractions import Fraction
 
 import numpy as np
 
@@ -45,6 +49,23 @@ class Rng:
     def uniform(self):  # uniformdivision.wgsl
         self.s = pcg(self.s)
         return F(self.s) / F(4294967296.0)
+
+
+def fma32(a, b, c):
+    """RN_f32(a*b + c) with a single rounding (exact rational arithmetic,
+    then round-to-odd in double so the final f32 rounding is correct)."""
+    a, b, c = F(a), F(b), F(c)
+    if not (np.isfinite(a) and np.isfinite(b) and np.isfinite(c)):
+        return F(float(a) * float(b) + float(c))
+    x = Fraction(float(a)) * Fraction(float(b)) + Fraction(float(c))
+    if x == 0:
+        # exact zero: the sign follows IEEE rules for the sum of the product and c
+        p = float(a) * float(b)
+        return F(p + float(c))
+    d = float(x)
+    if math.isfinite(d) and Fraction(d) != x and (np.array([d]).view(np.uint64)[0] & 1) == 0:
+        d = float(np.nextafter(d, math.inf if Fraction(d) < x else -math.inf))
+    return F(d)
 
 
 def rcp(x):
@@ -90,28 +111,33 @@ def spec_log(x):
     f = m - F(1)
     s = f / (F(2) + f)
     z = s * s
-    R = z * (F(0.6666666865348816) + z * (F(0.4000000059604645) + z * (
-        F(0.2857142984867096) + z * (F(0.2222222238779068) + z * F(0.1818181872367859)))))
-    lm = (s + s) + s * R
+    P = fma32(z, fma32(z, fma32(z, fma32(z, F(0.1818181872367859), F(0.2222222238779068)),
+                                 F(0.2857142984867096)), F(0.4000000059604645)), F(0.6666666865348816))
+    R = z * P
+    lm = fma32(s, R, s + s)
     ef = F(e)
-    return (ef * F(3.194618329871446e-05) + lm) + ef * F(0.693115234375)
+    return fma32(ef, F(0.693115234375), fma32(ef, F(3.194618329871446e-05), lm))
 
 
 def spec_sincos(x):
     x = F(x)
-    kf = np.floor(x * F(0.6366197466850281) + F(0.5))
-    r = ((x - kf * F(1.5703125)) - kf * F(0.0004837512969970703)) - kf * F(7.549790126404332e-08)
+    kf = np.floor(fma32(x, F(0.6366197466850281), F(0.5)))
+    r = fma32(-kf, F(7.549790126404332e-08),
+              fma32(-kf, F(0.0004837512969970703), fma32(-kf, F(1.5703125), x)))
     z = r * r
-    s = r + r * z * (F(-0.1666666716337204) + z * (F(0.008333333767950535) + z * (
-        F(-0.00019841270113829523) + z * (F(2.7557318844628753e-06) + z * F(-2.5052107943679403e-08)))))
-    c = (F(1) - F(0.5) * z) + z * z * (F(0.0416666679084301) + z * (F(-0.0013888889225199819) + z * (
-        F(2.4801587642286904e-05) + z * F(-2.755731998149713e-07))))
+    ps = fma32(z, fma32(z, fma32(z, fma32(z, F(-2.5052107943679403e-08), F(2.7557318844628753e-06)),
+                                 F(-0.00019841270113829523)), F(0.008333333767950535)),
+               F(-0.1666666716337204))
+    s = fma32(r * z, ps, r)
+    pc = fma32(z, fma32(z, fma32(z, F(-2.755731998149713e-07), F(2.4801587642286904e-05)),
+                        F(-0.0013888889225199819)), F(0.0416666679084301))
+    c = fma32(z * z, pc, fma32(F(-0.5), z, F(1)))
     k = int(kf) & 3
     return [(s, c), (c, -s), (-s, -c), (-c, s)][k]
 
 
 def dot(a, b):
-    return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]
+    return fma32(a[2], b[2], fma32(a[1], b[1], a[0] * b[0]))
 
 
 def normalize(v):
@@ -123,7 +149,7 @@ def axis(u, n):
     u = F(u)
     u = u if u >= F(-1) else F(-1)
     u = u if u <= F(2) else F(2)
-    x = u * F(n) - F(0.5)
+    x = fma32(u, F(n), F(-0.5))
     fl = np.floor(x)
     f = x - fl
     i = int(fl)
@@ -131,7 +157,7 @@ def axis(u, n):
 
 
 def lerp(a, b, f):
-    return a + f * (b - a)
+    return fma32(f, b - a, a)
 
 
 def tex3d(vol, p):
@@ -207,11 +233,13 @@ class Ref:
         return int(v) if v > 0 else 0
 
     def screen(self, x, y):  # wgsl:118
-        return ((F(x) + F(0.5)) * self.inv - F(0.5)) * F(2), ((F(y) + F(0.5)) * self.inv - F(0.5)) * F(-2)
+        return (fma32(F(x) + F(0.5), self.inv, F(-0.5)) * F(2),
+                fma32(F(y) + F(0.5), self.inv, F(-0.5)) * F(-2))
 
     def mat_vec(self, v):
         m = self.m
-        return [((m[r] * v[0] + m[4 + r] * v[1]) + m[8 + r] * v[2]) + m[12 + r] * v[3] for r in range(4)]
+        return [fma32(m[12 + r], v[3], fma32(m[8 + r], v[2], fma32(m[4 + r], v[1], m[r] * v[0])))
+                for r in range(4)]
 
     def disk(self, rng):
         radius = np.sqrt(rng.uniform())
@@ -221,10 +249,10 @@ class Ref:
 
     def reset(self, p, screen, rng):  # PhotonSpectral_reset, wgsl:249-266
         dx, dy = self.disk(rng)
-        nearp = [screen[0] + dx * self.blur, screen[1] + dy * self.blur, F(-1), F(1)]
+        nearp = [fma32(dx, self.blur, screen[0]), fma32(dy, self.blur, screen[1]), F(-1), F(1)]
         sqx, sqy = rng.uniform(), rng.uniform()
-        farp = [screen[0] + (sqx * F(2) - F(1)) * self.inv, screen[1] + (sqy * F(2) - F(1)) * self.inv,
-                F(1), F(1)]
+        farp = [fma32(fma32(sqx, F(2), F(-1)), self.inv, screen[0]),
+                fma32(fma32(sqy, F(2), F(-1)), self.inv, screen[1]), F(1), F(1)]
         fd, td = self.mat_vec(nearp), self.mat_vec(farp)
         iw, jw = rcp(fd[3]), rcp(td[3])
         frm = [fd[0] * iw, fd[1] * iw, fd[2] * iw]
@@ -235,10 +263,10 @@ class Ref:
         rd = [rcp(d[i]) for i in range(3)]
         t1 = [smin((F(0) - frm[i]) * rd[i], (F(1) - frm[i]) * rd[i]) for i in range(3)]
         tn = smax(smax(smax(t1[0], t1[1]), t1[2]), F(0))
-        p.position = [frm[i] + tn * d[i] for i in range(3)]
+        p.position = [fma32(tn, d[i], frm[i]) for i in range(3)]
         nb = self.nb()
         lo, hi = self.spec[1], self.spec[nb + 1]
-        lam = rng.uniform() * (hi - lo) + lo
+        lam = fma32(rng.uniform(), hi - lo, lo)
         p.wavelength = lam
         p.bin = (nb - 1) & M32
         for i in range(1, nb):
@@ -258,14 +286,14 @@ class Ref:
         inv_n = rcp(F(p.samples))
         for i in range(min(self.nb(), 12)):
             tgt = L if i == p.bin else F(0)
-            p.radiance[i] = p.radiance[i] + (tgt - p.radiance[i]) * inv_n
+            p.radiance[i] = fma32(tgt - p.radiance[i], inv_n, p.radiance[i])
 
     def render_pixel(self, p, x, y, seed):
         screen = self.screen(x, y)
         rng = Rng(hash3(x, y, seed))
         for _ in range(self.steps):
             dist = -spec_log(rng.uniform()) * rcp(self.ext)
-            p.position = [p.position[i] + dist * p.direction[i] for i in range(3)]
+            p.position = [fma32(dist, p.direction[i], p.position[i]) for i in range(3)]
             dens = tex3d(self.vol, p.position)
             t = (p.wavelength - F(400)) * rcp(F(700) - F(400))
             albedo, alpha, b = tex2d_tf(self.tf, t, dens)
@@ -295,25 +323,25 @@ class Ref:
         nb = self.nb()
         X = Y = Z = F(0)
         for i in range(min(nb, 12)):
-            X = X + p.radiance[i] * self.spec[2 + nb + i]
-            Y = Y + p.radiance[i] * self.spec[2 + 2 * nb + i]
-            Z = Z + p.radiance[i] * self.spec[2 + 3 * nb + i]
-        rgb = [(F(3.240479) * X - F(1.537150) * Y) - F(0.498536) * Z,
-               (F(-0.969255) * X + F(1.875990) * Y) + F(0.041556) * Z,
-               (F(0.055647) * X - F(0.204041) * Y) + F(1.057311) * Z]
+            X = fma32(p.radiance[i], self.spec[2 + nb + i], X)
+            Y = fma32(p.radiance[i], self.spec[2 + 2 * nb + i], Y)
+            Z = fma32(p.radiance[i], self.spec[2 + 3 * nb + i], Z)
+        rgb = [fma32(F(-0.498536), Z, fma32(F(-1.537150), Y, F(3.240479) * X)),
+               fma32(F(0.041556), Z, fma32(F(1.875990), Y, F(-0.969255) * X)),
+               fma32(F(1.057311), Z, fma32(F(-0.204041), Y, F(0.055647) * X))]
         return rgb
 
     def hg(self, rng, g, d):  # wgsl:82-97
         dx, dy = self.disk(rng)
-        nrm = dx * dx + dy * dy
+        nrm = fma32(dy, dy, dx * dx)
         radius = F(2) * np.sqrt(F(1) - nrm)
         u = [radius * dx, radius * dy, F(1) - F(2) * nrm]
         if abs(g) < EPS:
             return u
         g2 = g * g
-        c = (F(1) - g2) * rcp((F(1) - g) + (F(2) * g) * rng.uniform())
-        cos = ((F(1) + g2) - c * c) * rcp(F(2) * g)
+        c = (F(1) - g2) * rcp(fma32(F(2) * g, rng.uniform(), F(1) - g))
+        cos = fma32(-c, c, F(1) + g2) * rcp(F(2) * g)
         ud = dot(u, d)
-        circle = normalize([u[0] - ud * d[0], u[1] - ud * d[1], u[2] - ud * d[2]])
-        sn = np.sqrt(F(1) - cos * cos)
-        return [sn * circle[i] + cos * d[i] for i in range(3)]
+        circle = normalize([fma32(-ud, d[i], u[i]) for i in range(3)])
+        sn = np.sqrt(fma32(-cos, cos, F(1)))
+        return [fma32(sn, circle[i], cos * d[i]) for i in range(3)]

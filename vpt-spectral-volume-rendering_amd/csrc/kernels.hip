@@ -228,7 +228,7 @@ __device__ __forceinline__ void wave_record(uint32_t tile, bool entered, unsigne
 __device__ __forceinline__ float exit_radiance(const MarchParams& P, f3 dir, const WaveConst& wc) {
   float rad = wc.intensity;
   if (!P.light_iso) {
-    float cosl = (dir.x * P.light_dir[0] + dir.y * P.light_dir[1]) + dir.z * P.light_dir[2];
+    float cosl = fmaf(dir.z, P.light_dir[2], fmaf(dir.y, P.light_dir[1], dir.x * P.light_dir[0]));
     rad = smax(cosl * wc.intensity, 0.0f);
   }
   return rad;
@@ -245,7 +245,7 @@ __device__ __forceinline__ void add_radiance(const MarchParams& P, float* rad, f
 #pragma unroll
     for (int b = 0; b < kMaxBins; b++) {
       float tgt = ((uint32_t)b == bin) ? l : 0.0f;
-      rad[b] = rad[b] + (tgt - rad[b]) * inv_n;
+      rad[b] = fmaf(tgt - rad[b], inv_n, rad[b]);
     }
   } else if constexpr (NBF) {
     typedef float v2f __attribute__((ext_vector_type(2)));
@@ -254,7 +254,7 @@ __device__ __forceinline__ void add_radiance(const MarchParams& P, float* rad, f
       v2f r = {rad[b], rad[b + 1]};
       v2f t = {((uint32_t)b == bin) ? l : 0.0f, ((uint32_t)b + 1u == bin) ? l : 0.0f};
       v2f n = {inv_n, inv_n};
-      r = r + (t - r) * n;
+      r = v2f{fmaf(t.x - r.x, n.x, r.x), fmaf(t.y - r.y, n.y, r.y)};
       rad[b] = r.x;
       rad[b + 1] = r.y;
     }
@@ -263,7 +263,7 @@ __device__ __forceinline__ void add_radiance(const MarchParams& P, float* rad, f
     for (int b = 0; b < kMaxBins; b++) {
       if ((uint32_t)b < P.nb) {
         float tgt = ((uint32_t)b == bin) ? l : 0.0f;
-        rad[b] = rad[b] + (tgt - rad[b]) * inv_n;
+        rad[b] = fmaf(tgt - rad[b], inv_n, rad[b]);
       }
     }
   }
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       for (int b = 0; b < kMaxBins; b++) {
         if (NBF || (uint32_t)b < P.nb) {
           float tgt = ((uint32_t)b == pend_bin) ? pend_l : 0.0f;
-          float nv = p.rad[b] + (tgt - p.rad[b]) * inv;
+          float nv = fmaf(tgt - p.rad[b], inv, p.rad[b]);
           p.rad[b] = on ? nv : p.rad[b];
         }
       }
@@ -525,9 +525,9 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       // distance + wheel draws (exponential.wgsl, wgsl:124-125, :141)
       uint32_t s1 = pcg_hash(st);
       float dist = -spec_log_unit(s1) * P.rcp_extinction;
-      p.pos.x = p.pos.x + dist * p.dir.x;
-      p.pos.y = p.pos.y + dist * p.dir.y;
-      p.pos.z = p.pos.z + dist * p.dir.z;
+      p.pos.x = fmaf(dist, p.dir.x, p.pos.x);
+      p.pos.y = fmaf(dist, p.dir.y, p.pos.y);
+      p.pos.z = fmaf(dist, p.dir.z, p.pos.z);
       uint32_t sw = pcg_hash(s1);
       float wheel = (float)sw * 2.3283064365386963e-10f;
       bool oob = p.pos.x > 1.0f || p.pos.y > 1.0f || p.pos.z > 1.0f || p.pos.x < 0.0f ||
@@ -581,12 +581,13 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         wcr = wave_const(rc.lambda, s_light);
       }
       STAMP(2);  // speculative reset candidate
-      float nrm = dx * dx + dy * dy;  // sphere.wgsl
-      float srad = 2.0f * sqrt_cr(1.0f - nrm);
+      float nrm = fmaf(dy, dy, dx * dx);  // sphere.wgsl
+      float srad = 2.0f * sqrt_z(1.0f - nrm);
       f3 u{srad * dx, srad * dy, 1.0f - 2.0f * nrm};
       float u3 = (float)h3 * 2.3283064365386963e-10f;
       float ud = dot3(u, p.dir);
-      f3 circle = KO(4) ? u : norm3(f3{u.x - ud * p.dir.x, u.y - ud * p.dir.y, u.z - ud * p.dir.z});
+      f3 circle = KO(4) ? u : norm3(f3{fmaf(-ud, p.dir.x, u.x), fmaf(-ud, p.dir.y, u.y),
+                                       fmaf(-ud, p.dir.z, u.z)});
       STAMP(3);  // speculative scatter half
 
       // sample_volume_color (wgsl:75-80) -> probabilities (wgsl:132-139)
@@ -631,11 +632,11 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
           st = h2;
         } else {
           float g2 = g * g;
-          float c = (1.0f - g2) * rcp((1.0f - g) + (2.0f * g) * u3);
-          float hgcos = ((1.0f + g2) - c * c) * rcp(2.0f * g);
-          float sn = sqrt_cr(1.0f - hgcos * hgcos);
-          p.dir = f3{sn * circle.x + hgcos * p.dir.x, sn * circle.y + hgcos * p.dir.y,
-                     sn * circle.z + hgcos * p.dir.z};
+          float c = (1.0f - g2) * rcp_small(fmaf(2.0f * g, u3, 1.0f - g));
+          float hgcos = fmaf(-c, c, 1.0f + g2) * rcp_in_range(2.0f * g);
+          float sn = sqrt_z(fmaf(-hgcos, hgcos, 1.0f));
+          p.dir = f3{fmaf(sn, circle.x, hgcos * p.dir.x), fmaf(sn, circle.y, hgcos * p.dir.y),
+                     fmaf(sn, circle.z, hgcos * p.dir.z)};
           st = h3;
         }
         p.bounces++;
@@ -648,9 +649,9 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   } else {
     for (uint32_t step = 0; step < P.steps; step++) {
       float dist = -spec_log(rnd_uniform(st)) * P.rcp_extinction;  // exponential.wgsl
-      p.pos.x = p.pos.x + dist * p.dir.x;
-      p.pos.y = p.pos.y + dist * p.dir.y;
-      p.pos.z = p.pos.z + dist * p.dir.z;
+      p.pos.x = fmaf(dist, p.dir.x, p.pos.x);
+      p.pos.y = fmaf(dist, p.dir.y, p.pos.y);
+      p.pos.z = fmaf(dist, p.dir.z, p.pos.z);
       float wheel = rnd_uniform(st);  // wgsl:141 (drawn before the branch either way)
       bool oob = p.pos.x > 1.0f || p.pos.y > 1.0f || p.pos.z > 1.0f || p.pos.x < 0.0f ||
                  p.pos.y < 0.0f || p.pos.z < 0.0f;
@@ -704,15 +705,15 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 #pragma unroll
     for (int b = 0; b < kMaxBins; b++) {
       if ((uint32_t)b < P.nb) {
-        X = X + p.rad[b] * cmf[b];
-        Y = Y + p.rad[b] * cmf[kMaxBins + b];
-        Z = Z + p.rad[b] * cmf[2 * kMaxBins + b];
+        X = fmaf(p.rad[b], cmf[b], X);
+        Y = fmaf(p.rad[b], cmf[kMaxBins + b], Y);
+        Z = fmaf(p.rad[b], cmf[2 * kMaxBins + b], Z);
       }
     }
   }
-  float r = (3.240479f * X - 1.537150f * Y) - 0.498536f * Z;
-  float g = (-0.969255f * X + 1.875990f * Y) + 0.041556f * Z;
-  float bl = (0.055647f * X - 0.204041f * Y) + 1.057311f * Z;
+  float r = fmaf(-0.498536f, Z, fmaf(-1.537150f, Y, 3.240479f * X));
+  float g = fmaf(0.041556f, Z, fmaf(1.875990f, Y, -0.969255f * X));
+  float bl = fmaf(1.057311f, Z, fmaf(-0.204041f, Y, 0.055647f * X));
   uint2 px;
   px.x = (uint32_t)f2h(r) | ((uint32_t)f2h(g) << 16);
   px.y = (uint32_t)f2h(bl) | (0x3c00u << 16);
@@ -975,7 +976,7 @@ __global__ void k_verify(int fn, const MarchParams P, uint32_t lo, uint32_t n,
     if (fn == 14) {  // query: is the arithmetic bin path selected for this spectrum?
       ok = P.bins_uniform != 0u;
     } else if (fn == 13) {  // bin_of's arithmetic path vs the count, for lambda of every h5
-      float lambda = ((float)(lo + k) * 2.3283064365386963e-10f) * (P.max_lam - P.min_lam) + P.min_lam;
+      float lambda = fmaf((float)(lo + k) * 2.3283064365386963e-10f, P.max_lam - P.min_lam, P.min_lam);
       ok = bin_of(P, lambda) == bin_of(Pc, lambda);
     } else {
       float x = __uint_as_float(lo + k), ref;

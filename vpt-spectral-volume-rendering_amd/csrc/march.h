@@ -44,7 +44,7 @@ struct MarchParams {
   uint32_t steps;
   uint32_t nb;           // u32(spectrum[0] + 0.5)
   uint32_t bins_sorted;  // lam[1..nb-1] non-decreasing: branchless bin search valid
-  uint32_t bins_uniform; // lam[i] == lam[0] + f32(i) * bin_w exactly: arithmetic bin
+  uint32_t bins_uniform; // lam[i] == fma(f32(i), bin_w, lam[0]) exactly: arithmetic bin
   float bin_w, rcp_bin_w;
   float lam[13];         // spectrum[1 .. 13]: bin boundaries
   float min_lam, max_lam; // spectrum[1], spectrum[nb + 1] (wgsl:262-263)
@@ -81,7 +81,7 @@ __device__ __forceinline__ void rnd_disk(uint32_t& st, float& dx, float& dy) {  
 __device__ __forceinline__ f3 rnd_sphere(uint32_t& st) {  // sphere.wgsl:4-10
   float dx, dy;
   rnd_disk(st, dx, dy);
-  float nrm = dx * dx + dy * dy;
+  float nrm = fmaf(dy, dy, dx * dx);
   float radius = 2.0f * sqrt_z(1.0f - nrm);
   float z = 1.0f - 2.0f * nrm;
   return f3{radius * dx, radius * dy, z};
@@ -92,13 +92,13 @@ __device__ __forceinline__ f3 sample_hg(uint32_t& st, float g, f3 dir) {
   f3 u = rnd_sphere(st);
   if (__builtin_fabsf(g) < kEps) return u;
   float g2 = g * g;
-  float c = (1.0f - g2) * rcp_small((1.0f - g) + (2.0f * g) * rnd_uniform(st));
-  float hgcos = ((1.0f + g2) - c * c) * rcp_small(2.0f * g);
+  float c = (1.0f - g2) * rcp_small(fmaf(2.0f * g, rnd_uniform(st), 1.0f - g));
+  float hgcos = fmaf(-c, c, 1.0f + g2) * rcp_small(2.0f * g);
   float ud = dot3(u, dir);
-  f3 circle = norm3(f3{u.x - ud * dir.x, u.y - ud * dir.y, u.z - ud * dir.z});
-  float sn = sqrt_z(1.0f - hgcos * hgcos);
-  return f3{sn * circle.x + hgcos * dir.x, sn * circle.y + hgcos * dir.y,
-            sn * circle.z + hgcos * dir.z};
+  f3 circle = norm3(f3{fmaf(-ud, dir.x, u.x), fmaf(-ud, dir.y, u.y), fmaf(-ud, dir.z, u.z)});
+  float sn = sqrt_z(fmaf(-hgcos, hgcos, 1.0f));
+  return f3{fmaf(sn, circle.x, hgcos * dir.x), fmaf(sn, circle.y, hgcos * dir.y),
+            fmaf(sn, circle.z, hgcos * dir.z)};
 }
 
 // Per-photon wavelength constants: TF column taps + weight, and the light
@@ -127,7 +127,7 @@ __device__ __forceinline__ uint32_t bin_of(const MarchParams& P, float lambda) {
   if (P.nb == 0u) return 0xffffffffu;  // nb - 1 wraps (first-reset quirk)
   uint32_t bin;
   if (P.bins_uniform) {
-    // Host-verified: lam[i] == lam0 + f32(i) * w for i <= nb, lam0 > 0,
+    // Host-verified: lam[i] == fma(f32(i), w, lam0) for i <= nb, lam0 > 0,
     // lam[nb] <= 2 lam0 (so lambda - lam0 is exact). The candidate
     // floor((lambda - lam0) * RN(1/w)) is within one bin of the count, and
     // two exact comparisons against the boundaries fix it.
@@ -135,8 +135,8 @@ __device__ __forceinline__ uint32_t bin_of(const MarchParams& P, float lambda) {
     int k = (int)__builtin_floorf(q);
     k = k < 0 ? 0 : (k > (int)P.nb - 1 ? (int)P.nb - 1 : k);
     float kf = (float)k;
-    float lo = P.lam[0] + kf * P.bin_w;
-    float hi = P.lam[0] + (kf + 1.0f) * P.bin_w;
+    float lo = fmaf(kf, P.bin_w, P.lam[0]);
+    float hi = fmaf(kf + 1.0f, P.bin_w, P.lam[0]);
     k = (lambda < lo) ? k - 1 : ((!(lambda < hi) && k + 1 < (int)P.nb) ? k + 1 : k);
     return (uint32_t)k;
   }
@@ -168,7 +168,7 @@ struct Photon {
 __device__ __forceinline__ f3 unproject(const float* m, float a, float b, float z) {
   float d[4];
 #pragma unroll
-  for (int r = 0; r < 4; r++) d[r] = ((m[r] * a + m[4 + r] * b) + m[8 + r] * z) + m[12 + r] * 1.0f;
+  for (int r = 0; r < 4; r++) d[r] = fmaf(m[12 + r], 1.0f, fmaf(m[8 + r], z, fmaf(m[4 + r], b, m[r] * a)));
   float iw = rcp(d[3]);
   return f3{d[0] * iw, d[1] * iw, d[2] * iw};
 }
@@ -184,12 +184,12 @@ __device__ __forceinline__ void photon_reset(const MarchParams& P, Photon& p, fl
   } else {
     float dx, dy;
     rnd_disk(st, dx, dy);
-    from = unproject(P.m, sx + dx * P.blur, sy + dy * P.blur, -1.0f);
+    from = unproject(P.m, fmaf(dx, P.blur, sx), fmaf(dy, P.blur, sy), -1.0f);
   }
   float q0 = rnd_uniform(st);
   float q1 = rnd_uniform(st);
-  f3 to = unproject(P.m, sx + (q0 * 2.0f - 1.0f) * P.inv_res[0],
-                    sy + (q1 * 2.0f - 1.0f) * P.inv_res[1], 1.0f);
+  f3 to = unproject(P.m, fmaf(fmaf(q0, 2.0f, -1.0f), P.inv_res[0], sx),
+                    fmaf(fmaf(q1, 2.0f, -1.0f), P.inv_res[1], sy), 1.0f);
   f3 dir = norm3(f3{to.x - from.x, to.y - from.y, to.z - from.z});
   p.dir = dir;
   p.bounces = 0u;
@@ -198,8 +198,8 @@ __device__ __forceinline__ void photon_reset(const MarchParams& P, Photon& p, fl
   float t1y = smin((0.0f - from.y) * ry, (1.0f - from.y) * ry);
   float t1z = smin((0.0f - from.z) * rz, (1.0f - from.z) * rz);
   float tn = smax(smax(smax(t1x, t1y), t1z), 0.0f);
-  p.pos = f3{from.x + tn * dir.x, from.y + tn * dir.y, from.z + tn * dir.z};
-  float lambda = rnd_uniform(st) * (P.max_lam - P.min_lam) + P.min_lam;
+  p.pos = f3{fmaf(tn, dir.x, from.x), fmaf(tn, dir.y, from.y), fmaf(tn, dir.z, from.z)};
+  float lambda = fmaf(rnd_uniform(st), P.max_lam - P.min_lam, P.min_lam);
   p.lambda = lambda;
   p.bin = bin_of(P, lambda);
 }
@@ -212,8 +212,8 @@ __device__ __forceinline__ f3 ray_dir_from_draws(const MarchParams& P, float sx,
                                                  uint32_t h3, uint32_t h4) {
   float q0 = (float)h3 * 2.3283064365386963e-10f;
   float q1 = (float)h4 * 2.3283064365386963e-10f;
-  f3 to = unproject(P.m, sx + (q0 * 2.0f - 1.0f) * P.inv_res[0],
-                    sy + (q1 * 2.0f - 1.0f) * P.inv_res[1], 1.0f);
+  f3 to = unproject(P.m, fmaf(fmaf(q0, 2.0f, -1.0f), P.inv_res[0], sx),
+                    fmaf(fmaf(q1, 2.0f, -1.0f), P.inv_res[1], sy), 1.0f);
   return norm3(f3{to.x - from.x, to.y - from.y, to.z - from.z});
 }
 // Start point on the ray: from + max(tnear, 0) * dir (intersectCube.wgsl, wgsl:254-256).
@@ -223,17 +223,17 @@ __device__ __forceinline__ f3 ray_start(f3 from, f3 dir) {
   float t1y = smin((0.0f - from.y) * ry, (1.0f - from.y) * ry);
   float t1z = smin((0.0f - from.z) * rz, (1.0f - from.z) * rz);
   float tn = smax(smax(smax(t1x, t1y), t1z), 0.0f);
-  return f3{from.x + tn * dir.x, from.y + tn * dir.y, from.z + tn * dir.z};
+  return f3{fmaf(tn, dir.x, from.x), fmaf(tn, dir.y, from.y), fmaf(tn, dir.z, from.z)};
 }
 // Wavelength and bin (PhotonSpectral_set_wavelength, wgsl:276-290).
 __device__ __forceinline__ float lambda_of(const MarchParams& P, uint32_t h5) {
-  return ((float)h5 * 2.3283064365386963e-10f) * (P.max_lam - P.min_lam) + P.min_lam;
+  return fmaf((float)h5 * 2.3283064365386963e-10f, P.max_lam - P.min_lam, P.min_lam);
 }
 
 __device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p, float sx, float sy,
                                                  bool fixed_from, f3 from, float dx, float dy,
                                                  uint32_t h3, uint32_t h4, uint32_t h5) {
-  if (!fixed_from) from = unproject(P.m, sx + dx * P.blur, sy + dy * P.blur, -1.0f);
+  if (!fixed_from) from = unproject(P.m, fmaf(dx, P.blur, sx), fmaf(dy, P.blur, sy), -1.0f);
   p.dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
   p.pos = ray_start(from, p.dir);
   p.lambda = lambda_of(P, h5);
@@ -242,8 +242,8 @@ __device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p
 
 __device__ __forceinline__ void screen_of(const MarchParams& P, uint32_t x, uint32_t y, float& sx,
                                           float& sy) {  // wgsl:118
-  sx = (((float)x + 0.5f) * P.inv_res[0] - 0.5f) * 2.0f;
-  sy = (((float)y + 0.5f) * P.inv_res[1] - 0.5f) * -2.0f;
+  sx = fmaf((float)x + 0.5f, P.inv_res[0], -0.5f) * 2.0f;
+  sy = fmaf((float)y + 0.5f, P.inv_res[1], -0.5f) * -2.0f;
 }
 
 // Consecutive logical blocks -> same XCD (blocks are dealt round-robin over 8).

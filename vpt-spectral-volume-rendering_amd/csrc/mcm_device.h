@@ -2,7 +2,8 @@
 //
 // Implements the arithmetic specification of DESIGN.md ("Arithmetic
 // specification"): the WGSL operations of MCMSpectralComputeRenderer.wgsl with
-// every implementation-defined choice (log/sin/cos, FMA contraction, min/max,
+// every implementation-defined choice (log/sin/cos, which products are fused
+// into FMAs (explicit fmaf below, nothing else contracted), min/max,
 // normalize, mat*vec order, sampler filtering, f16 rounding) fixed, so the
 // kernels agree bit for bit with the CPU oracle. Compiled with
 // -ffp-contract=off; f32 division and sqrt are hipcc's correctly rounded
@@ -118,13 +119,12 @@ __device__ __forceinline__ float spec_log_normal(uint32_t b, int e0) {
   float f = m - 1.0f;
   float s = log_div(f);
   float z = s * s;
-  float R = z * (0.6666666865348816f +
-                 z * (0.4000000059604645f +
-                      z * (0.2857142984867096f +
-                           z * (0.2222222238779068f + z * 0.1818181872367859f))));
-  float lm = (s + s) + s * R;
+  float Pz = fmaf(z, fmaf(z, fmaf(z, fmaf(z, 0.1818181872367859f, 0.2222222238779068f),
+                                  0.2857142984867096f), 0.4000000059604645f), 0.6666666865348816f);
+  float R = z * Pz;
+  float lm = fmaf(s, R, s + s);
   float ef = (float)e;
-  return (ef * 3.194618329871446e-05f + lm) + ef * 0.693115234375f;
+  return fmaf(ef, 0.693115234375f, fmaf(ef, 3.194618329871446e-05f, lm));
 }
 
 __device__ __forceinline__ float spec_log(float x) {
@@ -150,17 +150,17 @@ __device__ __forceinline__ float spec_log_unit(uint32_t h) {
 
 // sin/cos: 3-part Cody-Waite reduction by pi/2, Taylor on |r| <= pi/4.
 __device__ __forceinline__ void spec_sincos(float x, float* so, float* co) {
-  float kf = floorf(x * 0.6366197466850281f + 0.5f);
-  float r = ((x - kf * 1.5703125f) - kf * 0.0004837512969970703f) - kf * 7.549790126404332e-08f;
+  float kf = floorf(fmaf(x, 0.6366197466850281f, 0.5f));
+  float r = fmaf(-kf, 7.549790126404332e-08f,
+                 fmaf(-kf, 0.0004837512969970703f, fmaf(-kf, 1.5703125f, x)));
   float z = r * r;
-  float s = r + r * z * (-0.1666666716337204f +
-                         z * (0.008333333767950535f +
-                              z * (-0.00019841270113829523f +
-                                   z * (2.7557318844628753e-06f + z * -2.5052107943679403e-08f))));
-  float c = (1.0f - 0.5f * z) +
-            z * z * (0.0416666679084301f +
-                     z * (-0.0013888889225199819f +
-                          z * (2.4801587642286904e-05f + z * -2.755731998149713e-07f)));
+  float ps = fmaf(z, fmaf(z, fmaf(z, fmaf(z, -2.5052107943679403e-08f, 2.7557318844628753e-06f),
+                                  -0.00019841270113829523f), 0.008333333767950535f),
+                  -0.1666666716337204f);
+  float s = fmaf(r * z, ps, r);
+  float pc = fmaf(z, fmaf(z, fmaf(z, -2.755731998149713e-07f, 2.4801587642286904e-05f),
+                          -0.0013888889225199819f), 0.0416666679084301f);
+  float c = fmaf(z * z, pc, fmaf(-0.5f, z, 1.0f));
   int k = ((int)kf) & 3;
   float sa = (k & 1) ? c : s;
   float ca = (k & 1) ? s : c;
@@ -188,14 +188,18 @@ __device__ __forceinline__ float rnd_uniform(uint32_t& st) {
 // rcp(b) = RN(1/b), one correctly rounded reciprocal per divisor value.
 __device__ __forceinline__ float rcp(float x) { return rcp_cr(x); }
 
-__device__ __forceinline__ float dot3(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 __device__ __forceinline__ f3 norm3(f3 a) {
   float il = rcp(sqrt_cr(dot3(a, a)));
   return f3{a.x * il, a.y * il, a.z * il};
 }
 
 // float -> half, round to nearest even (v_cvt_f16_f32 under the default mode).
+// The empty asm pins f to a VGPR as an f32 value: without it the backend folds
+// fptrunc(fma(a, b, c)) into v_fma_mix*_f16, which rounds once to f16 instead
+// of f32 then f16 (a tie of the f32 result then rounds differently).
 __device__ __forceinline__ uint16_t f2h(float f) {
+  asm volatile("" : "+v"(f));
   _Float16 h = (_Float16)f;
   return __builtin_bit_cast(uint16_t, h);
 }
@@ -206,12 +210,12 @@ __device__ __forceinline__ float clampc(float u) {
 }
 // texel-space coordinate: x = clampc(u)*N - 0.5; returns floor as int and f.
 __device__ __forceinline__ int axis_floor(float u, float n, float* f) {
-  float x = clampc(u) * n - 0.5f;
+  float x = fmaf(clampc(u), n, -0.5f);
   float fl = floorf(x);
   *f = x - fl;
   return (int)fl;
 }
 __device__ __forceinline__ int clampi(int i, int hi) { return i < 0 ? 0 : (i > hi ? hi : i); }
-__device__ __forceinline__ float lerp(float a, float b, float f) { return a + f * (b - a); }
+__device__ __forceinline__ float lerp(float a, float b, float f) { return fmaf(f, b - a, a); }
 
 }  // namespace vpt

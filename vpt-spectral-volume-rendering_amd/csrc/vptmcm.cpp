@@ -208,8 +208,7 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
     bool ok = std::isfinite(l0) && std::isfinite(w) && l0 > 0.0f && w > 0.0f &&
               std::isfinite(s[nb + 1]) && s[nb + 1] <= 2.0f * l0;
     for (uint32_t i = 0; ok && i <= nb; i++) {
-      volatile float iw = (float)i * w;  // f32 rounding, no contraction
-      if (!(s[1 + i] == l0 + iw)) ok = false;
+      if (!(s[1 + i] == std::fmaf((float)i, w, l0))) ok = false;  // bin_of's boundary formula
     }
     if (ok) {
       P.bins_uniform = 1u;
@@ -223,7 +222,7 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
     P.zb[i] = s[2 + 3 * nb + i];
   }
   const float* ld = h->light_dir;
-  float dd = (ld[0] * ld[0] + ld[1] * ld[1]) + ld[2] * ld[2];
+  float dd = std::fmaf(ld[2], ld[2], std::fmaf(ld[1], ld[1], ld[0] * ld[0]));
   float len = sqrtf(dd);
   P.light_iso = len < kEps ? 1u : 0u;
   if (!P.light_iso) {  // normalize = v * RN(1/length)
