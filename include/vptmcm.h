@@ -158,6 +158,17 @@ int vptmcm_read_photons(vptmcm* h, void* out);
 /* Inverse of read_photons (checkpoint / resume and fixtures). */
 int vptmcm_write_photons(vptmcm* h, const void* in);
 
+/* ---- display ---------------------------------------------------------------- */
+
+/* The artistic tone mapper on the current render target (WebGPUArtisticToneMapper
+ * render(), src/js/tonemappers/WebGPUArtisticToneMapper.js:77-122, shader
+ * src/wgsl/tonemappers/ArtisticToneMapper.wgsl:38-48): rgba16float -> rgba8unorm,
+ * R*R*4 bytes, pixel (x, y) at ((y*R)+x)*4, alpha 255. params = {low, mid, high,
+ * saturation, gamma} (the tone mapper's properties, js:12-48). Runs on the
+ * handle's stream after the enqueued passes; out may be NULL (result kept on
+ * the device), else it is copied out (blocking). */
+int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out);
+
 /* ---- measurement ---------------------------------------------------------- */
 
 /* When enabled, every march launch is bracketed by HIP events on the

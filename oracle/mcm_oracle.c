@@ -266,6 +266,43 @@ float orc_sample_light(const uint8_t* light, float t) {
     return lerp((float)light[c0], (float)light[c1], fx) * INV255;
 }
 
+/* ------------------------------------------------------------ tone mapping */
+
+static double h2d(uint16_t h) { /* IEEE binary16 -> double */
+    int s = h >> 15, e = (h >> 10) & 31, m = h & 1023;
+    double v;
+    if (e == 0) v = ldexp((double)m, -24);
+    else if (e == 31) v = m ? NAN : INFINITY;
+    else v = ldexp((double)(m | 1024), e - 25);
+    return s ? -v : v;
+}
+static uint8_t unorm8d(double v) {
+    if (!(v > 0.0)) return 0;        /* NaN and <= 0 */
+    if (v >= 1.0) return 255;
+    return (uint8_t)floor(v * 255.0 + 0.5);
+}
+/* ArtisticToneMapper.wgsl:38-48: textureSample at the texel centre (exact),
+ * (c - low)/(high - low), mix(dot(c, g) g, c, saturation) with g =
+ * normalize(vec3(1)), pow(c, -log2(midpoint)/gamma), rgba8unorm store. */
+void orc_tonemap_artistic(const uint16_t* rgba16, uint32_t n, const float params[5],
+                          uint8_t* out) {
+    const double low = params[0], mid = params[1], high = params[2];
+    const double sat = params[3], gamma = params[4];
+    const double g = 1.0 / sqrt(3.0);
+    const double e = -log((mid - low) / (high - low)) / log(2.0) / gamma;
+    for (uint32_t i = 0; i < n; i++) {
+        double c[3];
+        for (int k = 0; k < 3; k++) c[k] = (h2d(rgba16[i * 4 + k]) - low) / (high - low);
+        double d = c[0] * g + c[1] * g + c[2] * g;
+        for (int k = 0; k < 3; k++) {
+            double m = d * g + (c[k] - d * g) * sat;
+            double p = (e == 0.0) ? 1.0 : exp2(e * log2(m));
+            out[i * 4 + k] = unorm8d(p);
+        }
+        out[i * 4 + 3] = 255;
+    }
+}
+
 /* ------------------------------------------------------------- kernel body */
 
 typedef struct ctx {

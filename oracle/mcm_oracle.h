@@ -55,6 +55,13 @@ void orc_render(uint32_t R, const orc_uniforms* u, const float* spectrum,
                 orc_photon* photons, float* rgb32, uint16_t* rgba16, int nthreads,
                 uint32_t y0, uint32_t y1);
 
+/* Artistic tone mapper (ArtisticToneMapper.wgsl:38-48) over n rgba16float
+ * pixels -> rgba8 (alpha 255), evaluated in double precision: the checker of
+ * the device's f32 version (tolerance test, see tests/test_gpu_tonemap.py).
+ * params = {low, mid, high, saturation, gamma}. */
+void orc_tonemap_artistic(const uint16_t* rgba16, uint32_t n, const float params[5],
+                          uint8_t* out);
+
 /* Primitives, exported for known-answer and device-parity tests. */
 uint32_t orc_hash(uint32_t v);
 uint32_t orc_hash3(uint32_t x, uint32_t y, uint32_t z);

@@ -53,6 +53,8 @@ def load() -> C.CDLL:
         L.orc_sample_tf.restype = None
         L.orc_sample_light.argtypes = [vp, C.c_float]
         L.orc_sample_light.restype = C.c_float
+        L.orc_tonemap_artistic.argtypes = [vp, C.c_uint32, vp, vp]
+        L.orc_tonemap_artistic.restype = None
         L.orc_eval_batch.argtypes = [C.c_int, vp, vp, C.c_uint32]
         L.orc_eval_batch.restype = None
         _L = L
@@ -116,6 +118,15 @@ class Oracle:
         self.L.orc_render(self.R, C.byref(u), _vp(self.spectrum), _vp(v), W, H, D, _vp(tf),
                           _vp(light), _vp(self.photons), _vp(rgb), _vp(rgba), nthreads, y0, y1)
         return rgb, rgba
+
+    def tonemap_artistic(self, rgba16: np.ndarray, low=0.0, mid=0.5, high=1.0, saturation=1.0,
+                         gamma=2.2) -> np.ndarray:
+        """ArtisticToneMapper.wgsl on an rgba16f image, double precision -> rgba8."""
+        src = np.ascontiguousarray(rgba16, dtype=np.uint16)
+        out = np.zeros(src.shape[:-1] + (4,), np.uint8)
+        p = np.array([low, mid, high, saturation, gamma], np.float32)
+        self.L.orc_tonemap_artistic(_vp(src), src.size // 4, _vp(p), _vp(out))
+        return out
 
     # primitives
     def eval_batch(self, fn: int, inp: np.ndarray) -> np.ndarray:

@@ -40,6 +40,14 @@ const V = require(path.join(ROOT, 'vpt-spectral-volume-rendering_amd', 'js'));
   const tex = renderer.getTexture();
   fs.writeFileSync(path.join(out, 'photons.bin'), Buffer.from(renderer.readPhotons().buffer));
   fs.writeFileSync(path.join(out, 'rgba.bin'), Buffer.from(tex.data.buffer));
+  if (c.tonemap) {                            // WebGPURenderingContext.js:156-188: tone map the target
+    const tm = new (V.ToneMapperFactory('artistic'))(V.createDevice(0), renderer, null,
+      { resolution: c.R });
+    Object.assign(tm, c.tonemap);
+    tm.render();
+    fs.writeFileSync(path.join(out, 'ldr.bin'), Buffer.from(tm.getTexture().buffer));
+    tm.destroy();
+  }
   fs.writeFileSync(path.join(out, 'meta.json'), JSON.stringify({ seeds_used: k }));
   renderer.destroy();
 })().catch(e => { console.error(e.stack); process.exit(1); });

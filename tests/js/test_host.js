@@ -68,7 +68,8 @@ test('addon loads; renderer construction fails loudly without a GPU', () => {
   for (const f of ['create', 'destroy', 'setVolume', 'volumeBegin', 'volumeWriteBlock', 'volumeEnd',
     'setMaterialTF', 'setLight', 'setSpectrum', 'setParams', 'reset', 'render', 'renderPasses',
     'synchronize', 'readRGBA16F', 'readPhotons', 'writePhotons', 'enableKernelTiming', 'kernelTime',
-    'commUniqueId', 'commInit', 'commAllreduceRadiance', 'commReadComposite', 'commBarrier', 'version']) {
+    'commUniqueId', 'commInit', 'commAllreduceRadiance', 'commReadComposite', 'commBarrier', 'version',
+    'tonemapArtistic']) {
     assert.strictEqual(typeof A[f], 'function', f);
   }
   assert.ok(/gfx950/.test(A.version()));
@@ -78,6 +79,23 @@ test('addon loads; renderer construction fails loudly without a GPU', () => {
   assert.throws(() => new V.MCMSpectralComputeRenderer(V.createDevice(0), null, new V.Camera(), null,
     { resolution: 16, cie: gold('cie1931.json') }), e => e.vptmcmCode === -2 && /HIP device/.test(e.message));
   assert.throws(() => A.create(0, -1, 1), /resolution/);
+});
+
+test('tone mapper surface mirrors WebGPUArtisticToneMapper (properties, factory)', () => {
+  const tm = new (V.ToneMapperFactory('artistic'))(V.createDevice(0), null, null, { resolution: 8 });
+  const byName = {};
+  for (const p of tm.properties) byName[p.name] = p;
+  assert.deepStrictEqual(Object.keys(byName), ['low', 'high', 'mid', 'saturation', 'gamma']);
+  assert.strictEqual(tm.low, 0);
+  assert.strictEqual(tm.high, 1);
+  assert.strictEqual(tm.mid, 0.5);
+  assert.strictEqual(tm.saturation, 1);
+  assert.strictEqual(tm.gamma, 2.2);
+  assert.strictEqual(byName.mid.min, 0.00001);
+  assert.strictEqual(tm.getTexture(), null);
+  assert.throws(() => tm.render(), /no texture/);
+  assert.throws(() => tm.setTexture(new Uint16Array(4)), /HIP renderer/);
+  assert.throws(() => V.ToneMapperFactory('reinhard'), /No suitable class/);
 });
 
 (async () => {

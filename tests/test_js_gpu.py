@@ -22,14 +22,14 @@ ROOT = Path(__file__).resolve().parents[1]
 
 
 def run_case(tmp_path, vol, tf, R=64, passes=3, ext=32.0, layout="corner8", stream=True,
-             change_event=False):
+             change_event=False, tonemap=None):
     D, H, W = vol.shape
     (tmp_path / "vol.raw").write_bytes(np.ascontiguousarray(vol).tobytes())
     (tmp_path / "tf.bin").write_bytes(np.ascontiguousarray(tf).tobytes())
     seeds = [float(np.uint32(cf.seed_bits(k)).view(np.float32)) for k in range(passes + 2)]
     case = dict(R=R, passes=passes, extinction=ext, bounces=8, steps=8, layout=layout,
                 W=W, H=H, D=D, volume_path=str(tmp_path / "vol.raw"), tf_path=str(tmp_path / "tf.bin"),
-                seeds=seeds, stream_volume=stream, change_event=change_event)
+                seeds=seeds, stream_volume=stream, change_event=change_event, tonemap=tonemap)
     (tmp_path / "case.json").write_text(json.dumps(case))
     r = subprocess.run(["node", str(ROOT / "tests" / "js" / "gpu_render.js"), str(tmp_path / "case.json"),
                         str(tmp_path)], capture_output=True, text=True, timeout=600)
@@ -80,3 +80,16 @@ def test_js_property_change_resets(tmp_path):
     want_ph, _ = oracle_replay(vol, tf, 48, seeds, 2, 16.0, change_event=True)
     assert same(ph[:, :34], want_ph[:, :34])
     assert (ph[:, 7] == 0).all()  # samples cleared by the reset
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+def test_js_tonemapper(tmp_path):
+    """ToneMapperFactory('artistic') on the renderer's target, through N-API, against
+    the double-precision oracle of ArtisticToneMapper.wgsl (<= 1 LSB, >= 99.5 % equal)."""
+    vol, tf = cf.sphere_in_cube(64), cf.tf_spectral()
+    tm = dict(low=0.0, high=0.8, mid=0.3, saturation=1.2, gamma=2.2)
+    _, rgba, _, _ = run_case(tmp_path, vol, tf, tonemap=tm)
+    ldr = np.frombuffer((tmp_path / "ldr.bin").read_bytes(), np.uint8).reshape(64, 64, 4)
+    want = orc.Oracle(1).tonemap_artistic(rgba, **tm)
+    d = np.abs(ldr.astype(int) - want.astype(int))
+    assert d.max() <= 1 and (d == 0).mean() >= 0.995

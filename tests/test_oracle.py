@@ -199,3 +199,17 @@ def test_oracle_regression_fixture():
     h = hashlib.sha256(o.photons.tobytes() + rgba.tobytes()).hexdigest()
     ref = json.loads((GOLD / "oracle_regression.json").read_text())
     assert h == ref["sha256_R32_sphere64_tf3_ext32_2pass"]
+
+
+def test_tonemap_oracle_known_answers():
+    """Identity settings (low 0, high 1, mid 0.5, gamma 1: exponent 1,
+    saturation 1) quantise the clamped input; saturation 0 gives grey;
+    negative / NaN inputs map to 0 (pow of a negative base is NaN in WGSL)."""
+    o = orc.Oracle(1)
+    v = np.float16([[0.0, 0.25, 1.0, 1.0], [2.0, -0.5, 0.5, 1.0], [np.nan, 0.1, 0.9, 1.0]])
+    out = o.tonemap_artistic(v.view(np.uint16), gamma=1.0)
+    assert out[0].tolist() == [0, 64, 255, 255]
+    assert out[1, 0] == 255 and out[1, 1] == 0 and out[1, 2] == 128
+    assert out[2, 0] == 0
+    grey = o.tonemap_artistic(v.view(np.uint16)[:1], saturation=0.0, gamma=1.0)
+    assert grey[0, 0] == grey[0, 1] == grey[0, 2] == round(255 * (0.0 + 0.25 + 1.0) / 3)

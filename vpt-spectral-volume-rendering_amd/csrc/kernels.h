@@ -56,6 +56,13 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
                         const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba,
                         hipStream_t s);
+// Artistic tone mapper uniforms, derived on the host from (low, mid, high,
+// saturation, gamma) (WebGPUArtisticToneMapper.js:81-88, ArtisticToneMapper.wgsl:40-46).
+struct ToneParams {
+  float low, inv_range, saturation, exponent;  // exponent = -log2((mid-low)/(high-low)) / gamma
+};
+hipError_t launch_tonemap_artistic(const uint16_t* rgba16, uint32_t n, const ToneParams& T,
+                                   uint32_t* out, hipStream_t s);
 hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, void* out,
                           hipStream_t s);
 hipError_t launch_pack(const MarchParams& P, const float* ph, const uint16_t* rgba, float4* out,

@@ -779,6 +779,41 @@ __global__ __launch_bounds__(256) void k_pack(const MarchParams P, const float* 
   out[pix] = make_float4(r * n, g * n, b * n, n);
 }
 
+// ------------------------------------------------------------ tone mapping
+// The artistic tone mapper (ArtisticToneMapper.wgsl:38-48, run by
+// WebGPUArtisticToneMapper._renderFrame, js:77-122) on the rgba16float render
+// target: one lane per pixel, rgba8unorm out (alpha 1). The uv of the
+// fullscreen pass lands on texel centres (quad.wgsl vertex uv), so the linear
+// sample is the texel itself. Uniform-only terms (1/(high-low), the exponent
+// -log2(midpoint)/gamma) come precomputed from the host.
+__device__ __forceinline__ uint32_t unorm8(float v) {
+  v = __builtin_fminf(__builtin_fmaxf(v, 0.0f), 1.0f);  // NaN -> 0
+  return (uint32_t)(v * 255.0f + 0.5f);
+}
+__device__ __forceinline__ float pow_wgsl(float x, float e) {  // exp2(e * log2(x))
+  return e == 0.0f ? 1.0f : __builtin_amdgcn_exp2f(e * __builtin_amdgcn_logf(x));
+}
+__global__ __launch_bounds__(256) void k_tonemap_artistic(const uint2* __restrict__ rgba16, uint32_t n,
+                                                          ToneParams T, uint32_t* __restrict__ out) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint2 px = rgba16[i];
+  float c[3] = {(float)__builtin_bit_cast(_Float16, (uint16_t)(px.x & 0xffffu)),
+                (float)__builtin_bit_cast(_Float16, (uint16_t)(px.x >> 16)),
+                (float)__builtin_bit_cast(_Float16, (uint16_t)(px.y & 0xffffu))};
+#pragma unroll
+  for (int k = 0; k < 3; k++) c[k] = (c[k] - T.low) * T.inv_range;  // (color - low) / (high - low)
+  const float gray = 0.57735026918962576f;                             // normalize(vec3f(1))
+  float d = (c[0] * gray + c[1] * gray) + c[2] * gray;                 // dot(color.rgb, gray)
+  uint32_t q = 0xff000000u;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    float m = d * gray + (c[k] - d * gray) * T.saturation;  // mix(dot * gray, rgb, saturation)
+    q |= unorm8(pow_wgsl(m, T.exponent)) << (8 * k);
+  }
+  out[i] = q;
+}
+
 // ----------------------------------------------------------- diagnostics
 __global__ void k_debug_eval(int fn, const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                              uint32_t n) {
@@ -857,6 +892,14 @@ hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D
 hipError_t launch_pack(const MarchParams& P, const float* ph, const uint16_t* rgba, float4* out,
                        hipStream_t s) {
   hipLaunchKernelGGL(k_pack, dim3(march_blocks(P)), dim3(kBlock), 0, s, P, ph, rgba, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_tonemap_artistic(const uint16_t* rgba16, uint32_t n, const ToneParams& T,
+                                   uint32_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_tonemap_artistic, dim3((n + 255) / 256), dim3(256), 0, s,
+                     reinterpret_cast<const uint2*>(rgba16), n, T, out);
   return hipGetLastError();
 }
 

@@ -40,6 +40,7 @@ struct vptmcm {
 
   float* photons = nullptr;    // kNumPlanes * npad words
   uint16_t* rgba = nullptr;    // R*R*4 halfs
+  uint32_t* ldr = nullptr;     // R*R rgba8 of the tone mapper (lazily allocated)
   uint8_t* vol_lin = nullptr;  // W*H*D (staging for CORNER8; the volume for LINEAR)
   void* vol_c8 = nullptr;      // (W+1)(H+1)(D+1) u64
   uint32_t W = 0, H = 0, D = 0;
@@ -405,6 +406,7 @@ void vptmcm_destroy(vptmcm* h) {
   free_volume(h);
   if (h->photons) (void)hipFree(h->photons);
   if (h->rgba) (void)hipFree(h->rgba);
+  if (h->ldr) (void)hipFree(h->ldr);
   if (h->tf_rg) (void)hipFree(h->tf_rg);
   if (h->tf_b4) (void)hipFree(h->tf_b4);
   if (h->tf_brow) (void)hipFree(h->tf_brow);
@@ -602,6 +604,29 @@ int vptmcm_read_rgba16f(vptmcm* h, uint16_t* out) {
   HIPCHK(h, hipMemcpyAsync(out, h->rgba, (size_t)h->R * h->R * 8, hipMemcpyDeviceToHost,
                            h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  return VPTMCM_OK;
+}
+
+int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!params) FAIL(h, VPTMCM_EINVAL, "tonemap_artistic: null params");
+  HIPCHK(h, hipSetDevice(h->device));
+  const size_t npx = (size_t)h->R * h->R;
+  if (!h->ldr) HIPCHK(h, hipMalloc(&h->ldr, npx * 4));
+  // uniform-only terms in f32, as the shader evaluates them once per fragment
+  const float low = params[0], mid = params[1], high = params[2];
+  const float range = high - low;
+  ToneParams T;
+  T.low = low;
+  T.inv_range = 1.0f / range;
+  T.saturation = params[3];
+  const float midpoint = (mid - low) / range;
+  T.exponent = (float)(-std::log((double)midpoint) / std::log(2.0)) / params[4];
+  HIPCHK(h, launch_tonemap_artistic(h->rgba, (uint32_t)npx, T, h->ldr, h->stream));
+  if (rgba8_out) {
+    HIPCHK(h, hipMemcpyAsync(rgba8_out, h->ldr, npx * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  }
   return VPTMCM_OK;
 }
 

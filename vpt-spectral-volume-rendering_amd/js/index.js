@@ -2,6 +2,7 @@
 // Public JS surface of the MI355X spectral MCM renderer.
 const { MCMSpectralComputeRenderer, native } = require('./MCMSpectralComputeRenderer');
 const { RendererFactory } = require('./RendererFactory');
+const { ArtisticToneMapper, ToneMapperFactory } = require('./ArtisticToneMapper');
 const { Camera, Transform, PerspectiveCamera, mvpInverse } = require('./Camera');
 const { PropertyBag } = require('./PropertyBag');
 const { BufferLoader, FileLoader, RAWReader, Volume } = require('./readers');
@@ -14,6 +15,6 @@ function createDevice(ordinal = 0, layout = 'corner8') {
 }
 
 module.exports = {
-  MCMSpectralComputeRenderer, RendererFactory, Camera, Transform, PerspectiveCamera, mvpInverse,
+  MCMSpectralComputeRenderer, RendererFactory, ArtisticToneMapper, ToneMapperFactory, Camera, Transform, PerspectiveCamera, mvpInverse,
   PropertyBag, BufferLoader, FileLoader, RAWReader, Volume, spectrum, mat4, createDevice, native,
 };

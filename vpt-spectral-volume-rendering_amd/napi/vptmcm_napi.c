@@ -303,6 +303,20 @@ static napi_value js_read_rgba16f(napi_env env, napi_callback_info info) {
     return check(env, h, vptmcm_read_rgba16f(h, p));
 }
 
+/* tonemapArtistic(h, Float32Array[low, mid, high, saturation, gamma], Uint8Array(R*R*4), R) */
+static napi_value js_tonemap_artistic(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (get_args(env, info, 4, argv)) return NULL;
+    vptmcm* h = get_handle(env, argv[0]);
+    if (!h) return NULL;
+    const float* params = get_typed(env, argv[1], 4, 5, NULL);
+    if (!params) return NULL;
+    uint32_t R = get_u32(env, argv[3]);
+    uint8_t* out = get_typed(env, argv[2], 1, (size_t)R * R * 4, NULL);
+    if (!out) return NULL;
+    return check(env, h, vptmcm_tonemap_artistic(h, params, out));
+}
+
 /* readPhotons(h, Uint8Array(R*R*144), R) / writePhotons(h, Uint8Array, R) */
 static napi_value photons_call(napi_env env, napi_callback_info info, int write) {
     napi_value argv[3];
@@ -429,6 +443,7 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("synchronize", js_synchronize);
     EXPORT("readRGBA16F", js_read_rgba16f);
     EXPORT("readPhotons", js_read_photons);
+    EXPORT("tonemapArtistic", js_tonemap_artistic);
     EXPORT("writePhotons", js_write_photons);
     EXPORT("enableKernelTiming", js_enable_kernel_timing);
     EXPORT("kernelTime", js_kernel_time);

@@ -27,6 +27,7 @@ EXPORTS = [
     "vptmcm_set_material_tf", "vptmcm_set_light", "vptmcm_set_spectrum", "vptmcm_set_params",
     "vptmcm_reset", "vptmcm_render", "vptmcm_render_passes", "vptmcm_synchronize",
     "vptmcm_read_rgba16f", "vptmcm_read_photons", "vptmcm_write_photons",
+    "vptmcm_tonemap_artistic",
     "vptmcm_enable_kernel_timing", "vptmcm_kernel_time", "vptmcm_comm_unique_id",
     "vptmcm_comm_init", "vptmcm_comm_allreduce_radiance", "vptmcm_comm_read_composite",
     "vptmcm_comm_barrier", "vptmcm_comm_allreduce_host", "vptmcm_debug_eval",
@@ -92,6 +93,7 @@ def load() -> C.CDLL:
         "vptmcm_render_passes": (C.c_int, [vp, f32p, u32p, C.c_uint32]),
         "vptmcm_synchronize": (C.c_int, [vp]),
         "vptmcm_read_rgba16f": (C.c_int, [vp, vp]),
+        "vptmcm_tonemap_artistic": (C.c_int, [vp, vp, vp]),
         "vptmcm_read_photons": (C.c_int, [vp, vp]),
         "vptmcm_write_photons": (C.c_int, [vp, vp]),
         "vptmcm_enable_kernel_timing": (C.c_int, [vp, C.c_int]),
@@ -228,6 +230,13 @@ class Renderer:
     def read_rgba16f(self) -> np.ndarray:
         out = np.empty((self.R, self.R, 4), np.uint16)
         self._ck(self.L.vptmcm_read_rgba16f(self.h, _ptr(out)))
+        return out
+
+    def tonemap_artistic(self, low=0.0, mid=0.5, high=1.0, saturation=1.0, gamma=2.2) -> np.ndarray:
+        """WebGPUArtisticToneMapper on the current render target -> rgba8 [R, R, 4]."""
+        p = np.array([low, mid, high, saturation, gamma], np.float32)
+        out = np.zeros((self.R, self.R, 4), np.uint8)
+        self._ck(self.L.vptmcm_tonemap_artistic(self.h, _ptr(p), _ptr(out)))
         return out
 
     def read_photons(self) -> np.ndarray:
