@@ -22,14 +22,18 @@ ROOT = Path(__file__).resolve().parents[1]
 
 
 def run_case(tmp_path, vol, tf, R=64, passes=3, ext=32.0, layout="corner8", stream=True,
-             change_event=False, tonemap=None):
+             change_event=False, tonemap=None, bvp=None):
     D, H, W = vol.shape
     (tmp_path / "vol.raw").write_bytes(np.ascontiguousarray(vol).tobytes())
     (tmp_path / "tf.bin").write_bytes(np.ascontiguousarray(tf).tobytes())
     seeds = [float(np.uint32(cf.seed_bits(k)).view(np.float32)) for k in range(passes + 2)]
     case = dict(R=R, passes=passes, extinction=ext, bounces=8, steps=8, layout=layout,
                 W=W, H=H, D=D, volume_path=str(tmp_path / "vol.raw"), tf_path=str(tmp_path / "tf.bin"),
-                seeds=seeds, stream_volume=stream, change_event=change_event, tonemap=tonemap)
+                seeds=seeds, stream_volume=stream, change_event=change_event, tonemap=tonemap,
+                bvp_path=None)
+    if bvp is not None:
+        (tmp_path / "vol.bvp").write_bytes(bvp)
+        case["bvp_path"] = str(tmp_path / "vol.bvp")
     (tmp_path / "case.json").write_text(json.dumps(case))
     r = subprocess.run(["node", str(ROOT / "tests" / "js" / "gpu_render.js"), str(tmp_path / "case.json"),
                         str(tmp_path)], capture_output=True, text=True, timeout=600)
@@ -93,3 +97,16 @@ def test_js_tonemapper(tmp_path):
     want = orc.Oracle(1).tonemap_artistic(rgba, **tm)
     d = np.abs(ldr.astype(int) - want.astype(int))
     assert d.max() <= 1 and (d == 0).mean() >= 0.995
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+def test_js_bvp_volume_streams_bitexact(tmp_path):
+    """A bricked BVP archive (48 placements, some blocks deflated) streamed
+    block by block into HBM (vptmcm_volume_write_block) renders bit-exactly like
+    the oracle on the assembled volume."""
+    from bvp import write_bvp
+    vol, tf = cf.fbm_volume(64, 8), cf.tf_spectral()
+    ph, rgba, seeds, _ = run_case(tmp_path, vol, tf, bvp=write_bvp(vol, (16, 32, 24), 5))
+    want_ph, want_rgba = oracle_replay(vol, tf, 64, seeds, 3, 32.0)
+    assert same(ph[:, :34], want_ph[:, :34])
+    assert np.array_equal(rgba, want_rgba)

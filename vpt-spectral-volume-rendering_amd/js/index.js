@@ -5,7 +5,7 @@ const { RendererFactory } = require('./RendererFactory');
 const { ArtisticToneMapper, ToneMapperFactory } = require('./ArtisticToneMapper');
 const { Camera, Transform, PerspectiveCamera, mvpInverse } = require('./Camera');
 const { PropertyBag } = require('./PropertyBag');
-const { BufferLoader, FileLoader, RAWReader, Volume } = require('./readers');
+const { BufferLoader, FileLoader, RAWReader, ZIPReader, BVPReader, ReaderFactory, Volume } = require('./readers');
 const spectrum = require('./spectrum');
 const mat4 = require('./mat4');
 
@@ -16,5 +16,5 @@ function createDevice(ordinal = 0, layout = 'corner8') {
 
 module.exports = {
   MCMSpectralComputeRenderer, RendererFactory, ArtisticToneMapper, ToneMapperFactory, Camera, Transform, PerspectiveCamera, mvpInverse,
-  PropertyBag, BufferLoader, FileLoader, RAWReader, Volume, spectrum, mat4, createDevice, native,
+  PropertyBag, BufferLoader, FileLoader, RAWReader, ZIPReader, BVPReader, ReaderFactory, Volume, spectrum, mat4, createDevice, native,
 };

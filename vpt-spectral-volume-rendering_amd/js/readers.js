@@ -5,12 +5,21 @@
 //   Volume.readModality  (WebGPUVolume.js:34-96): for every placement, read
 //     its block and write it at its origin — here into the renderer's HBM
 //     volume through vptmcm_volume_write_block instead of queue.writeTexture.
-// Loaders return Uint8Array ranges (AjaxLoader/BlobLoader's readData).
+//   ZIPReader / BVPReader (readers/ZIPReader.js:20-91, BVPReader.js:13-29): the
+//     zip central directory, and a BVP's manifest.json + per-block files;
+//   ReaderFactory (readers/ReaderFactory.js): 'bvp' | 'raw' | 'zip'.
+// Loaders return Uint8Array ranges (AjaxLoader/BlobLoader's readData) and the
+// total length (readLength, AbstractLoader.js).
 const fs = require('fs');
+const zlib = require('zlib');
 
 class BufferLoader {
   constructor(bytes) {
     this.bytes = bytes instanceof Uint8Array ? bytes : new Uint8Array(bytes);
+  }
+
+  async readLength() {
+    return this.bytes.length;
   }
 
   async readData(start, end) {
@@ -21,6 +30,10 @@ class BufferLoader {
 class FileLoader {
   constructor(path) {
     this.path = path;
+  }
+
+  async readLength() {
+    return fs.statSync(this.path).size;
   }
 
   async readData(start, end) {
@@ -63,6 +76,106 @@ class RAWReader {
   async readBlock(block) {
     const slice = this.width * this.height;
     return this._loader.readData(block * slice, (block + 1) * slice);
+  }
+}
+
+// ZIP archive reader (ZIPReader.js): end-of-central-directory record, central
+// directory entries, local header -> file data. The reference returns the
+// stored bytes as they are (BVP archives are written uncompressed, method 0);
+// deflated entries (method 8) are inflated here with Node's zlib.
+class ZIPReader {
+  constructor(loader) {
+    this._loader = loader;
+    this._eocd = null;
+    this._cd = null;
+  }
+
+  async getFiles() {
+    if (!this._cd) await this._readCD();
+    return this._cd.map(e => e.name);
+  }
+
+  async readFile(fileName) {
+    if (!this._cd) await this._readCD();
+    const entry = this._cd.find(e => e.name === fileName);
+    if (!entry) throw new Error(`ZIPReader: file ${fileName} not in CD`);
+    const headerStart = entry.headerOffset;
+    const headerEnd = headerStart + 30;
+    const header = view(await this._loader.readData(headerStart, headerEnd));
+    if (header.getUint32(0, true) !== 0x04034b50) throw new Error(`ZIPReader: bad local header for ${fileName}`);
+    const dataStart = headerEnd + header.getUint16(26, true) + header.getUint16(28, true);
+    const data = await this._loader.readData(dataStart, dataStart + entry.compressedSize);
+    if (entry.method === 0) return data;
+    if (entry.method === 8) return new Uint8Array(zlib.inflateRawSync(Buffer.from(data)));
+    throw new Error(`ZIPReader: unsupported compression method ${entry.method} for ${fileName}`);
+  }
+
+  async _readEOCD() {
+    const MIN_EOCD_SIZE = 22;
+    const length = await this._loader.readLength();
+    const offset = Math.max(length - MIN_EOCD_SIZE, 0);
+    const v = view(await this._loader.readData(offset, offset + Math.min(length, MIN_EOCD_SIZE)));
+    if (v.byteLength < MIN_EOCD_SIZE || v.getUint32(0, true) !== 0x06054b50) {
+      throw new Error('ZIPReader: no end-of-central-directory record (archive comments are not supported)');
+    }
+    this._eocd = { entries: v.getUint16(10, true), size: v.getUint32(12, true), offset: v.getUint32(16, true) };
+  }
+
+  async _readCD() {
+    if (!this._eocd) await this._readEOCD();
+    const { offset: cdStart, size, entries: n } = this._eocd;
+    const bytes = await this._loader.readData(cdStart, cdStart + size);
+    const v = view(bytes);
+    const entries = [];
+    let o = 0;
+    for (let i = 0; i < n; i++) {
+      if (v.getUint32(o, true) !== 0x02014b50) throw new Error('ZIPReader: corrupt central directory');
+      const nameLength = v.getUint16(o + 28, true);
+      entries.push({
+        gpflag: v.getUint16(o + 8, true),
+        method: v.getUint16(o + 10, true),
+        compressedSize: v.getUint32(o + 20, true),
+        uncompressedSize: v.getUint32(o + 24, true),
+        name: Buffer.from(bytes.buffer, bytes.byteOffset + o + 46, nameLength).toString('utf8'),
+        headerOffset: v.getUint32(o + 42, true),
+      });
+      o += 46 + nameLength + v.getUint16(o + 30, true) + v.getUint16(o + 32, true);
+    }
+    this._cd = entries;
+  }
+}
+
+function view(u8) {
+  return new DataView(u8.buffer, u8.byteOffset, u8.byteLength);
+}
+
+// BVP volume archive (BVPReader.js): manifest.json holds modalities (dimensions,
+// placements) and blocks (url, dimensions); each block is a file in the zip.
+class BVPReader {
+  constructor(loader) {
+    this._loader = loader;
+    this._metadata = null;
+    this._zipReader = new ZIPReader(loader);
+  }
+
+  async readMetadata() {
+    const data = await this._zipReader.readFile('manifest.json');
+    this._metadata = JSON.parse(Buffer.from(data.buffer, data.byteOffset, data.byteLength).toString('utf8'));
+    return this._metadata;
+  }
+
+  async readBlock(block) {
+    if (!this._metadata) await this.readMetadata();
+    return this._zipReader.readFile(this._metadata.blocks[block].url);
+  }
+}
+
+function ReaderFactory(which) {  // readers/ReaderFactory.js
+  switch (which) {
+    case 'bvp': return BVPReader;
+    case 'raw': return RAWReader;
+    case 'zip': return ZIPReader;
+    default: throw new Error('No suitable class');
   }
 }
 
@@ -126,4 +239,4 @@ class Volume {
   }
 }
 
-module.exports = { BufferLoader, FileLoader, RAWReader, Volume };
+module.exports = { BufferLoader, FileLoader, RAWReader, ZIPReader, BVPReader, ReaderFactory, Volume };
