@@ -47,7 +47,12 @@ extern "C" {
 #define VPTMCM_TF_BYTES (256 * 256 * 4) /* rgba8 256x256, js:158-162       */
 #define VPTMCM_LIGHT_BYTES 256      /* r8 256x1, js:144-148                */
 #define VPTMCM_PHOTON_BYTES 144     /* struct PhotonSpectral stride, js:131 */
+#define VPTMCM_PHOTON_RGB_BYTES 64  /* struct Photon stride (Photon.wgsl), WebGPUMCMComputeRenderer.js */
 #define VPTMCM_UNIQUE_ID_BYTES 128  /* sizeof(ncclUniqueId)                */
+
+/* Renderer kinds behind the same boundary (WebGPURendererFactory.js:12-27). */
+#define VPTMCM_RENDERER_SPECTRAL 0  /* 'mcm-spectral-compute', WebGPUMCMSpectralComputeRenderer */
+#define VPTMCM_RENDERER_RGB 1       /* 'mcm-compute', WebGPUMCMComputeRenderer (MCMComputeRenderer.wgsl) */
 
 /* Volume layouts in HBM (see DESIGN.md "Data layout"). */
 #define VPTMCM_LAYOUT_LINEAR 0   /* x-fastest u8, as writeTexture lays it out */
@@ -61,6 +66,7 @@ typedef struct vptmcm_config {
     uint32_t max_bins;      /* must be VPTMCM_MAX_BINS (12)                        */
     int32_t device;         /* HIP device ordinal; -1 = current device             */
     uint32_t volume_layout; /* VPTMCM_LAYOUT_*                                     */
+    uint32_t renderer;      /* VPTMCM_RENDERER_* (0 = spectral, the default)       */
 } vptmcm_config;
 
 /* Per-pass parameters (render UBO fields other than the matrix and seed;
@@ -121,7 +127,20 @@ int vptmcm_set_light(vptmcm* h, const uint8_t* spd /* 256 */, const float dir[3]
  * n_bins = u32(buf[0] + 0.5) must be <= 12. */
 int vptmcm_set_spectrum(vptmcm* h, const float* buf /* 64 */);
 
-/* The scalar render uniforms, js:296-306. */
+/* RGB renderer only: the rgba8unorm-srgb transfer function texture
+ * (WebGPUAbstractComputeRenderer.setTransferFunction, js:62-69; the default
+ * 2x1 texture of the ctor, :23-28, is installed by vptmcm_create). The kernel
+ * samples it at (density, 0) (MCMComputeRenderer.wgsl:52-56), i.e. row 0;
+ * width <= 4096. */
+int vptmcm_set_transfer_function(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height);
+
+/* RGB renderer: the environment texture sampled on exit (wgsl:49-52, 126-131).
+ * Only the 1x1 map the rendering context creates (WebGPURenderingContext.js:
+ * 97-108; default white) is supported: every direction reads its texel. */
+int vptmcm_set_environment(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height);
+
+/* The scalar render uniforms, js:296-306 (the RGB renderer also reads
+ * anisotropy, MCMComputeRenderer.wgsl:140). */
 int vptmcm_set_params(vptmcm* h, const vptmcm_params* p);
 
 /* ---- the hot path -------------------------------------------------------- */
@@ -149,10 +168,11 @@ int vptmcm_synchronize(vptmcm* h);
  * pixel (x, y) at ((y*R)+x)*4 (textureStore(uRadiance, globalId.xy), wgsl:168). */
 int vptmcm_read_rgba16f(vptmcm* h, uint16_t* out);
 
-/* The photon buffer in the reference's 144-byte PhotonSpectral layout
- * (wgsl:238-247), photon of pixel (x, y) at index y*R + x. out must hold
- * R*R*144 bytes. The transmittance field (never read by the kernel) is
- * returned as 1.0f, the value every reset writes. */
+/* The photon buffer in the reference's layout, photon of pixel (x, y) at
+ * index y*R + x: the 144-byte PhotonSpectral (wgsl:238-247; out holds R*R*144
+ * bytes; the transmittance field, never read by the kernel, is returned as
+ * 1.0f, the value every reset writes) or, for the RGB renderer, the 64-byte
+ * Photon (Photon.wgsl; R*R*VPTMCM_PHOTON_RGB_BYTES). */
 int vptmcm_read_photons(vptmcm* h, void* out);
 
 /* Inverse of read_photons (checkpoint / resume and fixtures). */

@@ -581,6 +581,174 @@ void orc_render(uint32_t R, const orc_uniforms* u, const float* spectrum, const 
     run_rows(&c, R, y0, y1, 0, photons, rgb32, rgba16, nthreads);
 }
 
+/* ===================================================== RGB sibling renderer
+ * MCMComputeRenderer.wgsl ('mcm-compute', WebGPUMCMComputeRenderer.js): the
+ * same Woodcock march with an RGB photon (Photon.wgsl), the TF sampled at
+ * (density, 0) of an rgba8unorm-srgb texture (WebGPUAbstractComputeRenderer.js:
+ * 23-28, :62-69), scattering probability alpha * max3(rgb), transmittance
+ * tinting, HG with the anisotropy uniform, and the environment texel on exit. */
+
+float orc_srgb_to_linear(uint8_t b) {
+    double v = b / 255.0;
+    return (float)(v <= 0.04045 ? v / 12.92 : pow((v + 0.055) / 1.055, 2.4));
+}
+
+typedef struct rgb_ctx {
+    const orc_uniforms* u;
+    const uint8_t* vol;
+    uint32_t W, H, D;
+    float tf[4096][4]; /* row 0 of the TF, decoded (row v = 0 is all a (d, 0) lookup reads) */
+    uint32_t tf_w;
+    float env[4];
+} rgb_ctx;
+
+/* textureSampleLevel(uTransferFunction, (d, g=0)): the v axis at 0 clamps to
+ * row 0 for both taps (lerp(a, a, f) = a), the u axis is a linear lerp of the
+ * decoded texels. */
+static void rgb_sample_tf(const rgb_ctx* c, float d, float out[4]) {
+    uint32_t i0, i1;
+    float f;
+    axis(d, c->tf_w, &i0, &i1, &f);
+    for (int k = 0; k < 4; k++) out[k] = lerp(c->tf[i0][k], c->tf[i1][k], f);
+}
+
+/* resetPhoton, MCMComputeRenderer.wgsl:38-47 */
+static void rgb_reset_photon(const rgb_ctx* c, orc_photon_rgb* p, v2 screen, uint32_t* st) {
+    v3 from, to;
+    unproject_rand(st, screen, c->u->mvp_inverse, c->u->inv_res, c->u->blur, &from, &to);
+    v3 diff = {to.x - from.x, to.y - from.y, to.z - from.z};
+    v3 dir = norm3(diff);
+    p->direction[0] = dir.x; p->direction[1] = dir.y; p->direction[2] = dir.z;
+    p->bounces = 0u;
+    float tn = smax(intersect_cube_near(from, dir), 0.0f);
+    p->position[0] = fmaf(tn, dir.x, from.x);
+    p->position[1] = fmaf(tn, dir.y, from.y);
+    p->position[2] = fmaf(tn, dir.z, from.z);
+    p->transmittance[0] = p->transmittance[1] = p->transmittance[2] = 1.0f;
+}
+
+static inline void rgb_add_radiance(orc_photon_rgb* p, const float L[3]) {
+    float in = rcp((float)p->samples);
+    for (int k = 0; k < 3; k++) p->radiance[k] = fmaf(L[k] - p->radiance[k], in, p->radiance[k]);
+}
+
+/* render compute_main, MCMComputeRenderer.wgsl:97-162 */
+static void rgb_render_pixel(const rgb_ctx* c, uint32_t R, uint32_t x, uint32_t y,
+                             orc_photon_rgb* photons, uint16_t* rgba16) {
+    const orc_uniforms* u = c->u;
+    v2 screen = screen_pos(x, y, u->inv_res);
+    orc_photon_rgb p = photons[(size_t)y * R + x];
+    uint32_t st = orc_hash3(x, y, u->seed_bits);
+    for (uint32_t i = 0u; i < u->steps; i++) {
+        float dist = rnd_exponential(&st, u->extinction);
+        p.position[0] = fmaf(dist, p.direction[0], p.position[0]);
+        p.position[1] = fmaf(dist, p.direction[1], p.position[1]);
+        p.position[2] = fmaf(dist, p.direction[2], p.position[2]);
+        float vs[4];
+        rgb_sample_tf(c, orc_sample_volume(c->vol, c->W, c->H, c->D, p.position), vs);
+        float pnull = 1.0f - vs[3];
+        float pscat = (p.bounces >= u->max_bounces) ? 0.0f : vs[3] * smax(smax(vs[0], vs[1]), vs[2]);
+        float pabs = (1.0f - pnull) - pscat;
+        float wheel = rnd_uniform(&st);
+        int oob = p.position[0] > 1.0f || p.position[1] > 1.0f || p.position[2] > 1.0f ||
+                  p.position[0] < 0.0f || p.position[1] < 0.0f || p.position[2] < 0.0f;
+        if (oob) { /* environment texel (1x1 map: every coordinate reads it) */
+            float L[3] = {p.transmittance[0] * c->env[0], p.transmittance[1] * c->env[1],
+                          p.transmittance[2] * c->env[2]};
+            p.samples++;
+            rgb_add_radiance(&p, L);
+            rgb_reset_photon(c, &p, screen, &st);
+        } else if (wheel < pabs) {
+            float L[3] = {0.0f, 0.0f, 0.0f};
+            p.samples++;
+            rgb_add_radiance(&p, L);
+            rgb_reset_photon(c, &p, screen, &st);
+        } else if (wheel < pabs + pscat) {
+            for (int k = 0; k < 3; k++) p.transmittance[k] = p.transmittance[k] * vs[k];
+            v3 d = {p.direction[0], p.direction[1], p.direction[2]};
+            v3 nd = sample_hg(&st, u->anisotropy, d);
+            p.direction[0] = nd.x; p.direction[1] = nd.y; p.direction[2] = nd.z;
+            p.bounces++;
+        }
+    }
+    photons[(size_t)y * R + x] = p;
+    if (rgba16) {
+        size_t pix = (size_t)y * R + x;
+        for (int k = 0; k < 3; k++) rgba16[pix * 4 + k] = orc_f2h(p.radiance[k]);
+        rgba16[pix * 4 + 3] = 0x3c00u;
+    }
+}
+
+typedef struct rgb_job {
+    const rgb_ctx* c;
+    uint32_t R, y0, y1;
+    int is_reset;
+    orc_photon_rgb* photons;
+    uint16_t* rgba16;
+} rgb_job;
+
+static void* rgb_run_job(void* arg) {
+    rgb_job* j = (rgb_job*)arg;
+    for (uint32_t y = j->y0; y < j->y1; y++)
+        for (uint32_t x = 0; x < j->R; x++) {
+            if (j->is_reset) { /* reset compute_main */
+                v2 screen = screen_pos(x, y, j->c->u->inv_res);
+                orc_photon_rgb p;
+                memset(&p, 0, sizeof p);
+                uint32_t st = orc_hash3(x, y, j->c->u->seed_bits);
+                rgb_reset_photon(j->c, &p, screen, &st);
+                p.radiance[0] = p.radiance[1] = p.radiance[2] = 1.0f;
+                p.samples = 0u;
+                j->photons[(size_t)y * j->R + x] = p;
+            } else {
+                rgb_render_pixel(j->c, j->R, x, y, j->photons, j->rgba16);
+            }
+        }
+    return NULL;
+}
+
+static void rgb_run(const rgb_ctx* c, uint32_t R, int is_reset, orc_photon_rgb* photons,
+                    uint16_t* rgba16, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if ((uint32_t)nthreads > R) nthreads = R ? (int)R : 1;
+    pthread_t th[256];
+    rgb_job jobs[256];
+    for (int t = 0; t < nthreads; t++) {
+        rgb_job j = {c, R, (uint32_t)((uint64_t)R * t / nthreads),
+                     (uint32_t)((uint64_t)R * (t + 1) / nthreads), is_reset, photons, rgba16};
+        jobs[t] = j;
+    }
+    for (int t = 1; t < nthreads; t++) pthread_create(&th[t], NULL, rgb_run_job, &jobs[t]);
+    rgb_run_job(&jobs[0]);
+    for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
+void orc_reset_rgb(uint32_t R, const orc_uniforms* u, orc_photon_rgb* photons, int nthreads) {
+    static rgb_ctx c; /* large; the oracle is not re-entrant across threads of the caller */
+    memset(&c, 0, sizeof c);
+    c.u = u;
+    rgb_run(&c, R, 1, photons, NULL, nthreads);
+}
+
+void orc_render_rgb(uint32_t R, const orc_uniforms* u, const uint8_t* volume, uint32_t W,
+                    uint32_t H, uint32_t D, const uint8_t* tf, uint32_t tf_w, uint32_t tf_h,
+                    const uint8_t env[4], orc_photon_rgb* photons, uint16_t* rgba16, int nthreads) {
+    static rgb_ctx c;
+    (void)tf_h;
+    memset(&c, 0, sizeof c);
+    c.u = u;
+    c.vol = volume;
+    c.W = W; c.H = H; c.D = D;
+    c.tf_w = tf_w > 4096 ? 4096 : tf_w;
+    for (uint32_t i = 0; i < c.tf_w; i++) {
+        for (int k = 0; k < 3; k++) c.tf[i][k] = orc_srgb_to_linear(tf[i * 4 + k]);
+        c.tf[i][3] = (float)tf[i * 4 + 3] * INV255;
+    }
+    for (int k = 0; k < 4; k++) c.env[k] = (float)env[k] * INV255;
+    rgb_run(&c, R, 0, photons, rgba16, nthreads);
+}
+
 /* Batch evaluation of the primitives (fn as in vptmcm_debug_eval). */
 void orc_eval_batch(int fn, const uint32_t* in, uint32_t* out, uint32_t n) {
     for (uint32_t i = 0; i < n; i++) {

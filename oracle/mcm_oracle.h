@@ -55,6 +55,34 @@ void orc_render(uint32_t R, const orc_uniforms* u, const float* spectrum,
                 orc_photon* photons, float* rgb32, uint16_t* rgba16, int nthreads,
                 uint32_t y0, uint32_t y1);
 
+/* ---- RGB sibling renderer (MCMComputeRenderer.wgsl, 'mcm-compute') ------ */
+
+/* struct Photon (src/wgsl/mixins/Photon.wgsl): 64-byte stride. */
+typedef struct orc_photon_rgb {
+    float position[3];
+    uint32_t bounces;
+    float direction[3];
+    uint32_t samples;
+    float transmittance[3];
+    uint32_t _pad0;
+    float radiance[3];
+    uint32_t _pad1;
+} orc_photon_rgb;
+
+/* sRGB -> linear decode of an rgba8unorm-srgb texel channel (the sampler
+ * decodes before filtering): byte/255 <= 0.04045 ? v/12.92 :
+ * ((v+0.055)/1.055)^2.4, in double, rounded to f32. */
+float orc_srgb_to_linear(uint8_t b);
+
+/* reset compute_main (MCMComputeRenderer.wgsl reset part) / render
+ * compute_main (render part). The transfer function is the rgba8unorm-srgb
+ * texture (tf_w x tf_h, row-major) of setTransferFunction; the environment is
+ * the 1x1 rgba8unorm texel the rendering context creates. */
+void orc_reset_rgb(uint32_t R, const orc_uniforms* u, orc_photon_rgb* photons, int nthreads);
+void orc_render_rgb(uint32_t R, const orc_uniforms* u, const uint8_t* volume, uint32_t W,
+                    uint32_t H, uint32_t D, const uint8_t* tf, uint32_t tf_w, uint32_t tf_h,
+                    const uint8_t env[4], orc_photon_rgb* photons, uint16_t* rgba16, int nthreads);
+
 /* Artistic tone mapper (ArtisticToneMapper.wgsl:38-48) over n rgba16float
  * pixels -> rgba8 (alpha 255), evaluated in double precision: the checker of
  * the device's f32 version (tolerance test, see tests/test_gpu_tonemap.py).

@@ -53,6 +53,13 @@ def load() -> C.CDLL:
         L.orc_sample_tf.restype = None
         L.orc_sample_light.argtypes = [vp, C.c_float]
         L.orc_sample_light.restype = C.c_float
+        L.orc_reset_rgb.argtypes = [C.c_uint32, C.POINTER(Uniforms), vp, C.c_int]
+        L.orc_reset_rgb.restype = None
+        L.orc_render_rgb.argtypes = [C.c_uint32, C.POINTER(Uniforms), vp, C.c_uint32, C.c_uint32,
+                                     C.c_uint32, vp, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_int]
+        L.orc_render_rgb.restype = None
+        L.orc_srgb_to_linear.argtypes = [C.c_uint8]
+        L.orc_srgb_to_linear.restype = C.c_float
         L.orc_tonemap_artistic.argtypes = [vp, C.c_uint32, vp, vp]
         L.orc_tonemap_artistic.restype = None
         L.orc_eval_batch.argtypes = [C.c_int, vp, vp, C.c_uint32]
@@ -134,3 +141,31 @@ class Oracle:
         o = np.empty_like(i)
         self.L.orc_eval_batch(fn, _vp(i), _vp(o), i.size)
         return o
+
+
+class OracleRGB(Oracle):
+    """The RGB sibling renderer ('mcm-compute', MCMComputeRenderer.wgsl): 64-B
+    photons, an rgba8unorm-srgb TF image [H, W, 4] and a 1x1 environment texel."""
+    PHOTON_WORDS_RGB = 16
+
+    def __init__(self, R: int):
+        super().__init__(R)
+        self.photons = np.zeros((R * R, self.PHOTON_WORDS_RGB), np.uint32)
+        self.tf = np.array([[[255, 0, 0, 0], [255, 0, 0, 255]]], np.uint8)  # the ctor's 2x1 default
+        self.env = np.array([255, 255, 255, 255], np.uint8)
+
+    def reset(self, mvp, seed_bits: int, nthreads: int = 8) -> None:
+        u = self.uniforms(mvp, seed_bits)
+        self.L.orc_reset_rgb(self.R, C.byref(u), _vp(self.photons), nthreads)
+
+    def render(self, mvp, seed_bits: int, nthreads: int = 8, rows=None):
+        """One pass; returns (None, rgba16 [R,R,4])."""
+        v = np.ascontiguousarray(self.volume, dtype=np.uint8)
+        D, H, W = v.shape
+        u = self.uniforms(mvp, seed_bits)
+        rgba = np.zeros((self.R, self.R, 4), np.uint16)
+        tf = np.ascontiguousarray(self.tf, dtype=np.uint8)
+        env = np.ascontiguousarray(self.env, dtype=np.uint8)
+        self.L.orc_render_rgb(self.R, C.byref(u), _vp(v), W, H, D, _vp(tf), tf.shape[1], tf.shape[0],
+                              _vp(env), _vp(self.photons), _vp(rgba), nthreads)
+        return None, rgba

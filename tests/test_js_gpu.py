@@ -110,3 +110,36 @@ def test_js_bvp_volume_streams_bitexact(tmp_path):
     want_ph, want_rgba = oracle_replay(vol, tf, 64, seeds, 3, 32.0)
     assert same(ph[:, :34], want_ph[:, :34])
     assert np.array_equal(rgba, want_rgba)
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+def test_js_rgb_renderer_bitexact(tmp_path):
+    """RendererFactory('mcm-compute') (the RGB sibling, MCMComputeRenderer.wgsl)
+    through N-API against the RGB oracle, with a coloured environment texel."""
+    from test_gpu_rgb import tf_rgb
+    vol, tf = cf.fbm_volume(48, 13), tf_rgb("ramp")
+    D, H, W = vol.shape
+    (tmp_path / "vol.raw").write_bytes(np.ascontiguousarray(vol).tobytes())
+    (tmp_path / "tf.bin").write_bytes(tf.tobytes())
+    seeds = [float(np.uint32(cf.seed_bits(k)).view(np.float32)) for k in range(5)]
+    env = [230, 200, 170, 255]
+    case = dict(R=64, passes=3, extinction=16.0, bounces=8, steps=8, layout="corner8", W=W, H=H, D=D,
+                volume_path=str(tmp_path / "vol.raw"), tf_path=str(tmp_path / "tf.bin"), seeds=seeds,
+                stream_volume=True, change_event=False, tonemap=None, bvp_path=None,
+                renderer="mcm-compute", anisotropy=0.5, tf_w=tf.shape[1], tf_h=tf.shape[0], env=env)
+    (tmp_path / "case.json").write_text(json.dumps(case))
+    r = subprocess.run(["node", str(ROOT / "tests" / "js" / "gpu_render.js"), str(tmp_path / "case.json"),
+                        str(tmp_path)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    ph = np.frombuffer((tmp_path / "photons.bin").read_bytes(), np.uint32).reshape(64 * 64, 16)
+    rgba = np.frombuffer((tmp_path / "rgba.bin").read_bytes(), np.uint16).reshape(64, 64, 4)
+    o = orc.OracleRGB(64)
+    o.volume, o.tf, o.env = vol, tf, np.array(env, np.uint8)
+    o.params.update(extinction=16.0, anisotropy=0.5, bounces=8, steps=8)
+    mvp = cf.default_mvp_inverse()
+    bits = lambda s: int(np.float32(s).view(np.uint32))  # noqa: E731
+    o.reset(mvp, bits(seeds[0]))
+    for k in range(3):
+        _, want = o.render(mvp, bits(seeds[1 + k]))
+    assert same(ph, o.photons)
+    assert np.array_equal(rgba, want)

@@ -213,3 +213,19 @@ def test_tonemap_oracle_known_answers():
     assert out[2, 0] == 0
     grey = o.tonemap_artistic(v.view(np.uint16)[:1], saturation=0.0, gamma=1.0)
     assert grey[0, 0] == grey[0, 1] == grey[0, 2] == round(255 * (0.0 + 0.25 + 1.0) / 3)
+
+
+def test_rgb_oracle_srgb_decode_and_reset():
+    """sRGB decode endpoints/midpoints (IEC 61966-2-1) and the RGB reset kernel's
+    state: transmittance 1, radiance 1, samples 0, rays starting on the cube."""
+    o = orc.OracleRGB(8)
+    f = o.L.orc_srgb_to_linear
+    assert f(0) == 0.0 and f(255) == 1.0
+    assert abs(f(10) - (10 / 255) / 12.92) < 1e-9
+    assert abs(f(128) - ((128 / 255 + 0.055) / 1.055) ** 2.4) < 1e-7
+    o.reset(cf.default_mvp_inverse(), cf.seed_bits(0))
+    w = o.photons
+    fl = w.view(np.float32)
+    assert (fl[:, 8:11] == 1.0).all() and (fl[:, 12:15] == 1.0).all()
+    assert (w[:, 7] == 0).all() and (w[:, 3] == 0).all()
+    assert np.allclose(np.linalg.norm(fl[:, 4:7], axis=1), 1.0, atol=1e-6)

@@ -63,6 +63,10 @@ struct ToneParams {
 };
 hipError_t launch_tonemap_artistic(const uint16_t* rgba16, uint32_t n, const ToneParams& T,
                                    uint32_t* out, hipStream_t s);
+// RGB sibling renderer (MCMComputeRenderer.wgsl): reset / march kernels.
+hipError_t launch_reset_rgb(const MarchParams& P, float* ph, hipStream_t s);
+hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSeeds& PS, float* ph,
+                            const uint8_t* vol, const float4* tf, uint16_t* rgba, hipStream_t s);
 hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, void* out,
                           hipStream_t s);
 hipError_t launch_pack(const MarchParams& P, const float* ph, const uint16_t* rgba, float4* out,

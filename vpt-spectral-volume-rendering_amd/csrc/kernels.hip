@@ -735,6 +735,166 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 
 
 
+// ------------------------------------------------------- RGB sibling march
+// MCMComputeRenderer.wgsl ('mcm-compute'): the same Woodcock march with an RGB
+// photon (Photon.wgsl, 14 SoA planes), TF = row 0 of an sRGB texture decoded
+// on the host (float4 per texel, staged in LDS), P_scat = alpha * max3(rgb),
+// transmittance tinting on scatter, HG with the anisotropy uniform, and the 1x1
+// environment texel times the transmittance on exit. Same tile/photon mapping,
+// XCD swizzle, pass fusion and speculative step structure as k_march.
+__device__ __forceinline__ void rgb_reset_draws(const MarchParams& P, float sx, float sy, bool fixed,
+                                                f3 from, uint32_t h1, uint32_t h2, uint32_t h3,
+                                                uint32_t h4, f3& pos, f3& dir) {
+  if (!fixed) {
+    float dx, dy;
+    disk_of(h1, h2, dx, dy);
+    from = unproject(P.m, fmaf(dx, P.blur, sx), fmaf(dy, P.blur, sy), -1.0f);
+  }
+  dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
+  pos = ray_start(from, dir);
+}
+
+__global__ __launch_bounds__(kBlock) void k_reset_rgb(const MarchParams P, float* __restrict__ ph) {
+  uint32_t x, y;
+  size_t i;
+  if (!tile_pixel(P, x, y, i)) return;
+  const size_t S = P.npad;
+  float sx, sy;
+  screen_of(P, x, y, sx, sy);
+  f3 from{0.0f, 0.0f, 0.0f};
+  bool fixed = near_fixed(P, sx, sy, from);
+  uint32_t h1 = pcg_hash(hash3(x, y, P.seed)), h2 = pcg_hash(h1), h3 = pcg_hash(h2), h4 = pcg_hash(h3);
+  f3 pos, dir;
+  rgb_reset_draws(P, sx, sy, fixed, from, h1, h2, h3, h4, pos, dir);
+  const float w[kRgbPlanes] = {pos.x, pos.y, pos.z, dir.x, dir.y, dir.z, 0.0f, 0.0f,
+                               1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f};
+#pragma unroll
+  for (uint32_t k = 0; k < kRgbPlanes; k++) ph[k * S + i] = w[k];
+}
+
+template <uint32_t L>
+__global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, const MarchParams P,
+                                                           float* __restrict__ ph,
+                                                           const uint8_t* __restrict__ vol,
+                                                           const float4* __restrict__ tf,
+                                                           uint16_t* __restrict__ rgba) {
+  __shared__ float4 s_tf[kRgbTfMax];
+  const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x) * (kMarchBlock / 64) +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
+  const uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
+  const size_t i = (size_t)tile * 64u + lane;
+  const bool live = tile < P.n_tiles && x < P.R && y < P.R;
+  const size_t S = P.npad;
+  f3 pos{0.0f, 0.0f, 0.0f}, dir{0.0f, 0.0f, 0.0f}, tr{0.0f, 0.0f, 0.0f}, rad{0.0f, 0.0f, 0.0f};
+  uint32_t bounces = 0u, samples = 0u;
+  if (live) {
+    pos = f3{ph[kPx * S + i], ph[kPy * S + i], ph[kPz * S + i]};
+    dir = f3{ph[kDx * S + i], ph[kDy * S + i], ph[kDz * S + i]};
+    bounces = as_u(ph[kBounces * S + i]);
+    samples = as_u(ph[kSamples * S + i]);
+    tr = f3{ph[(kTr0 + 0) * S + i], ph[(kTr0 + 1) * S + i], ph[(kTr0 + 2) * S + i]};
+    rad = f3{ph[(kRgbRad0 + 0) * S + i], ph[(kRgbRad0 + 1) * S + i], ph[(kRgbRad0 + 2) * S + i]};
+  }
+  for (uint32_t k = threadIdx.x; k < P.tf_w; k += kMarchBlock) s_tf[k] = tf[k];
+  __syncthreads();
+  if (!live) return;
+
+  float sx, sy;
+  screen_of(P, x, y, sx, sy);
+  f3 from{0.0f, 0.0f, 0.0f};
+  const bool fixed = near_fixed(P, sx, sy, from);
+  const float g = P.anisotropy;
+  const bool iso = __builtin_fabsf(g) < kEps;  // uniform
+  const float tfw = (float)P.tf_w;
+  const int tfm = (int)P.tf_w - 1;
+
+  for (uint32_t pass = 0; pass < PS.n; pass++) {
+    uint32_t st = hash3(x, y, pass_seed(pass));  // MCMComputeRenderer.wgsl:112
+    for (uint32_t step = 0; step < P.steps; step++) {
+      uint32_t s1 = pcg_hash(st);
+      float dist = -spec_log_unit(s1) * P.rcp_extinction;  // exponential.wgsl
+      pos = f3{fmaf(dist, dir.x, pos.x), fmaf(dist, dir.y, pos.y), fmaf(dist, dir.z, pos.z)};
+      uint32_t sw = pcg_hash(s1);
+      float wheel = (float)sw * 2.3283064365386963e-10f;
+      bool oob = pos.x > 1.0f || pos.y > 1.0f || pos.z > 1.0f || pos.x < 0.0f || pos.y < 0.0f ||
+                 pos.z < 0.0f;
+      uint32_t h1 = pcg_hash(sw), h2 = pcg_hash(h1), h3 = pcg_hash(h2), h4 = pcg_hash(h3);
+      if (__builtin_amdgcn_ballot_w64(!oob) == 0ull) {  // every lane leaves: exit + reset
+        samples++;
+        float inv = rcp_in_range((float)samples);
+        rad = f3{fmaf(tr.x * P.env[0] - rad.x, inv, rad.x), fmaf(tr.y * P.env[1] - rad.y, inv, rad.y),
+                 fmaf(tr.z * P.env[2] - rad.z, inv, rad.z)};
+        rgb_reset_draws(P, sx, sy, fixed, from, h1, h2, h3, h4, pos, dir);
+        bounces = 0u;
+        tr = f3{1.0f, 1.0f, 1.0f};
+        st = h4;
+        continue;
+      }
+      VolTap vt = vol_fetch<L>(P, vol, pos);  // gather in flight from here
+      // speculative reset candidate (draws h1..h4) and the g-independent HG half
+      f3 rpos, rdir;
+      rgb_reset_draws(P, sx, sy, fixed, from, h1, h2, h3, h4, rpos, rdir);
+      float dx, dy;
+      disk_of(h1, h2, dx, dy);
+      float nrm = fmaf(dy, dy, dx * dx);  // sphere.wgsl
+      float srad = 2.0f * sqrt_z(1.0f - nrm);
+      f3 u{srad * dx, srad * dy, 1.0f - 2.0f * nrm};
+      float ud = dot3(u, dir);
+      f3 circle = norm3(f3{fmaf(-ud, dir.x, u.x), fmaf(-ud, dir.y, u.y), fmaf(-ud, dir.z, u.z)});
+      // sampleVolumeColor: TF at (density, 0) = a lerp along row 0 (wgsl:52-56)
+      float d = vol_filter(vt);
+      float ft;
+      int it = axis_floor(d, tfw, &ft);
+      float4 ta = s_tf[clampi(it, tfm)], tb = s_tf[clampi(it + 1, tfm)];
+      float cr = lerp(ta.x, tb.x, ft), cg = lerp(ta.y, tb.y, ft), cb = lerp(ta.z, tb.z, ft);
+      float ca = lerp(ta.w, tb.w, ft);
+      float pnull = 1.0f - ca;
+      float pscat = (bounces >= P.max_bounces) ? 0.0f : ca * smax(smax(cr, cg), cb);
+      float pabs = (1.0f - pnull) - pscat;
+      if (oob || wheel < pabs) {  // exit (environment) or absorption (wgsl:126-139)
+        samples++;
+        float inv = rcp_in_range((float)samples);
+        f3 Lr = oob ? f3{tr.x * P.env[0], tr.y * P.env[1], tr.z * P.env[2]} : f3{0.0f, 0.0f, 0.0f};
+        rad = f3{fmaf(Lr.x - rad.x, inv, rad.x), fmaf(Lr.y - rad.y, inv, rad.y),
+                 fmaf(Lr.z - rad.z, inv, rad.z)};
+        pos = rpos;
+        dir = rdir;
+        bounces = 0u;
+        tr = f3{1.0f, 1.0f, 1.0f};
+        st = h4;
+      } else if (wheel < pabs + pscat) {  // scattering (wgsl:140-144)
+        tr = f3{tr.x * cr, tr.y * cg, tr.z * cb};
+        if (iso) {
+          dir = u;
+          st = h2;
+        } else {
+          float u3 = (float)h3 * 2.3283064365386963e-10f;
+          float g2 = g * g;
+          float c = (1.0f - g2) * rcp_small(fmaf(2.0f * g, u3, 1.0f - g));
+          float hgcos = fmaf(-c, c, 1.0f + g2) * rcp_small(2.0f * g);
+          float sn = sqrt_z(fmaf(-hgcos, hgcos, 1.0f));
+          dir = f3{fmaf(sn, circle.x, hgcos * dir.x), fmaf(sn, circle.y, hgcos * dir.y),
+                   fmaf(sn, circle.z, hgcos * dir.z)};
+          st = h3;
+        }
+        bounces++;
+      } else {
+        st = sw;  // null collision
+      }
+    }
+    uint2 px;  // textureStore(uRadiance, (radiance, 1)) (wgsl:161)
+    px.x = (uint32_t)f2h(rad.x) | ((uint32_t)f2h(rad.y) << 16);
+    px.y = (uint32_t)f2h(rad.z) | (0x3c00u << 16);
+    reinterpret_cast<uint2*>(rgba)[(size_t)y * P.R + x] = px;
+  }
+  const float w[kRgbPlanes] = {pos.x, pos.y, pos.z, dir.x, dir.y, dir.z, as_f(bounces), as_f(samples),
+                               tr.x, tr.y, tr.z, rad.x, rad.y, rad.z};
+#pragma unroll
+  for (uint32_t k = 0; k < kRgbPlanes; k++) ph[k * S + i] = w[k];
+}
+
 // --------------------------------------------------------- volume relayout
 // cell (cx,cy,cz) in [0,W]x[0,H]x[0,D] holds voxels clamp(c-1), clamp(c) per axis;
 // byte (dz*4 + dy*2 + dx) of the u64 = voxel (x0+dx, y0+dy, z0+dz).
@@ -876,6 +1036,21 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   }
 #undef VPT_LAUNCH_NB
 #undef VPT_LAUNCH
+  return hipGetLastError();
+}
+
+hipError_t launch_reset_rgb(const MarchParams& P, float* ph, hipStream_t s) {
+  hipLaunchKernelGGL(k_reset_rgb, dim3(march_blocks(P)), dim3(kBlock), 0, s, P, ph);
+  return hipGetLastError();
+}
+
+hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSeeds& PS, float* ph,
+                            const uint8_t* vol, const float4* tf, uint16_t* rgba, hipStream_t s) {
+  dim3 grid(tile_blocks(P, kMarchBlock));
+  if (layout == kLayoutCorner8)
+    hipLaunchKernelGGL((k_march_rgb<kLayoutCorner8>), grid, dim3(kMarchBlock), 0, s, PS, P, ph, vol, tf, rgba);
+  else
+    hipLaunchKernelGGL((k_march_rgb<kLayoutLinear>), grid, dim3(kMarchBlock), 0, s, PS, P, ph, vol, tf, rgba);
   return hipGetLastError();
 }
 

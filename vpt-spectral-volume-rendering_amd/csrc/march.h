@@ -32,6 +32,9 @@ enum : uint32_t { kLayoutLinear = 0, kLayoutCorner8 = 1 };
 enum Plane : uint32_t {
   kPx = 0, kPy, kPz, kDx, kDy, kDz, kBounces, kSamples, kBin, kLambda, kRad0, kNumPlanes = kRad0 + kMaxBins
 };
+// Planes of the RGB sibling's photon (Photon.wgsl): the first eight coincide.
+enum RgbPlane : uint32_t { kTr0 = 8, kRgbRad0 = 11, kRgbPlanes = 14 };
+constexpr uint32_t kRgbTfMax = 4096;  // TF texels staged in LDS (row 0, decoded float4)
 
 struct MarchParams {
   float m[16];           // mvpInverse, column-major
@@ -50,6 +53,9 @@ struct MarchParams {
   float min_lam, max_lam; // spectrum[1], spectrum[nb + 1] (wgsl:262-263)
   float xb[kMaxBins], yb[kMaxBins], zb[kMaxBins];  // CMF bin means (0 past nb)
   float light_dir[3];    // normalize(light_direction) (host-computed, IEEE)
+  float anisotropy;      // RGB sibling: the HG g uniform (MCMComputeRenderer.wgsl:140)
+  uint32_t tf_w;         // RGB sibling: TF width (texels of row 0 in LDS)
+  float env[4];          // RGB sibling: the 1x1 environment texel, unorm -> f32
   uint32_t light_iso;    // length(light_direction) < EPS
   uint32_t b_rows;       // TF blue channel column-invariant: use the LDS row table
   uint32_t sched;        // march tile mapping: 0 scheduled (TileSched flags), 1 raster

@@ -36,6 +36,7 @@ struct vptmcm {
   hipStream_t stream = nullptr;
   uint32_t R = 0, tiles_x = 0, n_tiles = 0, npad = 0;
   uint32_t layout = kLayoutLinear;
+  uint32_t kind = VPTMCM_RENDERER_SPECTRAL;
   uint32_t variant = 0;  // tuning knob (VPTMCM_MARCH_VARIANT), results identical
 
   float* photons = nullptr;    // kNumPlanes * npad words
@@ -50,6 +51,9 @@ struct vptmcm {
   uint8_t* tf_brow = nullptr;  // 256 anisotropy rows (valid when b_rows)
   uint32_t b_rows = 1;         // zero TF: column-invariant
   uint8_t* light = nullptr;    // 256 bytes
+  float4* tf_rgb = nullptr;    // RGB sibling: decoded TF row 0 (kRgbTfMax texels)
+  uint32_t tf_rgb_w = 0;
+  float env[4] = {1.0f, 1.0f, 1.0f, 1.0f};  // RGB sibling: 1x1 white (WebGPURenderingContext.js:97-108)
   uint8_t* sched = nullptr;    // tile schedule flags: [2][sched_flag_bytes(n_tiles)]
   uint32_t sched_cur = 0;      // which flag row the next march reads
 
@@ -102,6 +106,13 @@ struct vptmcm {
 namespace {
 
 const float kNoMatrix[16] = {};  // for launches that only read the non-camera fields
+
+// rgba8unorm-srgb decode (the sampler converts before filtering), in double,
+// rounded to f32; identical to the oracle's orc_srgb_to_linear
+float srgb_to_linear(uint8_t b) {
+  double v = b / 255.0;
+  return (float)(v <= 0.04045 ? v / 12.92 : std::pow((v + 0.055) / 1.055, 2.4));
+}
 
 // Robust-miss region of the march (MarchParams::robust, k_march's robust
 // path). In exact arithmetic a camera ray of pixel (sx, sy) runs from the
@@ -233,6 +244,9 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
     P.light_dir[2] = ld[2] * il;
   }
   P.b_rows = h->b_rows;
+  P.anisotropy = h->params.anisotropy;
+  P.tf_w = h->tf_rgb_w;
+  for (int k = 0; k < 4; k++) P.env[k] = h->env[k];
   float rb[4];
   P.robust = (P.blur == 0.0f && P.rcp_extinction > 0.0f && std::isfinite(P.rcp_extinction) &&
               robust_region(mvp, P.inv_res[0], rb)) ? 1u : 0u;
@@ -283,8 +297,11 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
   TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf};
   P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : 0u;
-  HIPCHK(h, launch_march(h->layout, h->variant, P, PS, T, h->photons, vol, h->tf_rg, h->tf_b4,
-                         h->tf_brow, h->light, h->rgba, h->stream));
+  if (h->kind == VPTMCM_RENDERER_RGB)
+    HIPCHK(h, launch_march_rgb(h->layout, P, PS, h->photons, vol, h->tf_rgb, h->rgba, h->stream));
+  else
+    HIPCHK(h, launch_march(h->layout, h->variant, P, PS, T, h->photons, vol, h->tf_rg, h->tf_b4,
+                           h->tf_brow, h->light, h->rgba, h->stream));
   h->sched_cur = c ^ 1u;
   if (ep) HIPCHK(h, hipEventRecord(ep->end, h->stream));
   return VPTMCM_OK;
@@ -324,6 +341,10 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
     g_create_error = "vptmcm_create: max_bins must be 12 (MAX_N_BINS)";
     return VPTMCM_EINVAL;
   }
+  if (cfg->renderer > VPTMCM_RENDERER_RGB) {
+    g_create_error = "vptmcm_create: unknown renderer kind";
+    return VPTMCM_EINVAL;
+  }
   if (cfg->volume_layout > VPTMCM_LAYOUT_CORNER8) {
     g_create_error = "vptmcm_create: unknown volume layout";
     return VPTMCM_EINVAL;
@@ -353,6 +374,7 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
     (void)hipGetDevice(&h->device);
   }
   h->layout = cfg->volume_layout;
+  h->kind = cfg->renderer;
   if (const char* v = getenv("VPTMCM_MARCH_VARIANT")) h->variant = (uint32_t)strtoul(v, nullptr, 0);
   h->R = cfg->resolution;
   h->tiles_x = (h->R + 7) / 8;
@@ -380,8 +402,13 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   CK(hipMemsetAsync(h->tf_brow, 0, 256, h->stream));
   CK(hipMalloc(&h->light, 256));
   CK(hipMemsetAsync(h->light, 0, 256, h->stream));
+  CK(hipMalloc(&h->tf_rgb, kRgbTfMax * sizeof(float4)));
   CK(hipMalloc(&h->sched, 2 * (size_t)sched_flag_bytes(h->n_tiles)));
   CK(hipMemsetAsync(h->sched, 0, 2 * (size_t)sched_flag_bytes(h->n_tiles), h->stream));
+  if (h->kind == VPTMCM_RENDERER_RGB) {  // WebGPUAbstractComputeRenderer.js:23-28
+    static const uint8_t kDefaultTf[8] = {255, 0, 0, 0, 255, 0, 0, 255};
+    if (vptmcm_set_transfer_function(h, kDefaultTf, 2, 1)) return fail(VPTMCM_EHIP);
+  }
   CK(hipStreamSynchronize(h->stream));
 #undef CK
   *out = h;
@@ -407,6 +434,7 @@ void vptmcm_destroy(vptmcm* h) {
   if (h->photons) (void)hipFree(h->photons);
   if (h->rgba) (void)hipFree(h->rgba);
   if (h->ldr) (void)hipFree(h->ldr);
+  if (h->tf_rgb) (void)hipFree(h->tf_rgb);
   if (h->tf_rg) (void)hipFree(h->tf_rg);
   if (h->tf_b4) (void)hipFree(h->tf_b4);
   if (h->tf_brow) (void)hipFree(h->tf_brow);
@@ -550,6 +578,37 @@ int vptmcm_set_spectrum(vptmcm* h, const float* buf) {
   return VPTMCM_OK;
 }
 
+int vptmcm_set_transfer_function(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (h->kind != VPTMCM_RENDERER_RGB)
+    FAIL(h, VPTMCM_ESTATE, "set_transfer_function: the spectral renderer uses set_material_tf");
+  if (!rgba || width == 0 || height == 0 || width > kRgbTfMax)
+    FAIL(h, VPTMCM_EINVAL, "set_transfer_function: need 1 <= width <= %u, height >= 1", kRgbTfMax);
+  HIPCHK(h, hipSetDevice(h->device));
+  // the kernel samples at (density, 0): row 0 only (see MarchParams::tf_w); the
+  // rgba8unorm-srgb texel is decoded before filtering, alpha is linear
+  std::vector<float4> row(width);
+  for (uint32_t i = 0; i < width; i++) {
+    const uint8_t* t = rgba + 4 * (size_t)i;
+    row[i] = make_float4(srgb_to_linear(t[0]), srgb_to_linear(t[1]), srgb_to_linear(t[2]),
+                         (float)t[3] * kInv255);
+  }
+  HIPCHK(h, hipMemcpyAsync(h->tf_rgb, row.data(), width * sizeof(float4), hipMemcpyHostToDevice,
+                           h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->tf_rgb_w = width;
+  return VPTMCM_OK;
+}
+
+int vptmcm_set_environment(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!rgba || width != 1 || height != 1)
+    FAIL(h, VPTMCM_EINVAL, "set_environment: only the 1x1 environment of the rendering context "
+                           "(WebGPURenderingContext.js:97-108) is supported");
+  for (int k = 0; k < 4; k++) h->env[k] = (float)rgba[k] * kInv255;
+  return VPTMCM_OK;
+}
+
 int vptmcm_set_params(vptmcm* h, const vptmcm_params* p) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (!p) FAIL(h, VPTMCM_EINVAL, "set_params: null params");
@@ -564,7 +623,10 @@ int vptmcm_reset(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   if (!mvp) FAIL(h, VPTMCM_EINVAL, "reset: null matrix");
   HIPCHK(h, hipSetDevice(h->device));
   MarchParams P = make_params(h, mvp, seed_bits);
-  HIPCHK(h, launch_reset(P, h->photons, h->stream));
+  if (h->kind == VPTMCM_RENDERER_RGB)
+    HIPCHK(h, launch_reset_rgb(P, h->photons, h->stream));
+  else
+    HIPCHK(h, launch_reset(P, h->photons, h->stream));
   return VPTMCM_OK;
 }
 
@@ -639,6 +701,22 @@ int vptmcm_read_photons(vptmcm* h, void* out) {
                            h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   uint32_t* o = static_cast<uint32_t*>(out);
+  if (h->kind == VPTMCM_RENDERER_RGB) {  // struct Photon, Photon.wgsl: 64-B stride
+    for (uint32_t y = 0; y < h->R; y++)
+      for (uint32_t x = 0; x < h->R; x++) {
+        size_t i = (size_t)((y / 8) * h->tiles_x + x / 8) * 64 + (y % 8) * 8 + (x % 8);
+        uint32_t* w = o + ((size_t)y * h->R + x) * (VPTMCM_PHOTON_RGB_BYTES / 4);
+        for (int k = 0; k < 3; k++) w[k] = planes[(kPx + k) * (size_t)h->npad + i];
+        w[3] = planes[kBounces * (size_t)h->npad + i];
+        for (int k = 0; k < 3; k++) w[4 + k] = planes[(kDx + k) * (size_t)h->npad + i];
+        w[7] = planes[kSamples * (size_t)h->npad + i];
+        for (int k = 0; k < 3; k++) w[8 + k] = planes[(kTr0 + k) * (size_t)h->npad + i];
+        w[11] = 0u;
+        for (int k = 0; k < 3; k++) w[12 + k] = planes[(kRgbRad0 + k) * (size_t)h->npad + i];
+        w[15] = 0u;
+      }
+    return VPTMCM_OK;
+  }
   const uint32_t one = 0x3f800000u;
   for (uint32_t y = 0; y < h->R; y++)
     for (uint32_t x = 0; x < h->R; x++) {
@@ -663,7 +741,20 @@ int vptmcm_write_photons(vptmcm* h, const void* in) {
   HIPCHK(h, hipSetDevice(h->device));
   std::vector<uint32_t> planes((size_t)kNumPlanes * h->npad, 0u);
   const uint32_t* src = static_cast<const uint32_t*>(in);
-  for (uint32_t y = 0; y < h->R; y++)
+  if (h->kind == VPTMCM_RENDERER_RGB) {
+    for (uint32_t y = 0; y < h->R; y++)
+      for (uint32_t x = 0; x < h->R; x++) {
+        size_t i = (size_t)((y / 8) * h->tiles_x + x / 8) * 64 + (y % 8) * 8 + (x % 8);
+        const uint32_t* w = src + ((size_t)y * h->R + x) * (VPTMCM_PHOTON_RGB_BYTES / 4);
+        for (int k = 0; k < 3; k++) planes[(kPx + k) * (size_t)h->npad + i] = w[k];
+        planes[kBounces * (size_t)h->npad + i] = w[3];
+        for (int k = 0; k < 3; k++) planes[(kDx + k) * (size_t)h->npad + i] = w[4 + k];
+        planes[kSamples * (size_t)h->npad + i] = w[7];
+        for (int k = 0; k < 3; k++) planes[(kTr0 + k) * (size_t)h->npad + i] = w[8 + k];
+        for (int k = 0; k < 3; k++) planes[(kRgbRad0 + k) * (size_t)h->npad + i] = w[12 + k];
+      }
+  }
+  for (uint32_t y = 0; h->kind == VPTMCM_RENDERER_SPECTRAL && y < h->R; y++)
     for (uint32_t x = 0; x < h->R; x++) {
       size_t i = (size_t)((y / 8) * h->tiles_x + x / 8) * 64 + (y % 8) * 8 + (x % 8);
       const uint32_t* w = src + ((size_t)y * h->R + x) * (VPTMCM_PHOTON_BYTES / 4);

@@ -2,6 +2,7 @@
 // Public JS surface of the MI355X spectral MCM renderer.
 const { MCMSpectralComputeRenderer, native } = require('./MCMSpectralComputeRenderer');
 const { RendererFactory } = require('./RendererFactory');
+const { MCMComputeRenderer } = require('./MCMComputeRenderer');
 const { ArtisticToneMapper, ToneMapperFactory } = require('./ArtisticToneMapper');
 const { Camera, Transform, PerspectiveCamera, mvpInverse } = require('./Camera');
 const { PropertyBag } = require('./PropertyBag');
@@ -15,6 +16,6 @@ function createDevice(ordinal = 0, layout = 'corner8') {
 }
 
 module.exports = {
-  MCMSpectralComputeRenderer, RendererFactory, ArtisticToneMapper, ToneMapperFactory, Camera, Transform, PerspectiveCamera, mvpInverse,
+  MCMSpectralComputeRenderer, MCMComputeRenderer, RendererFactory, ArtisticToneMapper, ToneMapperFactory, Camera, Transform, PerspectiveCamera, mvpInverse,
   PropertyBag, BufferLoader, FileLoader, RAWReader, ZIPReader, BVPReader, ReaderFactory, Volume, spectrum, mat4, createDevice, native,
 };

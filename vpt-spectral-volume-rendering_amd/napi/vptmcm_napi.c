@@ -20,6 +20,7 @@
 
 typedef struct {
     vptmcm* h;
+    uint32_t photon_bytes; /* 144 spectral, 64 RGB */
 } handle_box;
 
 #define NAPI_OK(env, call)                                                   \
@@ -131,7 +132,7 @@ static void finalize_box(napi_env env, void* data, void* hint) {
     free(box);
 }
 
-/* create(resolution, device, layout) -> handle */
+/* create(resolution, device, layout[, renderer]) -> handle */
 static napi_value js_create(napi_env env, napi_callback_info info) {
     napi_value argv[3];
     if (get_args(env, info, 3, argv)) return NULL;
@@ -142,11 +143,22 @@ static napi_value js_create(napi_env env, napi_callback_info info) {
     napi_get_value_int32(env, argv[1], &dev);
     cfg.device = dev;
     cfg.volume_layout = get_u32(env, argv[2]);
+    cfg.renderer = VPTMCM_RENDERER_SPECTRAL;
+    {   /* optional 4th argument: renderer kind */
+        size_t argc = 4;
+        napi_value all[4];
+        if (napi_get_cb_info(env, info, &argc, all, NULL, NULL) == napi_ok && argc >= 4) {
+            napi_valuetype t;
+            napi_typeof(env, all[3], &t);
+            if (t == napi_number) cfg.renderer = get_u32(env, all[3]);
+        }
+    }
     vptmcm* h = NULL;
     int rc = vptmcm_create(&cfg, &h);
     if (rc) return throw_code(env, rc, vptmcm_last_error(NULL));
     handle_box* box = (handle_box*)malloc(sizeof *box);
     box->h = h;
+    box->photon_bytes = cfg.renderer == VPTMCM_RENDERER_RGB ? VPTMCM_PHOTON_RGB_BYTES : VPTMCM_PHOTON_BYTES;
     napi_value ext;
     NAPI_OK(env, napi_create_external(env, box, finalize_box, NULL, &ext));
     return ext;
@@ -303,6 +315,21 @@ static napi_value js_read_rgba16f(napi_env env, napi_callback_info info) {
     return check(env, h, vptmcm_read_rgba16f(h, p));
 }
 
+/* setTransferFunction(h, Uint8Array(w*h*4), w, h) / setEnvironment(h, Uint8Array(4), 1, 1) */
+static napi_value image_call(napi_env env, napi_callback_info info, int env_map) {
+    napi_value argv[4];
+    if (get_args(env, info, 4, argv)) return NULL;
+    vptmcm* h = get_handle(env, argv[0]);
+    if (!h) return NULL;
+    uint32_t w = get_u32(env, argv[2]), hh = get_u32(env, argv[3]);
+    const uint8_t* p = get_typed(env, argv[1], 1, (size_t)w * hh * 4, NULL);
+    if (!p) return NULL;
+    return check(env, h, env_map ? vptmcm_set_environment(h, p, w, hh)
+                                 : vptmcm_set_transfer_function(h, p, w, hh));
+}
+static napi_value js_set_transfer_function(napi_env env, napi_callback_info info) { return image_call(env, info, 0); }
+static napi_value js_set_environment(napi_env env, napi_callback_info info) { return image_call(env, info, 1); }
+
 /* tonemapArtistic(h, Float32Array[low, mid, high, saturation, gamma], Uint8Array(R*R*4), R) */
 static napi_value js_tonemap_artistic(napi_env env, napi_callback_info info) {
     napi_value argv[4];
@@ -317,14 +344,17 @@ static napi_value js_tonemap_artistic(napi_env env, napi_callback_info info) {
     return check(env, h, vptmcm_tonemap_artistic(h, params, out));
 }
 
-/* readPhotons(h, Uint8Array(R*R*144), R) / writePhotons(h, Uint8Array, R) */
+/* readPhotons(h, Uint8Array(R*R*stride), R) / writePhotons(h, Uint8Array, R);
+ * stride = 144 (spectral) or 64 (RGB), from the handle's renderer kind */
 static napi_value photons_call(napi_env env, napi_callback_info info, int write) {
     napi_value argv[3];
     if (get_args(env, info, 3, argv)) return NULL;
     vptmcm* h = get_handle(env, argv[0]);
     if (!h) return NULL;
+    handle_box* box = NULL;
+    napi_get_value_external(env, argv[0], (void**)&box);
     uint32_t R = get_u32(env, argv[2]);
-    uint8_t* p = get_typed(env, argv[1], 1, (size_t)R * R * VPTMCM_PHOTON_BYTES, NULL);
+    uint8_t* p = get_typed(env, argv[1], 1, (size_t)R * R * box->photon_bytes, NULL);
     if (!p) return NULL;
     return check(env, h, write ? vptmcm_write_photons(h, p) : vptmcm_read_photons(h, p));
 }
@@ -444,6 +474,8 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("readRGBA16F", js_read_rgba16f);
     EXPORT("readPhotons", js_read_photons);
     EXPORT("tonemapArtistic", js_tonemap_artistic);
+    EXPORT("setTransferFunction", js_set_transfer_function);
+    EXPORT("setEnvironment", js_set_environment);
     EXPORT("writePhotons", js_write_photons);
     EXPORT("enableKernelTiming", js_enable_kernel_timing);
     EXPORT("kernelTime", js_kernel_time);

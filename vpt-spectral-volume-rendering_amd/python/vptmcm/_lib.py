@@ -17,6 +17,8 @@ LIB_DIR = PKG / "lib"
 
 OK, EINVAL, EHIP, ESTATE, ENOMEM, ECOMM = 0, -1, -2, -3, -4, -5
 LAYOUT_LINEAR, LAYOUT_CORNER8 = 0, 1
+RENDERER_SPECTRAL, RENDERER_RGB = 0, 1
+PHOTON_RGB_BYTES = 64
 PHOTON_BYTES = 144
 MAX_BINS = 12
 
@@ -27,7 +29,7 @@ EXPORTS = [
     "vptmcm_set_material_tf", "vptmcm_set_light", "vptmcm_set_spectrum", "vptmcm_set_params",
     "vptmcm_reset", "vptmcm_render", "vptmcm_render_passes", "vptmcm_synchronize",
     "vptmcm_read_rgba16f", "vptmcm_read_photons", "vptmcm_write_photons",
-    "vptmcm_tonemap_artistic",
+    "vptmcm_tonemap_artistic", "vptmcm_set_transfer_function", "vptmcm_set_environment",
     "vptmcm_enable_kernel_timing", "vptmcm_kernel_time", "vptmcm_comm_unique_id",
     "vptmcm_comm_init", "vptmcm_comm_allreduce_radiance", "vptmcm_comm_read_composite",
     "vptmcm_comm_barrier", "vptmcm_comm_allreduce_host", "vptmcm_debug_eval",
@@ -37,7 +39,7 @@ EXPORTS = [
 
 class Config(C.Structure):
     _fields_ = [("resolution", C.c_uint32), ("max_bins", C.c_uint32), ("device", C.c_int32),
-                ("volume_layout", C.c_uint32)]
+                ("volume_layout", C.c_uint32), ("renderer", C.c_uint32)]
 
 
 class Params(C.Structure):
@@ -94,6 +96,8 @@ def load() -> C.CDLL:
         "vptmcm_synchronize": (C.c_int, [vp]),
         "vptmcm_read_rgba16f": (C.c_int, [vp, vp]),
         "vptmcm_tonemap_artistic": (C.c_int, [vp, vp, vp]),
+        "vptmcm_set_transfer_function": (C.c_int, [vp, vp, C.c_uint32, C.c_uint32]),
+        "vptmcm_set_environment": (C.c_int, [vp, vp, C.c_uint32, C.c_uint32]),
         "vptmcm_read_photons": (C.c_int, [vp, vp]),
         "vptmcm_write_photons": (C.c_int, [vp, vp]),
         "vptmcm_enable_kernel_timing": (C.c_int, [vp, C.c_int]),
@@ -137,9 +141,11 @@ def mat_f32(mvp) -> np.ndarray:
 class Renderer:
     """Thin handle wrapper (one HIP device, one stream)."""
 
-    def __init__(self, resolution: int = 512, device: int = -1, layout: int = LAYOUT_CORNER8):
+    def __init__(self, resolution: int = 512, device: int = -1, layout: int = LAYOUT_CORNER8,
+                 renderer: int = RENDERER_SPECTRAL):
         self.L = load()
-        cfg = Config(resolution, MAX_BINS, device, layout)
+        cfg = Config(resolution, MAX_BINS, device, layout, renderer)
+        self.kind = renderer
         h = C.c_void_p()
         rc = self.L.vptmcm_create(C.byref(cfg), C.byref(h))
         if rc != OK:
@@ -239,15 +245,29 @@ class Renderer:
         self._ck(self.L.vptmcm_tonemap_artistic(self.h, _ptr(p), _ptr(out)))
         return out
 
+    def _photon_words(self) -> int:
+        return (PHOTON_RGB_BYTES if self.kind == RENDERER_RGB else PHOTON_BYTES) // 4
+
+    def set_transfer_function(self, rgba: np.ndarray) -> None:
+        """RGB renderer: rgba8unorm-srgb TF image [H, W, 4] (setTransferFunction)."""
+        t = np.ascontiguousarray(rgba, dtype=np.uint8)
+        self._ck(self.L.vptmcm_set_transfer_function(self.h, _ptr(t), t.shape[1], t.shape[0]))
+
+    def set_environment(self, rgba) -> None:
+        """RGB renderer: the 1x1 environment texel (rgba8unorm)."""
+        t = np.ascontiguousarray(np.asarray(rgba, dtype=np.uint8).reshape(4))
+        self._ck(self.L.vptmcm_set_environment(self.h, _ptr(t), 1, 1))
+
     def read_photons(self) -> np.ndarray:
-        """(R*R, 36) uint32 words in the reference's 144-B PhotonSpectral layout."""
-        out = np.empty((self.R * self.R, PHOTON_BYTES // 4), np.uint32)
+        """(R*R, words) uint32 in the reference's layout: 144-B PhotonSpectral
+        (36 words) or, for the RGB renderer, 64-B Photon (16 words)."""
+        out = np.empty((self.R * self.R, self._photon_words()), np.uint32)
         self._ck(self.L.vptmcm_read_photons(self.h, _ptr(out)))
         return out
 
     def write_photons(self, words: np.ndarray) -> None:
         w = np.ascontiguousarray(words, dtype=np.uint32)
-        assert w.size == self.R * self.R * PHOTON_BYTES // 4
+        assert w.size == self.R * self.R * self._photon_words()
         self._ck(self.L.vptmcm_write_photons(self.h, _ptr(w)))
 
     # -- measurement
