@@ -147,10 +147,11 @@ __device__ __forceinline__ uint32_t bin_of(const MarchParams& P, float lambda) {
     return (uint32_t)k;
   }
   if (P.bins_sorted) {
+    // uniform trip count (nb - 1): no per-bin masks held live across the
+    // march (they used to spill 22 SGPRs into VGPR lanes)
     bin = 0u;
-#pragma unroll
-    for (uint32_t i = 1u; i < (uint32_t)kMaxBins; i++)
-      bin += (i < P.nb && !(lambda < P.lam[i])) ? 1u : 0u;
+    const uint32_t nb = __builtin_amdgcn_readfirstlane(P.nb);
+    for (uint32_t i = 1u; i < nb; i++) bin += !(lambda < P.lam[i]) ? 1u : 0u;
   } else {
     bin = P.nb - 1u;
     for (uint32_t i = 1u; i < P.nb; i++) {
