@@ -576,6 +576,13 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         rc.dir = f3{dx, dy, 1.0f};
         rc.lambda = p.lambda;
         rc.bin = p.bin;
+      } else if (KO(5) | KO(6) | KO(7) | KO(8)) {  // finer knock-outs of the candidate's parts
+        f3 d0 = KO(6) ? f3{dx, dy, 1.0f} : ray_dir_from_draws(P, sx, sy, from, h3, h4);
+        rc.dir = d0;
+        rc.pos = KO(5) ? from : ray_start(from, d0);
+        rc.lambda = lambda_of(P, h5);
+        rc.bin = KO(8) ? p.bin : bin_of(P, rc.lambda);
+        if (!KO(7)) wcr = wave_const(rc.lambda, s_light);
       } else {
         reset_from_draws(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5);
         wcr = wave_const(rc.lambda, s_light);
