@@ -356,3 +356,40 @@ def test_camera_change_without_reset():
     assert_photons_equal(gpu.read_photons(), cpu.photons, "camera change")
     assert_rgba_equal(gpu.read_rgba16f(), want, "camera change")
     gpu.close()
+
+
+def test_tiny_resolutions_and_empty_volume():
+    """R = 1, 2, 3 (one partial tile, pixel centres on the screen axes for odd R:
+    the near point is then not hoisted) and an all-zero volume."""
+    mvp = cf.default_mvp_inverse()
+    seeds = cf.seed_stream(4, start=5)
+    for R in (1, 2, 3):
+        gpu, cpu = make_pair(R, cf.sphere_in_cube(16), cf.tf_spectral(), ext=8.0)
+        run_and_compare(gpu, cpu, mvp, seeds, f"R={R}")
+        gpu.close()
+    gpu, cpu = make_pair(16, np.zeros((8, 8, 8), np.uint8), cf.tf_spectral(), ext=8.0)
+    run_and_compare(gpu, cpu, mvp, seeds, "empty volume")
+    gpu.close()
+
+
+def test_large_frame_rows_against_oracle():
+    """R = 2048 (65536 tiles: the raster tile mapping, 4.2 M photons): a band of
+    rows through the cube and the image edge, checked against the oracle's
+    row-restricted run after two fused passes."""
+    R = 2048
+    vol = cf.fbm_volume(128, 99)
+    gpu, cpu = make_pair(R, vol, cf.tf_spectral(), ext=32.0)
+    mvp = cf.default_mvp_inverse()
+    seeds = cf.seed_stream(3, start=9)
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0], nthreads=16)
+    gpu.render_passes(mvp, seeds[1:])
+    for s in seeds[1:]:
+        _, want = cpu.render(mvp, s, nthreads=16, rows=(1000, 1040))
+    got = gpu.read_photons().reshape(R, R, -1)
+    exp = cpu.photons.reshape(R, R, -1)
+    for y0, y1 in ((1000, 1040),):
+        assert_photons_equal(got[y0:y1].reshape(-1, got.shape[-1]), exp[y0:y1].reshape(-1, exp.shape[-1]),
+                             f"R=2048 rows {y0}:{y1}")
+        assert_rgba_equal(gpu.read_rgba16f()[y0:y1], want[y0:y1], f"R=2048 rows {y0}:{y1}")
+    gpu.close()
