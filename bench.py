@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--extinction", type=float, default=32.0)
     ap.add_argument("--layout", choices=["corner8", "linear"], default="corner8")
     ap.add_argument("--tf", choices=["spectral", "grey", "zero"], default="spectral")
+    ap.add_argument("--camera", choices=["default", "near", "orbit", "orbit_tilted"],
+                    default="default", help="golden camera pose (non-default: analysis only)")
     ap.add_argument("--fuse", type=int, default=16,
                     help="passes per march launch (render_passes; photon state stays in "
                          "registers between them, every pass stores its image); 1 = one launch "
@@ -107,7 +109,7 @@ def main():
     tf = {"spectral": cf.tf_spectral, "grey": cf.tf_grey, "zero": cf.tf_zero}[a.tf]()
     spd, ldir = cf.light_default()
     spec = cf.spectrum_buffer("12")
-    mvp = cf.default_mvp_inverse()
+    mvp = cf.default_mvp_inverse() if a.camera == "default" else cf.golden_mvp(a.camera)
 
     # VPTMCM_BENCH_DEVICE pins every rank to one ordinal (rehearsing the N > 1
     # path on a one-GPU box); the default is one GPU per local rank
@@ -222,7 +224,7 @@ def main():
             "config": {
                 "workload": f"C{'4' if multi else '3'}: {a.volume}^3 fBm volume (seed 512), spectral TF "
                             f"(HG g=0.702), R={R}, S={S}, 12 bins, extinction {a.extinction}, "
-                            "default camera",
+                            f"{a.camera} camera",
                 "resolution": R, "photon_steps_per_pass": S, "volume": a.volume,
                 "volume_layout": a.layout, "passes_per_launch": F,
                 "parallelism": (f"photon-parallel replicas x{world}, RCCL all-reduce of (rgb*n, n) "

@@ -18,6 +18,9 @@
 #ifndef VPT_ROBUST
 #define VPT_ROBUST 1  // robust-miss background path
 #endif
+#ifndef VPT_OH_PEND
+#define VPT_OH_PEND 1  // byte one-hot pending bin, zero-weight apply
+#endif
 #ifndef VPT_PRIO
 #define VPT_PRIO 1  // s_setprio level of volume waves (0 = off); 11 % faster passes
 #endif
@@ -457,8 +460,46 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     // shadow (it only touches the radiance bins, applied in the same order).
     float pend_n = 0.0f, pend_l = 0.0f;
     uint32_t pend_bin = 0u;
+#if VPT_OH_PEND
+    // The pending bin as a byte one-hot: byte (bin & 3) of word bin >> 2 is 1,
+    // so each bin's 0/1 factor is one v_cvt_f32_ubyteN (no per-bin compare
+    // masks held in SGPRs). 0xffffffff (no bins) sets no byte.
+    uint32_t pend_oh[3] = {0u, 0u, 0u};
+    auto set_pending = [&](float n, float l, uint32_t bin) {
+      pend_n = n;
+      pend_l = l;
+      const uint32_t one = 1u << ((bin & 3u) << 3), wi = bin >> 2;
+      pend_oh[0] = wi == 0u ? one : 0u;
+      pend_oh[1] = wi == 1u ? one : 0u;
+      pend_oh[2] = wi == 2u ? one : 0u;
+    };
+#else
+    auto set_pending = [&](float n, float l, uint32_t bin) {
+      pend_n = n;
+      pend_l = l;
+      pend_bin = bin;
+    };
+#endif
     auto apply_pending = [&]() {
-#if VPT_BF_PEND
+#if VPT_OH_PEND
+      // Branch-free with a zero weight for lanes without a pending sample:
+      // fma(d, +0, r) == r for every finite r, and the radiance bins are
+      // finite in every state the march produces (convex combinations of
+      // finite light samples), so no per-bin select is needed. The target
+      // difference fma(oh, l, -r) is RN(l - r) for the pending bin and -r
+      // (exact) elsewhere: the same values as (tgt - r).
+      const bool on = pend_n != 0.0f;
+      const float inv = on ? rcp_in_range(on ? pend_n : 1.0f) : 0.0f;
+#pragma unroll
+      for (int b = 0; b < kMaxBins; b++) {
+        if (NBF || (uint32_t)b < P.nb) {
+          const float oh = (float)((pend_oh[b >> 2] >> ((b & 3) * 8)) & 0xffu);
+          p.rad[b] = fmaf(fmaf(oh, pend_l, -p.rad[b]), inv, p.rad[b]);
+        }
+      }
+      pend_n = 0.0f;
+      pend_oh[0] = pend_oh[1] = pend_oh[2] = 0u;
+#elif VPT_BF_PEND
       // Branch-free: every lane runs the update and lanes without a pending
       // sample keep their old bins through one shared select per bin (no
       // exec-mask split, no phi copies). pend_n is a sample count >= 1, so
@@ -485,9 +526,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     // reset candidate (drawn from h1..h5) and continue from state h5
     auto terminate = [&](float rad, const Photon& rc) {
       p.samples++;
-      pend_n = (float)p.samples;
-      pend_l = rad;
-      pend_bin = p.bin;
+      set_pending((float)p.samples, rad, p.bin);
       p.pos = rc.pos;
       p.dir = rc.dir;
       p.bounces = 0u;
@@ -509,9 +548,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         uint32_t h1 = pcg_hash(sw), h2 = pcg_hash(h1), h3 = pcg_hash(h2);
         uint32_t h4 = pcg_hash(h3), h5 = pcg_hash(h4);
         p.samples++;
-        pend_n = (float)p.samples;
-        pend_l = exit_radiance(P, p.dir, wc);
-        pend_bin = p.bin;
+        set_pending((float)p.samples, exit_radiance(P, p.dir, wc), p.bin);
         p.dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
         p.bounces = 0u;
         p.lambda = lambda_of(P, h5);

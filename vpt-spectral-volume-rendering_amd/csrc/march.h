@@ -143,8 +143,12 @@ __device__ __forceinline__ uint32_t bin_of(const MarchParams& P, float lambda) {
     float kf = (float)k;
     float lo = fmaf(kf, P.bin_w, P.lam[0]);
     float hi = fmaf(kf + 1.0f, P.bin_w, P.lam[0]);
-    k = (lambda < lo) ? k - 1 : ((!(lambda < hi) && k + 1 < (int)P.nb) ? k + 1 : k);
-    return (uint32_t)k;
+    // (lambda < lo) ? k - 1 : (!(lambda < hi) && k + 1 < nb) ? k + 1 : k,
+    // as arithmetic on the compare bits (the ternary chain compiles to
+    // exec-mask branches)
+    const bool dn = lambda < lo;
+    const bool up = !(lambda < hi) & (k + 1 < (int)P.nb) & !dn;
+    return (uint32_t)(k - (int)dn + (int)up);
   }
   if (P.bins_sorted) {
     // uniform trip count (nb - 1): no per-bin masks held live across the

@@ -42,13 +42,35 @@ __device__ __forceinline__ float smax(float a, float b) { return (b > a || a != 
 __device__ __forceinline__ float rcp_slow(float x) { return 1.0f / x; }
 __device__ __forceinline__ float sqrt_slow(float x) { return __builtin_sqrtf(x); }
 
+// Rare-input fix-up as a wave-uniform branch: one compare into an SGPR mask
+// and a scalar branch on it, instead of an exec-mask region (saveexec + the
+// exec restore, whose hazards cost ~2x a plain instruction each). Inside the
+// branch the slow value is selected per lane.
+#ifndef VPT_UNIFORM_GUARDS
+#define VPT_UNIFORM_GUARDS 1
+#endif
+#if VPT_UNIFORM_GUARDS
+#define VPT_FIXUP(bad, y, slow)                                                  \
+  do {                                                                           \
+    const bool _bad = (bad);                                                     \
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(_bad) != 0ull, 0)) {        \
+      (y) = _bad ? (slow) : (y);                                                 \
+    }                                                                            \
+  } while (0)
+#else
+#define VPT_FIXUP(bad, y, slow)                     \
+  do {                                              \
+    if (__builtin_expect((bad), 0)) (y) = (slow);   \
+  } while (0)
+#endif
+
 // RN(1/x): v_rcp_f32 + one Newton step is exact for biased exponent 1..252.
 __device__ __forceinline__ float rcp_cr(float x) {
   float y = __builtin_amdgcn_rcpf(x);
   float e = __builtin_fmaf(-x, y, 1.0f);
   y = __builtin_fmaf(e, y, y);
   uint32_t ex = (__float_as_uint(x) >> 23) & 0xffu;
-  if (__builtin_expect(ex - 1u >= 252u, 0)) y = rcp_slow(x);
+  VPT_FIXUP(ex - 1u >= 252u, y, rcp_slow(x));
   return y;
 }
 
@@ -66,7 +88,7 @@ __device__ __forceinline__ float rcp_in_range(float x) {
 // with an abs modifier detects (vs the 3-instruction exponent range test).
 __device__ __forceinline__ float rcp_small(float x) {
   float y = rcp_in_range(x);
-  if (__builtin_expect(!(__builtin_fabsf(x) >= 1.17549435e-38f), 0)) y = rcp_slow(x);
+  VPT_FIXUP(!(__builtin_fabsf(x) >= 1.17549435e-38f), y, rcp_slow(x));
   return y;
 }
 
@@ -78,7 +100,7 @@ __device__ __forceinline__ float sqrt_cr(float x) {
   float h = 0.5f * __builtin_amdgcn_rsqf(x);
   s = __builtin_fmaf(e, h, s);
   uint32_t ex = __float_as_uint(x) >> 23;  // sign bit included: negatives excluded
-  if (__builtin_expect(ex - 32u > 222u, 0)) s = sqrt_slow(x);
+  VPT_FIXUP(ex - 32u > 222u, s, sqrt_slow(x));
   return s;
 }
 
