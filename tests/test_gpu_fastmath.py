@@ -22,6 +22,8 @@ ALL = (0, 1 << 32)
     (10, "rcp_small: RN(1/x) for finite |x| < 2^126 and NaN", *ALL),
     (11, "sqrt_z: RN(sqrt x) for +-0, NaN, normal x < 0, x > 0 with exponent 32..254", *ALL),
     (12, "rcp_in_range: RN(1/x) for exponent 1..252", *ALL),
+    (15, "clampc_q (v_max/v_min) == clampc for non-signalling x", *ALL),
+    (16, "v_min/v_max/v_max3 == smin/smax chains (quiet, no +-0 pair)", *ALL),
 ])
 def test_fast_sequences_are_correctly_rounded(fn, name, lo, n):
     with vptmcm.Renderer(8, device=0) as g:

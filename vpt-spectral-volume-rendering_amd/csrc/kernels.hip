@@ -21,6 +21,9 @@
 #ifndef VPT_OH_PEND
 #define VPT_OH_PEND 1  // byte one-hot pending bin, zero-weight apply
 #endif
+#ifndef VPT_SLAB_HW
+#define VPT_SLAB_HW 1  // hardware min/max slab test for generic fixed near points
+#endif
 #ifndef VPT_PRIO
 #define VPT_PRIO 1  // s_setprio level of volume waves (0 = off); 11 % faster passes
 #endif
@@ -104,9 +107,10 @@ template <uint32_t L>
 __device__ __forceinline__ VolTap vol_fetch(const MarchParams& P, const uint8_t* __restrict__ vol,
                                             f3 q) {
   VolTap t;
-  int ix = axis_floor(q.x, (float)P.W, &t.fx);
-  int iy = axis_floor(q.y, (float)P.H, &t.fy);
-  int iz = axis_floor(q.z, (float)P.D, &t.fz);
+  // q is an arithmetic result (the advanced position), never a signalling NaN
+  int ix = axis_floor_q(q.x, (float)P.W, &t.fx);
+  int iy = axis_floor_q(q.y, (float)P.H, &t.fy);
+  int iz = axis_floor_q(q.z, (float)P.D, &t.fz);
   if constexpr (L == kLayoutCorner8) {
     const uint32_t W1 = P.W + 1u, H1 = P.H + 1u;
     uint32_t cx = (uint32_t)(clampi(ix + 1, (int)P.W));
@@ -428,6 +432,11 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   f3 from{0.0f, 0.0f, 0.0f};
   bool fixed = near_fixed(P, sx, sy, from);
   WaveConst wc = wave_const(p.lambda, s_light);
+#if VPT_SLAB_HW
+  const bool slab_hw = __builtin_amdgcn_ballot_w64(!slab_generic(fixed, from)) == 0ull;
+#else
+  const bool slab_hw = false;
+#endif
 
 #if VPT_PRIO
   // Waves whose tile entered the volume last pass are the long ones; they win
@@ -580,7 +589,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         float dx = 0.0f, dy = 0.0f;
         if (!fixed) disk_of(h1, h2, dx, dy);
         Photon rc;
-        reset_from_draws(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5);
+        reset_from_draws(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw);
         terminate(exit_radiance(P, p.dir, wc), rc);
         wc = wave_const(rc.lambda, s_light);
         st = h5;
@@ -621,7 +630,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         rc.bin = KO(8) ? p.bin : bin_of(P, rc.lambda);
         if (!KO(7)) wcr = wave_const(rc.lambda, s_light);
       } else {
-        reset_from_draws(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5);
+        reset_from_draws(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw);
         wcr = wave_const(rc.lambda, s_light);
       }
       STAMP(2);  // speculative reset candidate
@@ -635,9 +644,9 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       STAMP(3);  // speculative scatter half
 
       // sample_volume_color (wgsl:75-80) -> probabilities (wgsl:132-139)
-      float d = vol_filter(vt);
+      float d = vol_filter(vt);  // in [0, 1]: a lerp of bytes times RN(1/255)
       float fr;
-      int ir = axis_floor(d, 256.0f, &fr);
+      int ir = axis_floor_in(d, 256.0f, &fr);
       uint32_t b4 = 0u;
       if (!P.b_rows) b4 = tf_b4[(uint32_t)clampi(ir + 1, 256) * kTfCells + (uint32_t)wc.cc];
       const uint32_t ri0 = (uint32_t)clampi(ir, 255), ri1 = (uint32_t)clampi(ir + 1, 255);
@@ -1215,6 +1224,12 @@ __device__ __forceinline__ float cand_eval(int fn, float x, float* ref) {
       uint32_t ex = (__float_as_uint(x) >> 23) & 0xffu;
       return (ex >= 1u && ex <= 252u) ? rcp_in_range(x) : *ref;
     }
+    case 15: {  // clampc_q (hardware max/min) vs clampc on non-signalling inputs
+      *ref = clampc(x);
+      uint32_t a = __float_as_uint(x) & 0x7fffffffu;
+      bool snan = a > 0x7f800000u && !(a & 0x00400000u);
+      return snan ? *ref : clampc_q(x);
+    }
     case 5: {  // v_sqrt_f32 + one Newton correction using the rsq estimate
       *ref = __builtin_sqrtf(x);
       float s0 = __builtin_amdgcn_sqrtf(x);
@@ -1235,7 +1250,32 @@ __global__ void k_verify(int fn, const MarchParams P, uint32_t lo, uint32_t n,
   Pc.bins_uniform = 0u;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
     bool ok;
-    if (fn == 14) {  // query: is the arithmetic bin path selected for this spectrum?
+    if (fn == 16) {  // hw_min/hw_max/hw_max3 vs smin/smax for x against special and nearby y
+      const float x = __uint_as_float(lo + k);
+      const uint32_t xb = lo + k;
+      const float ys[] = {__uint_as_float(0x7fc00000u), __uint_as_float(0xffc00123u),
+                          __builtin_inff(), -__builtin_inff(), 1.0f, -1.0f, 0.0f, -0.0f,
+                          1.17549435e-38f, __uint_as_float(1u), __uint_as_float(0x80000001u),
+                          x, -x, __uint_as_float(xb + 1u), __uint_as_float(xb - 1u),
+                          __uint_as_float(pcg_hash(xb)), __uint_as_float(pcg_hash(xb) | 0x7f800000u)};
+      auto quiet = [](float v) {
+        uint32_t a = __float_as_uint(v) & 0x7fffffffu;
+        return !(a > 0x7f800000u && !(a & 0x00400000u));
+      };
+      auto zpair = [](float a, float b) { return a == 0.0f && b == 0.0f && __float_as_uint(a) != __float_as_uint(b); };
+      ok = true;
+      if (quiet(x)) {
+        for (float y : ys) {
+          if (!quiet(y)) continue;
+          if (!zpair(x, y)) {
+            ok = ok && same_bits(hw_min(x, y), smin(x, y)) && same_bits(hw_max(x, y), smax(x, y));
+          }
+          const float z = __uint_as_float(pcg_hash(__float_as_uint(y) ^ xb));
+          if (quiet(z) && !zpair(x, y) && !zpair(smax(x, y), z))
+            ok = ok && same_bits(hw_max3(x, y, z), smax(smax(x, y), z));
+        }
+      }
+    } else if (fn == 14) {  // query: is the arithmetic bin path selected for this spectrum?
       ok = P.bins_uniform != 0u;
     } else if (fn == 13) {  // bin_of's arithmetic path vs the count, for lambda of every h5
       float lambda = fmaf((float)(lo + k) * 2.3283064365386963e-10f, P.max_lam - P.min_lam, P.min_lam);

@@ -227,6 +227,23 @@ __device__ __forceinline__ f3 ray_dir_from_draws(const MarchParams& P, float sx,
                     fmaf(fmaf(q1, 2.0f, -1.0f), P.inv_res[1], sy), 1.0f);
   return norm3(f3{to.x - from.x, to.y - from.y, to.z - from.z});
 }
+// Start point on the ray with hardware min/max3: valid when no slab distance
+// is zero, i.e. no coordinate of `from` is exactly 0 or 1 (then every
+// (c - from)*RN(1/d) is a non-zero number, an infinity or a quiet NaN, and
+// v_min/v_max/v_max3 return what smin/smax do; see hw_min).
+__device__ __forceinline__ f3 ray_start_hw(f3 from, f3 dir) {
+  float rx = rcp_small(dir.x), ry = rcp_small(dir.y), rz = rcp_small(dir.z);
+  float t1x = hw_min((0.0f - from.x) * rx, (1.0f - from.x) * rx);
+  float t1y = hw_min((0.0f - from.y) * ry, (1.0f - from.y) * ry);
+  float t1z = hw_min((0.0f - from.z) * rz, (1.0f - from.z) * rz);
+  float tn = hw_max(hw_max3(t1x, t1y, t1z), 0.0f);
+  return f3{fmaf(tn, dir.x, from.x), fmaf(tn, dir.y, from.y), fmaf(tn, dir.z, from.z)};
+}
+// A lane whose near point is fixed and has no coordinate equal to 0 or 1.
+__device__ __forceinline__ bool slab_generic(bool fixed_from, f3 from) {
+  return fixed_from && from.x != 0.0f && from.x != 1.0f && from.y != 0.0f && from.y != 1.0f &&
+         from.z != 0.0f && from.z != 1.0f;
+}
 // Start point on the ray: from + max(tnear, 0) * dir (intersectCube.wgsl, wgsl:254-256).
 __device__ __forceinline__ f3 ray_start(f3 from, f3 dir) {
   float rx = rcp_small(dir.x), ry = rcp_small(dir.y), rz = rcp_small(dir.z);
@@ -243,10 +260,14 @@ __device__ __forceinline__ float lambda_of(const MarchParams& P, uint32_t h5) {
 
 __device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p, float sx, float sy,
                                                  bool fixed_from, f3 from, float dx, float dy,
-                                                 uint32_t h3, uint32_t h4, uint32_t h5) {
+                                                 uint32_t h3, uint32_t h4, uint32_t h5,
+                                                 bool slab_hw = false) {
   if (!fixed_from) from = unproject(P.m, fmaf(dx, P.blur, sx), fmaf(dy, P.blur, sy), -1.0f);
   p.dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
-  p.pos = ray_start(from, p.dir);
+  if (slab_hw)  // wave-uniform: every lane's from is slab_generic
+    p.pos = ray_start_hw(from, p.dir);
+  else
+    p.pos = ray_start(from, p.dir);
   p.lambda = lambda_of(P, h5);
   p.bin = bin_of(P, p.lambda);
 }

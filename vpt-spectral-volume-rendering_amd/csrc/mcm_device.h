@@ -237,6 +237,50 @@ __device__ __forceinline__ int axis_floor(float u, float n, float* f) {
   *f = x - fl;
   return (int)fl;
 }
+// clampc for a quiet (arithmetic-result) input: v_max_f32 then v_min_f32
+// with IEEE-mode NaN handling (a quiet NaN yields the other operand, so NaN
+// -> -1 like clampc). Exact equality with clampc on every non-signalling bit
+// pattern is proven exhaustively (tests/test_gpu_fastmath.py, fn 15). The
+// asm keeps the backend from adding canonicalising v_max before fmaxf/fminf.
+__device__ __forceinline__ float clampc_q(float u) {
+  float r;
+  asm("v_max_f32 %0, -1.0, %1\n\tv_min_f32 %0, 2.0, %0" : "=&v"(r) : "v"(u));
+  return r;
+}
+__device__ __forceinline__ int axis_floor_q(float u, float n, float* f) {
+  float x = fmaf(clampc_q(u), n, -0.5f);
+  float fl = floorf(x);
+  *f = x - fl;
+  return (int)fl;
+}
+// axis_floor for u known to lie in [-1, 2] (e.g. a filtered texel value in
+// [0, 1]): clampc is the identity there.
+__device__ __forceinline__ int axis_floor_in(float u, float n, float* f) {
+  float x = fmaf(u, n, -0.5f);
+  float fl = floorf(x);
+  *f = x - fl;
+  return (int)fl;
+}
+// Hardware min/max (IEEE minNum/maxNum). They equal smin/smax whenever no
+// operand is a signalling NaN and the operands are not a (+0, -0) pair
+// (fn 16 checks the pairing rule over every bit pattern of one operand
+// against special and neighbouring values of the other).
+__device__ __forceinline__ float hw_min(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float hw_max(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float hw_max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 __device__ __forceinline__ int clampi(int i, int hi) { return i < 0 ? 0 : (i > hi ? hi : i); }
 __device__ __forceinline__ float lerp(float a, float b, float f) { return fmaf(f, b - a, a); }
 
