@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--unfused-steps", type=int, default=64,
                     help="passes of a second timed region at one launch per pass (reported "
                          "as 'unfused'; 0 = skip; N = 1 only)")
+    ap.add_argument("--no-timing", action="store_true",
+                    help="diagnostics: no per-launch kernel timestamps (wall clock only; the "
+                         "roofline fields are then null)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="budget of the CPU-oracle baseline (0 = skip)")
     ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "pmc_traffic.json"),
@@ -158,7 +161,7 @@ def main():
         r.barrier()
 
     # ---- timed region: K passes (+ composites), bracketed by barrier + sync
-    r.enable_kernel_timing(True)
+    r.enable_kernel_timing(not a.no_timing)
     t0 = time.perf_counter()
     launches = passes(1 + a.warmup, a.steps)
     r.synchronize()
@@ -168,6 +171,8 @@ def main():
     if multi:
         r.barrier()
     kern_ms, n_launch = r.kernel_time()
+    if a.no_timing:
+        kern_ms, n_launch = float("nan"), len(launches)
     assert n_launch == len(launches), (n_launch, len(launches))
     vals = np.array([el, kern_ms])
     if multi:
@@ -177,8 +182,11 @@ def main():
     photon_steps = world * R * R * S * a.steps
     value = photon_steps / el_max / 1e6
     # roofline of the march kernel: the algorithmic bytes its launches
-    # materialise over their summed duration (= bytes per launch / average
-    # launch duration for equal launches)
+    # materialise over the GPU time of the timed region, stamped by HIP events
+    # on the renderer's stream (begin = the first launch's dispatch, end = a
+    # marker behind the last launch); for equal launches this is bytes per
+    # launch / average launch duration, the inter-launch gaps included
+    # (conservative: rocprof's per-kernel average is slightly lower)
     alg_bytes = sum(cf.algorithmic_bytes_per_launch(R, S, n) for n in launches)
     achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
     kern_avg_ms = kern_ms_max / len(launches)
@@ -189,12 +197,14 @@ def main():
     unfused = None
     if n_unfused > 0:
         r.synchronize()
-        r.enable_kernel_timing(True)  # restart the launch timings
+        r.enable_kernel_timing(not a.no_timing)  # restart the launch timings
         t1 = time.perf_counter()
         ul = passes(1 + a.warmup + a.steps, n_unfused, F=1)
         r.synchronize()
         el1 = time.perf_counter() - t1
         uk_ms, un = r.kernel_time()
+        if a.no_timing:
+            uk_ms, un = float("nan"), len(ul)
         assert un == len(ul)
         ub = cf.algorithmic_bytes_per_launch(R, S, 1)
         ua = ub * un / (uk_ms * 1e-3) / 1e9

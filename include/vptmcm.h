@@ -191,9 +191,13 @@ int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out
 
 /* ---- measurement ---------------------------------------------------------- */
 
-/* When enabled, every march launch is bracketed by HIP events on the
- * handle's stream; vptmcm_kernel_time returns the summed elapsed time (ms)
- * and launch count since the last enable, and synchronises. */
+/* When enabled, the march launches from here on form one timed region on the
+ * handle's stream: the first launch stamps the begin event from its own
+ * dispatch packet, vptmcm_synchronize (or vptmcm_kernel_time) enqueues the end
+ * event behind the last one. vptmcm_kernel_time returns the region's elapsed
+ * GPU time (ms; launch gaps included, so launch-average durations derived
+ * from it are upper bounds) and the launch count since the last enable, and
+ * synchronises. */
 int vptmcm_enable_kernel_timing(vptmcm* h, int enable);
 int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches);
 

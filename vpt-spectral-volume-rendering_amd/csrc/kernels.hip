@@ -1057,7 +1057,7 @@ hipError_t launch_reset(const MarchParams& P, float* ph, hipStream_t s) {
 hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P, const PassSeeds& PS,
                         const TileSched& T, float* ph, const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba,
-                        hipStream_t s) {
+                        hipStream_t s, hipEvent_t ev_beg, hipEvent_t ev_end) {
   dim3 grid(tile_blocks(P, kMarchBlock));
 #ifdef VPT_EXPERIMENTS
   {
@@ -1072,9 +1072,11 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
 #endif
   const bool spec = (variant & 1u) == 0u;  // variant bit 0: plain (non-speculative) step
   const bool nbf = P.nb >= (uint32_t)kMaxBins;  // every radiance bin in use
-#define VPT_LAUNCH(LAY, SP, NB)                                                                  \
-  hipLaunchKernelGGL((k_march<LAY, SP, NB>), grid, dim3(kMarchBlock), 0, s, PS, P, T, ph, vol, tf_rg, \
-                     tf_b4, tf_brow, light, rgba)
+  // hipExtLaunchKernelGGL stamps the events from the dispatch packet itself
+  // (no extra barrier/marker packets between back-to-back launches)
+#define VPT_LAUNCH(LAY, SP, NB)                                                                \
+  hipExtLaunchKernelGGL((k_march<LAY, SP, NB>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
+                        PS, P, T, ph, vol, tf_rg, tf_b4, tf_brow, light, rgba)
 #define VPT_LAUNCH_NB(LAY, SP) \
   do {                         \
     if (nbf)                   \
@@ -1098,12 +1100,15 @@ hipError_t launch_reset_rgb(const MarchParams& P, float* ph, hipStream_t s) {
 }
 
 hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSeeds& PS, float* ph,
-                            const uint8_t* vol, const float4* tf, uint16_t* rgba, hipStream_t s) {
+                            const uint8_t* vol, const float4* tf, uint16_t* rgba, hipStream_t s,
+                            hipEvent_t ev_beg, hipEvent_t ev_end) {
   dim3 grid(tile_blocks(P, kMarchBlock));
   if (layout == kLayoutCorner8)
-    hipLaunchKernelGGL((k_march_rgb<kLayoutCorner8>), grid, dim3(kMarchBlock), 0, s, PS, P, ph, vol, tf, rgba);
+    hipExtLaunchKernelGGL((k_march_rgb<kLayoutCorner8>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end,
+                          0, PS, P, ph, vol, tf, rgba);
   else
-    hipLaunchKernelGGL((k_march_rgb<kLayoutLinear>), grid, dim3(kMarchBlock), 0, s, PS, P, ph, vol, tf, rgba);
+    hipExtLaunchKernelGGL((k_march_rgb<kLayoutLinear>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end,
+                          0, PS, P, ph, vol, tf, rgba);
   return hipGetLastError();
 }
 

@@ -63,9 +63,15 @@ struct vptmcm {
   vptmcm_params params{1.0f, 0.0f, 8u, 8u, 0.0f};  // property defaults, js:19-48
 
   // timing
+  // Region timing: the first march launch after enable stamps `region.beg`
+  // from its own dispatch packet; synchronize / kernel_time enqueue
+  // `region.end` behind the last launch. Per-launch event pairs were measured
+  // to cost 1.6 us per fused pass (the markers' cache maintenance between
+  // back-to-back launches), so only the region is bracketed.
   bool timing = false;
-  std::vector<EventPair> events;
-  size_t events_used = 0;
+  bool region_closed = false;
+  EventPair region;
+  uint64_t launches = 0;
 
   // multi-GPU
   ncclComm_t comm = nullptr;
@@ -268,17 +274,25 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
 
 int check_handle(vptmcm* h) { return h ? VPTMCM_OK : VPTMCM_EINVAL; }
 
-int time_begin(vptmcm* h, EventPair** ep) {
-  *ep = nullptr;
+// The start event of the next march launch: the region's begin event for the
+// first timed launch (stamped by the dispatch packet itself), else none.
+int time_slot(vptmcm* h, hipEvent_t* beg) {
+  *beg = nullptr;
   if (!h->timing) return VPTMCM_OK;
-  if (h->events_used == h->events.size()) {
-    EventPair e;
-    HIPCHK(h, hipEventCreate(&e.beg));
-    HIPCHK(h, hipEventCreate(&e.end));
-    h->events.push_back(e);
+  if (!h->region.beg) {
+    HIPCHK(h, hipEventCreateWithFlags(&h->region.beg, hipEventDisableSystemFence));
+    HIPCHK(h, hipEventCreateWithFlags(&h->region.end, hipEventDisableSystemFence));
   }
-  *ep = &h->events[h->events_used++];
-  HIPCHK(h, hipEventRecord((*ep)->beg, h->stream));
+  if (h->launches++ == 0) *beg = h->region.beg;
+  h->region_closed = false;
+  return VPTMCM_OK;
+}
+
+// Enqueue the region's end event behind the last timed launch (once).
+int time_close(vptmcm* h) {
+  if (!h->timing || h->launches == 0 || h->region_closed) return VPTMCM_OK;
+  HIPCHK(h, hipEventRecord(h->region.end, h->stream));
+  h->region_closed = true;
   return VPTMCM_OK;
 }
 
@@ -290,20 +304,19 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   memset(&PS, 0, sizeof PS);
   PS.n = n;
   memcpy(PS.seed, seeds, n * sizeof(uint32_t));
-  EventPair* ep = nullptr;
-  int rc = time_begin(h, &ep);
+  hipEvent_t eb = nullptr, ee = nullptr;
+  int rc = time_slot(h, &eb);
   if (rc) return rc;
   const uint8_t* vol = h->layout == kLayoutCorner8 ? (const uint8_t*)h->vol_c8 : h->vol_lin;
   const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
   TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf};
   P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : 0u;
   if (h->kind == VPTMCM_RENDERER_RGB)
-    HIPCHK(h, launch_march_rgb(h->layout, P, PS, h->photons, vol, h->tf_rgb, h->rgba, h->stream));
+    HIPCHK(h, launch_march_rgb(h->layout, P, PS, h->photons, vol, h->tf_rgb, h->rgba, h->stream, eb, ee));
   else
     HIPCHK(h, launch_march(h->layout, h->variant, P, PS, T, h->photons, vol, h->tf_rg, h->tf_b4,
-                           h->tf_brow, h->light, h->rgba, h->stream));
+                           h->tf_brow, h->light, h->rgba, h->stream, eb, ee));
   h->sched_cur = c ^ 1u;
-  if (ep) HIPCHK(h, hipEventRecord(ep->end, h->stream));
   return VPTMCM_OK;
 }
 
@@ -426,10 +439,8 @@ void vptmcm_destroy(vptmcm* h) {
     if (h->comp_done[k]) (void)hipEventDestroy(h->comp_done[k]);
   }
   if (h->host_scratch) (void)hipFree(h->host_scratch);
-  for (auto& e : h->events) {
-    if (e.beg) (void)hipEventDestroy(e.beg);
-    if (e.end) (void)hipEventDestroy(e.end);
-  }
+  if (h->region.beg) (void)hipEventDestroy(h->region.beg);
+  if (h->region.end) (void)hipEventDestroy(h->region.end);
   free_volume(h);
   if (h->photons) (void)hipFree(h->photons);
   if (h->rgba) (void)hipFree(h->rgba);
@@ -652,6 +663,8 @@ int vptmcm_render_passes(vptmcm* h, const float* mvp, const uint32_t* seeds, uin
 int vptmcm_synchronize(vptmcm* h) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   HIPCHK(h, hipSetDevice(h->device));
+  int rc = time_close(h);
+  if (rc) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->comm_stream) HIPCHK(h, hipStreamSynchronize(h->comm_stream));
   return VPTMCM_OK;
@@ -779,7 +792,8 @@ int vptmcm_enable_kernel_timing(vptmcm* h, int enable) {
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->timing = enable != 0;
-  h->events_used = 0;
+  h->launches = 0;
+  h->region_closed = false;
   return VPTMCM_OK;
 }
 
@@ -787,15 +801,13 @@ int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (!total_ms || !launches) FAIL(h, VPTMCM_EINVAL, "kernel_time: null output");
   HIPCHK(h, hipSetDevice(h->device));
+  int rc = time_close(h);
+  if (rc) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  double sum = 0.0;
-  for (size_t k = 0; k < h->events_used; k++) {
-    float ms = 0.0f;
-    HIPCHK(h, hipEventElapsedTime(&ms, h->events[k].beg, h->events[k].end));
-    sum += ms;
-  }
-  *total_ms = sum;
-  *launches = h->events_used;
+  float ms = 0.0f;
+  if (h->timing && h->launches) HIPCHK(h, hipEventElapsedTime(&ms, h->region.beg, h->region.end));
+  *total_ms = ms;
+  *launches = h->timing ? h->launches : 0;
 #ifdef VPT_EXPERIMENTS
   unsigned long long st[8];
   if (read_stamps(st) == hipSuccess) {
@@ -805,7 +817,7 @@ int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
     fprintf(stderr, "stamps:");
     for (int k = 0; k < 7; k++) fprintf(stderr, " %s=%.1f%%", names[k], tot ? 100.0 * st[k] / tot : 0.0);
     fprintf(stderr, " (wave-cycles/launch/wave %.0f)\n",
-            h->events_used ? (double)tot / h->events_used / (h->npad / 64) : 0.0);
+            h->launches ? (double)tot / h->launches / (h->npad / 64) : 0.0);
   }
   if (const char* path = getenv("VPTMCM_WAVE_DUMP")) {
     std::vector<uint8_t> buf((size_t)32 << 16);
