@@ -24,6 +24,7 @@ ALL = (0, 1 << 32)
     (12, "rcp_in_range: RN(1/x) for exponent 1..252", *ALL),
     (15, "clampc_q (v_max/v_min) == clampc for non-signalling x", *ALL),
     (16, "v_min/v_max/v_max3 == smin/smax chains (quiet, no +-0 pair)", *ALL),
+    (17, "inv_len: RN(1/RN(sqrt x)) with one guard", *ALL),
 ])
 def test_fast_sequences_are_correctly_rounded(fn, name, lo, n):
     with vptmcm.Renderer(8, device=0) as g:

@@ -103,6 +103,14 @@ struct VolTap {
   uint32_t lo, hi;  // the 8 corner voxels, byte (dz*4 + dy*2 + dx)
 };
 
+// v_mad_u32_u24 (full rate; a*b + c for a, b < 2^24; b wave-uniform), spelled out because the
+// backend otherwise merges the first multiply-add into a v_mad_u64_u32
+__device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+  return r;
+}
+
 template <uint32_t L>
 __device__ __forceinline__ VolTap vol_fetch(const MarchParams& P, const uint8_t* __restrict__ vol,
                                             f3 q) {
@@ -111,13 +119,20 @@ __device__ __forceinline__ VolTap vol_fetch(const MarchParams& P, const uint8_t*
   int ix = axis_floor_q(q.x, (float)P.W, &t.fx);
   int iy = axis_floor_q(q.y, (float)P.H, &t.fy);
   int iz = axis_floor_q(q.z, (float)P.D, &t.fz);
-  if constexpr (L == kLayoutCorner8) {
+  if constexpr (L == kTplCorner8 || L == kTplCorner8Wide) {
     const uint32_t W1 = P.W + 1u, H1 = P.H + 1u;
     uint32_t cx = (uint32_t)(clampi(ix + 1, (int)P.W));
     uint32_t cy = (uint32_t)(clampi(iy + 1, (int)P.H));
     uint32_t cz = (uint32_t)(clampi(iz + 1, (int)P.D));
-    size_t cell = ((size_t)cz * H1 + cy) * W1 + cx;
-    uint2 c = reinterpret_cast<const uint2*>(vol)[cell];
+    uint2 c;
+    if constexpr (L == kTplCorner8) {
+      // 32-bit byte offset from the SGPR base (u24 multiply-adds, saddr load)
+      const uint32_t off = (__umul24(mad_u24(cz, H1, cy), W1) + cx) << 3;
+      c = *reinterpret_cast<const uint2*>(vol + off);
+    } else {
+      size_t cell = ((size_t)cz * H1 + cy) * W1 + cx;
+      c = reinterpret_cast<const uint2*>(vol)[cell];
+    }
     t.lo = c.x;
     t.hi = c.y;
   } else {
@@ -412,12 +427,21 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   const size_t S = P.npad;
   bool entered = false;  // wave-uniform: some lane of this wave was inside the volume
   Photon p;
+#ifndef VPT_KO_STATE  // cost-attribution variant only (results invalid)
   if (live) load_photon(ph, S, i, p);  // issue the state loads before the LDS fill
+#else
+  p = Photon{};
+  p.pos = f3{0.5f, 0.5f, 0.5f};
+  p.dir = f3{0.0f, 0.0f, 1.0f};
+  p.lambda = 550.0f;
+#endif
 
   const uint4* src = reinterpret_cast<const uint4*>(tf_rg);
+#ifndef VPT_KO_TFFILL  // cost-attribution variant only (results invalid)
 #pragma unroll
   for (uint32_t k = 0; k < 256 * 256 * 2 / 16 / kMarchBlock; k++)
     s_tf4[threadIdx.x + k * kMarchBlock] = src[threadIdx.x + k * kMarchBlock];
+#endif
   if (threadIdx.x < 256u) {
     s_light[threadIdx.x] = (float)light[threadIdx.x];
     s_brow[threadIdx.x] = (float)tf_brow[threadIdx.x];
@@ -437,6 +461,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 #else
   const bool slab_hw = false;
 #endif
+  // 1 - from, kept in VGPRs for the whole launch (the backend would otherwise
+  // recompute it in every step's reset candidate)
+  f3 omf{1.0f - from.x, 1.0f - from.y, 1.0f - from.z};
+  asm volatile("" : "+v"(omf.x), "+v"(omf.y), "+v"(omf.z));
 
 #if VPT_PRIO
   // Waves whose tile entered the volume last pass are the long ones; they win
@@ -589,7 +617,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         float dx = 0.0f, dy = 0.0f;
         if (!fixed) disk_of(h1, h2, dx, dy);
         Photon rc;
-        reset_from_draws(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw);
+        reset_from_draws(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
         terminate(exit_radiance(P, p.dir, wc), rc);
         wc = wave_const(rc.lambda, s_light);
         st = h5;
@@ -630,7 +658,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         rc.bin = KO(8) ? p.bin : bin_of(P, rc.lambda);
         if (!KO(7)) wcr = wave_const(rc.lambda, s_light);
       } else {
-        reset_from_draws(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw);
+        reset_from_draws(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
         wcr = wave_const(rc.lambda, s_light);
       }
       STAMP(2);  // speculative reset candidate
@@ -776,9 +804,13 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 #if VPT_ROBUST
   if (stale) p.pos = ray_start(from, p.dir);  // the last robust reset's start point
 #endif
+#ifndef VPT_KO_STATE
   store_state(ph, S, i, p);  // uPhotons[globalIndex] = p (wgsl:165), once per launch
 #pragma unroll
   for (int b = 0; b < kMaxBins; b++) ph[(kRad0 + b) * S + i] = p.rad[b];
+#else
+  if (p.rad[0] == 12345.0f) ph[i] = p.rad[1] + p.rad[5] + p.rad[11] + p.pos.x + p.dir.y;
+#endif
 
   if (lane == 0u) T.flags_out[tile] = entered ? 1u : 0u;  // the next pass's schedule
   WAVE_RECORD(tile, entered);
@@ -1084,10 +1116,12 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
     else                       \
       VPT_LAUNCH(LAY, SP, false); \
   } while (0)
-  if (layout == kLayoutCorner8) {
-    if (spec) VPT_LAUNCH_NB(kLayoutCorner8, true); else VPT_LAUNCH_NB(kLayoutCorner8, false);
+  if (layout == kLayoutCorner8 && P.vol32) {
+    if (spec) VPT_LAUNCH_NB(kTplCorner8, true); else VPT_LAUNCH_NB(kTplCorner8, false);
+  } else if (layout == kLayoutCorner8) {
+    if (spec) VPT_LAUNCH_NB(kTplCorner8Wide, true); else VPT_LAUNCH_NB(kTplCorner8Wide, false);
   } else {
-    if (spec) VPT_LAUNCH_NB(kLayoutLinear, true); else VPT_LAUNCH_NB(kLayoutLinear, false);
+    if (spec) VPT_LAUNCH_NB(kTplLinear, true); else VPT_LAUNCH_NB(kTplLinear, false);
   }
 #undef VPT_LAUNCH_NB
 #undef VPT_LAUNCH
@@ -1103,11 +1137,14 @@ hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSee
                             const uint8_t* vol, const float4* tf, uint16_t* rgba, hipStream_t s,
                             hipEvent_t ev_beg, hipEvent_t ev_end) {
   dim3 grid(tile_blocks(P, kMarchBlock));
-  if (layout == kLayoutCorner8)
-    hipExtLaunchKernelGGL((k_march_rgb<kLayoutCorner8>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end,
+  if (layout == kLayoutCorner8 && P.vol32)
+    hipExtLaunchKernelGGL((k_march_rgb<kTplCorner8>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end,
                           0, PS, P, ph, vol, tf, rgba);
+  else if (layout == kLayoutCorner8)
+    hipExtLaunchKernelGGL((k_march_rgb<kTplCorner8Wide>), grid, dim3(kMarchBlock), 0, s, ev_beg,
+                          ev_end, 0, PS, P, ph, vol, tf, rgba);
   else
-    hipExtLaunchKernelGGL((k_march_rgb<kLayoutLinear>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end,
+    hipExtLaunchKernelGGL((k_march_rgb<kTplLinear>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end,
                           0, PS, P, ph, vol, tf, rgba);
   return hipGetLastError();
 }
@@ -1234,6 +1271,10 @@ __device__ __forceinline__ float cand_eval(int fn, float x, float* ref) {
       uint32_t a = __float_as_uint(x) & 0x7fffffffu;
       bool snan = a > 0x7f800000u && !(a & 0x00400000u);
       return snan ? *ref : clampc_q(x);
+    }
+    case 17: {  // norm3's inverse length: one guard for the sqrt / rcp pair
+      *ref = 1.0f / __builtin_sqrtf(x);
+      return inv_len(x);
     }
     case 5: {  // v_sqrt_f32 + one Newton correction using the rsq estimate
       *ref = __builtin_sqrtf(x);

@@ -27,6 +27,9 @@
 namespace vpt {
 
 enum : uint32_t { kLayoutLinear = 0, kLayoutCorner8 = 1 };
+// Kernel template layouts: CORNER8 with 32-bit cell offsets (MarchParams::vol32)
+// or with 64-bit ones (volumes whose cell array exceeds 4 GiB, e.g. 1024^3).
+enum : uint32_t { kTplLinear = 0, kTplCorner8 = 1, kTplCorner8Wide = 2 };
 
 // Plane indices of the SoA photon buffer.
 enum Plane : uint32_t {
@@ -67,6 +70,10 @@ struct MarchParams {
   float rb_x0, rb_x1, rb_y0, rb_y1;
   uint32_t R, tiles_x, n_tiles, npad;
   uint32_t W, H, D;
+  // CORNER8 cell byte offsets fit 32 bits ((W+1)(H+1)(D+1) * 8 < 2^32 and
+  // (D+1)(H+1) < 2^24): the gather address is u24 multiply-adds on a 32-bit
+  // offset from the SGPR base instead of a 64-bit multiply chain
+  uint32_t vol32;
 };
 
 // ---------------------------------------------------------------- RNG draws
@@ -231,11 +238,13 @@ __device__ __forceinline__ f3 ray_dir_from_draws(const MarchParams& P, float sx,
 // is zero, i.e. no coordinate of `from` is exactly 0 or 1 (then every
 // (c - from)*RN(1/d) is a non-zero number, an infinity or a quiet NaN, and
 // v_min/v_max/v_max3 return what smin/smax do; see hw_min).
-__device__ __forceinline__ f3 ray_start_hw(f3 from, f3 dir) {
+// omf = 1 - from (a per-pixel constant the caller keeps in registers); with
+// from != 0, 0 - from is exactly -from (a free negation modifier).
+__device__ __forceinline__ f3 ray_start_hw(f3 from, f3 omf, f3 dir) {
   float rx = rcp_small(dir.x), ry = rcp_small(dir.y), rz = rcp_small(dir.z);
-  float t1x = hw_min((0.0f - from.x) * rx, (1.0f - from.x) * rx);
-  float t1y = hw_min((0.0f - from.y) * ry, (1.0f - from.y) * ry);
-  float t1z = hw_min((0.0f - from.z) * rz, (1.0f - from.z) * rz);
+  float t1x = hw_min(-from.x * rx, omf.x * rx);
+  float t1y = hw_min(-from.y * ry, omf.y * ry);
+  float t1z = hw_min(-from.z * rz, omf.z * rz);
   float tn = hw_max(hw_max3(t1x, t1y, t1z), 0.0f);
   return f3{fmaf(tn, dir.x, from.x), fmaf(tn, dir.y, from.y), fmaf(tn, dir.z, from.z)};
 }
@@ -261,11 +270,11 @@ __device__ __forceinline__ float lambda_of(const MarchParams& P, uint32_t h5) {
 __device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p, float sx, float sy,
                                                  bool fixed_from, f3 from, float dx, float dy,
                                                  uint32_t h3, uint32_t h4, uint32_t h5,
-                                                 bool slab_hw = false) {
+                                                 bool slab_hw = false, f3 omf = f3{0.0f, 0.0f, 0.0f}) {
   if (!fixed_from) from = unproject(P.m, fmaf(dx, P.blur, sx), fmaf(dy, P.blur, sy), -1.0f);
   p.dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
-  if (slab_hw)  // wave-uniform: every lane's from is slab_generic
-    p.pos = ray_start_hw(from, p.dir);
+  if (slab_hw)  // wave-uniform: every lane's from is slab_generic, omf = 1 - from
+    p.pos = ray_start_hw(from, omf, p.dir);
   else
     p.pos = ray_start(from, p.dir);
   p.lambda = lambda_of(P, h5);

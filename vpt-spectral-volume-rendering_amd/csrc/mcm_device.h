@@ -211,8 +211,24 @@ __device__ __forceinline__ float rnd_uniform(uint32_t& st) {
 __device__ __forceinline__ float rcp(float x) { return rcp_cr(x); }
 
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+// RN(1 / RN(sqrt x)) with ONE range guard: where sqrt_cr's fast path is exact
+// (x > 0 with biased exponent 32..254) the root lies in [2^-48, 2^64), inside
+// rcp_in_range's exact range, so its own guard is redundant; every other x
+// takes the IEEE pair. Equal to rcp_cr(sqrt_cr(x)) for all 2^32 x
+// (tests/test_gpu_fastmath.py, fn 17).
+__device__ __forceinline__ float inv_len(float x) {
+  float s = __builtin_amdgcn_sqrtf(x);
+  float e = __builtin_fmaf(-s, s, x);
+  float h = 0.5f * __builtin_amdgcn_rsqf(x);
+  s = __builtin_fmaf(e, h, s);
+  float y = rcp_in_range(s);
+  uint32_t ex = __float_as_uint(x) >> 23;
+  VPT_FIXUP(ex - 32u > 222u, y, rcp_slow(sqrt_slow(x)));
+  return y;
+}
+
 __device__ __forceinline__ f3 norm3(f3 a) {
-  float il = rcp(sqrt_cr(dot3(a, a)));
+  float il = inv_len(dot3(a, a));
   return f3{a.x * il, a.y * il, a.z * il};
 }
 

@@ -269,6 +269,11 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
   P.W = h->W;
   P.H = h->H;
   P.D = h->D;
+  {
+    const uint64_t w1 = h->W + 1ull, h1 = h->H + 1ull, d1 = h->D + 1ull;
+    P.vol32 = (w1 * h1 * d1 * 8ull < (1ull << 32) && d1 * h1 < (1ull << 24) && w1 < (1ull << 24))
+                  ? 1u : 0u;
+  }
   return P;
 }
 
