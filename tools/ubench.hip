@@ -91,7 +91,7 @@ int main() {
   hipMalloc(&d, 8 * 8192);
   unsigned long long h[4096];
   for (auto& k : ks) {
-    for (int wps = 1; wps <= 2; wps++) {
+    for (int wps = 1; wps <= 4; wps++) {
       hipLaunchKernelGGL(k.f, dim3(1), dim3(256 * wps), 0, 0, d, 7u);
       hipDeviceSynchronize();
       hipLaunchKernelGGL(k.f, dim3(1), dim3(256 * wps), 0, 0, d, 7u);
