@@ -1,34 +1,66 @@
 #!/usr/bin/env python3
-"""Summarise a tools/pmc.sh run into profiles/: per-launch HBM traffic of k_march
-(FETCH_SIZE + WRITE_SIZE, KB -> bytes) and the SQ counters, averaged over launches.
-Usage: python tools/pmc_traffic.py <dir-glob> profiles/pmc_traffic.json [R S layout passes_per_launch]
-(<dir-glob> matches the rocprofv3 output dirs, e.g. 'gpurun_out/pmc_*')."""
+"""Per-launch HBM-side traffic of k_march from rocprofv3 --pmc runs, calibrated
+as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE / WRITE_SIZE are checked
+against a launch of our own access pattern whose bytes are known (S = 0, one
+pass per launch: the 22 photon-state planes read and written, the rgba16f
+image and the tile flags written, no volume gathers), and the resulting
+factors are applied to the benchmark launch.
+
+Usage: python tools/pmc_traffic.py <bench_FETCH_dir> <bench_WRITE_dir>
+           <calib_FETCH_dir> <calib_WRITE_dir> <out.json> [R S layout passes_per_launch]
+"""
 import csv
 import glob
 import json
 import sys
-from collections import defaultdict
+
+
+def mean_counter(d, name):
+    v = []
+    for f in glob.glob(f"{d}/run_counter_collection.csv"):
+        for row in csv.DictReader(open(f)):
+            if "k_march" in row["Kernel_Name"] and row["Counter_Name"] == name:
+                v.append(float(row["Counter_Value"]))
+    if not v:
+        raise SystemExit(f"no {name} samples of k_march under {d}")
+    return sum(v) / len(v), len(v)
 
 
 def main():
-    src, dst = sys.argv[1], sys.argv[2]
-    R, S, layout = (int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]) if len(sys.argv) > 5 else (512, 8, "corner8")
-    F = int(sys.argv[6]) if len(sys.argv) > 6 else 16
-    vals = defaultdict(list)
-    for f in sorted(glob.glob(f"{src}/run_counter_collection.csv")):
-        for row in csv.DictReader(open(f)):
-            if "k_march" in row["Kernel_Name"]:
-                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
-    mean = {k: sum(v) / len(v) for k, v in vals.items()}
-    out = {"kernel": "k_march", "resolution": R, "steps": S, "layout": layout,
-           "passes_per_launch": F,
-           "counters_mean_per_launch": mean,
-           "note": "FETCH_SIZE/WRITE_SIZE in KB (rocprofv3); FETCH_SIZE is uncalibrated for "
-                   "scattered 8-B gathers (MI355X_MICROARCH.md §HBM), reported uncorrected"}
-    if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
-        out["hbm_bytes_per_launch"] = int((mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024)
+    bf, bw, cf_, cw, dst = sys.argv[1:6]
+    R, S, layout, F = 512, 8, "corner8", 16
+    if len(sys.argv) > 9:
+        R, S, layout, F = int(sys.argv[6]), int(sys.argv[7]), sys.argv[8], int(sys.argv[9])
+    fetch_kb, nf = mean_counter(bf, "FETCH_SIZE")
+    write_kb, nw = mean_counter(bw, "WRITE_SIZE")
+    cfetch_kb, _ = mean_counter(cf_, "FETCH_SIZE")
+    cwrite_kb, _ = mean_counter(cw, "WRITE_SIZE")
+    n_tiles = ((R + 7) // 8) ** 2
+    npad = n_tiles * 64
+    state = 22 * 4 * npad                     # photon planes (pos, dir, bounces, samples, bin, lambda, rad[12])
+    # calibration launch: state in; state + image + flags out (the 128 KiB TF
+    # table misses once per XCD L2: 8 x 128 KiB, included in the read side)
+    known_read = state + 8 * 128 * 1024 + n_tiles
+    known_write = state + R * R * 8 + n_tiles
+    f_read = known_read / (cfetch_kb * 1024)
+    f_write = known_write / (cwrite_kb * 1024)
+    read_b = fetch_kb * 1024 * f_read
+    write_b = write_kb * 1024 * f_write
+    out = {
+        "kernel": "k_march", "resolution": R, "steps": S, "layout": layout, "passes_per_launch": F,
+        "raw_kb_per_launch": {"FETCH_SIZE": fetch_kb, "WRITE_SIZE": write_kb, "launches": [nf, nw]},
+        "calibration": {"launch": "S=0, 1 pass per launch", "known_read_bytes": known_read,
+                        "known_write_bytes": known_write, "FETCH_SIZE_kb": cfetch_kb,
+                        "WRITE_SIZE_kb": cwrite_kb, "read_factor": round(f_read, 4),
+                        "write_factor": round(f_write, 4)},
+        "read_bytes_per_launch": int(read_b), "write_bytes_per_launch": int(write_b),
+        "hbm_bytes_per_launch": int(read_b + write_b),
+        "note": "memory-side (L2 miss) bytes: Infinity-Cache hits are counted, so this bounds "
+                "HBM traffic from above; the read factor (~2) is the guide's gfx950 FETCH_SIZE "
+                "halving, measured on this kernel's own dword-coalesced plane loads",
+    }
     json.dump(out, open(dst, "w"), indent=1)
-    print(json.dumps({k: out.get(k) for k in ("hbm_bytes_per_launch",)}))
+    print(json.dumps({k: out[k] for k in ("hbm_bytes_per_launch", "calibration")}))
 
 
 if __name__ == "__main__":
