@@ -389,7 +389,10 @@ __device__ __forceinline__ const __attribute__((address_space(4))) float* cmf_ta
                                                                offsetof(MarchParams, xb)) / 4);
 }
 
-template <uint32_t L, bool SPEC, bool NBF>
+// MODE: 0 generic; 1 every radiance bin in use (nb >= 12); 2 additionally
+// equal-width bins (bin_of's arithmetic path) and a wavelength-invariant TF
+// blue channel (LDS row table): the per-step configuration branches vanish.
+template <uint32_t L, bool SPEC, uint32_t MODE>
 __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const MarchParams P,
                                                        const TileSched T, float* __restrict__ ph,
                                                        const uint8_t* __restrict__ vol,
@@ -398,6 +401,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
                                                        const uint8_t* __restrict__ tf_brow,
                                                        const uint8_t* __restrict__ light,
                                                        uint16_t* __restrict__ rgba) {
+  constexpr bool NBF = MODE >= 1u;
+  constexpr bool FAST = MODE == 2u;
   // (albedo, alpha) of the whole TF in LDS: every step's 4 TF taps become
   // ds_read_u16 instead of divergent L2 gathers. When the anisotropy channel
   // does not vary with wavelength (P.b_rows), its 256 row values sit in LDS
@@ -589,7 +594,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         p.dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
         p.bounces = 0u;
         p.lambda = lambda_of(P, h5);
-        p.bin = bin_of(P, p.lambda);
+        p.bin = bin_of<FAST>(P, p.lambda);
         wc = wave_const(p.lambda, s_light);
         st = h5;
         stale = true;
@@ -617,7 +622,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         float dx = 0.0f, dy = 0.0f;
         if (!fixed) disk_of(h1, h2, dx, dy);
         Photon rc;
-        reset_from_draws(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
+        reset_from_draws<FAST>(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
         terminate(exit_radiance(P, p.dir, wc), rc);
         wc = wave_const(rc.lambda, s_light);
         st = h5;
@@ -655,10 +660,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         rc.dir = d0;
         rc.pos = KO(5) ? from : ray_start(from, d0);
         rc.lambda = lambda_of(P, h5);
-        rc.bin = KO(8) ? p.bin : bin_of(P, rc.lambda);
+        rc.bin = KO(8) ? p.bin : bin_of<FAST>(P, rc.lambda);
         if (!KO(7)) wcr = wave_const(rc.lambda, s_light);
       } else {
-        reset_from_draws(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
+        reset_from_draws<FAST>(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
         wcr = wave_const(rc.lambda, s_light);
       }
       STAMP(2);  // speculative reset candidate
@@ -676,7 +681,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       float fr;
       int ir = axis_floor_in(d, 256.0f, &fr);
       uint32_t b4 = 0u;
-      if (!P.b_rows) b4 = tf_b4[(uint32_t)clampi(ir + 1, 256) * kTfCells + (uint32_t)wc.cc];
+      if (!(FAST || P.b_rows)) b4 = tf_b4[(uint32_t)clampi(ir + 1, 256) * kTfCells + (uint32_t)wc.cc];
       const uint32_t ri0 = (uint32_t)clampi(ir, 255), ri1 = (uint32_t)clampi(ir + 1, 255);
       uint32_t r0 = ri0 * 256u, r1 = ri1 * 256u;
       uint32_t t00, t10, t01, t11;
@@ -704,7 +709,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         st = h5;
       } else if (wheel < pabs + pscat) {
         // HG scatter (wgsl:82-97, :156-160) with g from the TF blue channel
-        float bch = P.b_rows ? lerp(s_brow[ri0], s_brow[ri1], fr) * kInv255
+        float bch = (FAST || P.b_rows) ? lerp(s_brow[ri0], s_brow[ri1], fr) * kInv255
                              : lerp(lerp(byte_f(b4, 0), byte_f(b4, 8), wc.fc),
                                     lerp(byte_f(b4, 16), byte_f(b4, 24), wc.fc), fr) * kInv255;
         float g = bch * 2.0f - 1.0f;
@@ -1104,17 +1109,20 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
 #endif
   const bool spec = (variant & 1u) == 0u;  // variant bit 0: plain (non-speculative) step
   const bool nbf = P.nb >= (uint32_t)kMaxBins;  // every radiance bin in use
+  const bool fast = nbf && P.bins_uniform && P.b_rows;
   // hipExtLaunchKernelGGL stamps the events from the dispatch packet itself
   // (no extra barrier/marker packets between back-to-back launches)
-#define VPT_LAUNCH(LAY, SP, NB)                                                                \
-  hipExtLaunchKernelGGL((k_march<LAY, SP, NB>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
+#define VPT_LAUNCH(LAY, SP, MO)                                                                \
+  hipExtLaunchKernelGGL((k_march<LAY, SP, MO>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
                         PS, P, T, ph, vol, tf_rg, tf_b4, tf_brow, light, rgba)
-#define VPT_LAUNCH_NB(LAY, SP) \
-  do {                         \
-    if (nbf)                   \
-      VPT_LAUNCH(LAY, SP, true); \
-    else                       \
-      VPT_LAUNCH(LAY, SP, false); \
+#define VPT_LAUNCH_NB(LAY, SP)        \
+  do {                                \
+    if (SP && fast)                   \
+      VPT_LAUNCH(LAY, SP, SP ? 2u : 1u); \
+    else if (nbf)                     \
+      VPT_LAUNCH(LAY, SP, 1u);        \
+    else                              \
+      VPT_LAUNCH(LAY, SP, 0u);        \
   } while (0)
   if (layout == kLayoutCorner8 && P.vol32) {
     if (spec) VPT_LAUNCH_NB(kTplCorner8, true); else VPT_LAUNCH_NB(kTplCorner8, false);

@@ -136,10 +136,13 @@ __device__ __forceinline__ WaveConst wave_const(float lambda, const float* s_lig
 // PhotonSpectral_set_wavelength, wgsl:276-290. For non-decreasing boundaries
 // the first i with lambda < lam[i] is 1 + #{i : !(lambda < lam[i])}, so the
 // search is a branchless count; otherwise the sequential first-match search.
+// UNI: the launch's host check guarantees bins_uniform and nb >= 1 (the fast
+// march specialisation), so the arithmetic path is taken without the branches.
+template <bool UNI = false>
 __device__ __forceinline__ uint32_t bin_of(const MarchParams& P, float lambda) {
-  if (P.nb == 0u) return 0xffffffffu;  // nb - 1 wraps (first-reset quirk)
+  if (!UNI && P.nb == 0u) return 0xffffffffu;  // nb - 1 wraps (first-reset quirk)
   uint32_t bin;
-  if (P.bins_uniform) {
+  if (UNI || P.bins_uniform) {
     // Host-verified: lam[i] == fma(f32(i), w, lam0) for i <= nb, lam0 > 0,
     // lam[nb] <= 2 lam0 (so lambda - lam0 is exact). The candidate
     // floor((lambda - lam0) * RN(1/w)) is within one bin of the count, and
@@ -241,7 +244,18 @@ __device__ __forceinline__ f3 ray_dir_from_draws(const MarchParams& P, float sx,
 // omf = 1 - from (a per-pixel constant the caller keeps in registers); with
 // from != 0, 0 - from is exactly -from (a free negation modifier).
 __device__ __forceinline__ f3 ray_start_hw(f3 from, f3 omf, f3 dir) {
-  float rx = rcp_small(dir.x), ry = rcp_small(dir.y), rz = rcp_small(dir.z);
+  // the three reciprocals share one wave-uniform range guard (rcp_small's)
+  float rx = rcp_in_range(dir.x), ry = rcp_in_range(dir.y), rz = rcp_in_range(dir.z);
+  {
+    const bool bx = !(__builtin_fabsf(dir.x) >= 1.17549435e-38f);
+    const bool by = !(__builtin_fabsf(dir.y) >= 1.17549435e-38f);
+    const bool bz = !(__builtin_fabsf(dir.z) >= 1.17549435e-38f);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bx | by | bz) != 0ull, 0)) {
+      rx = bx ? rcp_slow(dir.x) : rx;
+      ry = by ? rcp_slow(dir.y) : ry;
+      rz = bz ? rcp_slow(dir.z) : rz;
+    }
+  }
   float t1x = hw_min(-from.x * rx, omf.x * rx);
   float t1y = hw_min(-from.y * ry, omf.y * ry);
   float t1z = hw_min(-from.z * rz, omf.z * rz);
@@ -267,18 +281,22 @@ __device__ __forceinline__ float lambda_of(const MarchParams& P, uint32_t h5) {
   return fmaf((float)h5 * 2.3283064365386963e-10f, P.max_lam - P.min_lam, P.min_lam);
 }
 
+template <bool UNI = false>
 __device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p, float sx, float sy,
                                                  bool fixed_from, f3 from, float dx, float dy,
                                                  uint32_t h3, uint32_t h4, uint32_t h5,
                                                  bool slab_hw = false, f3 omf = f3{0.0f, 0.0f, 0.0f}) {
-  if (!fixed_from) from = unproject(P.m, fmaf(dx, P.blur, sx), fmaf(dy, P.blur, sy), -1.0f);
+  // slab_hw (wave-uniform) implies every lane's near point is fixed: a scalar
+  // branch skips the per-lane exec-mask region
+  if (!slab_hw && !fixed_from)
+    from = unproject(P.m, fmaf(dx, P.blur, sx), fmaf(dy, P.blur, sy), -1.0f);
   p.dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
   if (slab_hw)  // wave-uniform: every lane's from is slab_generic, omf = 1 - from
     p.pos = ray_start_hw(from, omf, p.dir);
   else
     p.pos = ray_start(from, p.dir);
   p.lambda = lambda_of(P, h5);
-  p.bin = bin_of(P, p.lambda);
+  p.bin = bin_of<UNI>(P, p.lambda);
 }
 
 __device__ __forceinline__ void screen_of(const MarchParams& P, uint32_t x, uint32_t y, float& sx,
