@@ -389,9 +389,11 @@ __device__ __forceinline__ const __attribute__((address_space(4))) float* cmf_ta
                                                                offsetof(MarchParams, xb)) / 4);
 }
 
-// MODE: 0 generic; 1 every radiance bin in use (nb >= 12); 2 additionally
-// equal-width bins (bin_of's arithmetic path) and a wavelength-invariant TF
-// blue channel (LDS row table): the per-step configuration branches vanish.
+// MODE: 0 generic; 1 every radiance bin in use (nb >= 12); 2 (FAST, the
+// benchmark configuration) additionally equal-width bins (bin_of's arithmetic
+// path), a wavelength-invariant TF blue channel (LDS row table), blur == 0 with
+// an even R (every near point fixed) and a host-bounded |w| (one-compare
+// reciprocal guard): the per-step configuration branches vanish.
 template <uint32_t L, bool SPEC, uint32_t MODE>
 __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const MarchParams P,
                                                        const TileSched T, float* __restrict__ ph,
@@ -609,10 +611,18 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       p.pos.z = fmaf(dist, p.dir.z, p.pos.z);
       uint32_t sw = pcg_hash(s1);
       float wheel = (float)sw * 2.3283064365386963e-10f;
-      bool oob = p.pos.x > 1.0f || p.pos.y > 1.0f || p.pos.z > 1.0f || p.pos.x < 0.0f ||
-                 p.pos.y < 0.0f || p.pos.z < 0.0f;
+      // any(p > 1) || any(p < 0) (wgsl:142; a NaN coordinate counts as inside):
+      // maxNum/minNum skip NaN operands, so max3 > 1 || min3 < 0 is the same
+      // test. The compares are taken as lane masks (v_cmp into SGPRs) and the
+      // per-lane bool is the mask itself (inverse ballot), so the all-exit
+      // test is scalar.
+      const float pmax = __builtin_fmaxf(__builtin_fmaxf(p.pos.x, p.pos.y), p.pos.z);
+      const float pmin = __builtin_fminf(__builtin_fminf(p.pos.x, p.pos.y), p.pos.z);
+      const uint64_t oob_m = __builtin_amdgcn_fcmpf(pmax, 1.0f, 2 /*OGT*/) |
+                             __builtin_amdgcn_fcmpf(pmin, 0.0f, 4 /*OLT*/);
+      const bool oob = __builtin_amdgcn_inverse_ballot_w64(oob_m);
 
-      if (__builtin_amdgcn_ballot_w64(!oob) == 0ull) {
+      if (oob_m == __builtin_amdgcn_read_exec()) {
         // Every lane of the wave leaves the volume this step (background tiles:
         // ~60% of wave-steps on the benchmark). The volume/TF samples, whose
         // values are unused on exit (wgsl:142), and the scatter half are skipped.
@@ -911,7 +921,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
       bool oob = pos.x > 1.0f || pos.y > 1.0f || pos.z > 1.0f || pos.x < 0.0f || pos.y < 0.0f ||
                  pos.z < 0.0f;
       uint32_t h1 = pcg_hash(sw), h2 = pcg_hash(h1), h3 = pcg_hash(h2), h4 = pcg_hash(h3);
-      if (__builtin_amdgcn_ballot_w64(!oob) == 0ull) {  // every lane leaves: exit + reset
+      if (__builtin_amdgcn_ballot_w64(oob) == __builtin_amdgcn_read_exec()) {  // every lane leaves: exit + reset
         samples++;
         float inv = rcp_in_range((float)samples);
         rad = f3{fmaf(tr.x * P.env[0] - rad.x, inv, rad.x), fmaf(tr.y * P.env[1] - rad.y, inv, rad.y),
@@ -1109,7 +1119,8 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
 #endif
   const bool spec = (variant & 1u) == 0u;  // variant bit 0: plain (non-speculative) step
   const bool nbf = P.nb >= (uint32_t)kMaxBins;  // every radiance bin in use
-  const bool fast = nbf && P.bins_uniform && P.b_rows;
+  const bool fast = nbf && P.bins_uniform && P.b_rows && P.w_bounded && P.blur == 0.0f &&
+                    (P.R & 1u) == 0u;
   // hipExtLaunchKernelGGL stamps the events from the dispatch packet itself
   // (no extra barrier/marker packets between back-to-back launches)
 #define VPT_LAUNCH(LAY, SP, MO)                                                                \

@@ -74,6 +74,9 @@ struct MarchParams {
   // (D+1)(H+1) < 2^24): the gather address is u24 multiply-adds on a 32-bit
   // offset from the SGPR base instead of a 64-bit multiply chain
   uint32_t vol32;
+  // |w| of every unprojected point < 2^120 (host bound from the matrix, the
+  // resolution and blur): a precondition of the FAST march specialisation
+  uint32_t w_bounded;
 };
 
 // ---------------------------------------------------------------- RNG draws
@@ -136,8 +139,9 @@ __device__ __forceinline__ WaveConst wave_const(float lambda, const float* s_lig
 // PhotonSpectral_set_wavelength, wgsl:276-290. For non-decreasing boundaries
 // the first i with lambda < lam[i] is 1 + #{i : !(lambda < lam[i])}, so the
 // search is a branchless count; otherwise the sequential first-match search.
-// UNI: the launch's host check guarantees bins_uniform and nb >= 1 (the fast
-// march specialisation), so the arithmetic path is taken without the branches.
+// UNI: the launch's host check guarantees bins_uniform, nb >= 1, w_bounded,
+// blur == 0 and an even R (the FAST march specialisation), so the arithmetic
+// path is taken without the branches.
 template <bool UNI = false>
 __device__ __forceinline__ uint32_t bin_of(const MarchParams& P, float lambda) {
   if (!UNI && P.nb == 0u) return 0xffffffffu;  // nb - 1 wraps (first-reset quirk)
@@ -185,12 +189,15 @@ struct Photon {
   float rad[kMaxBins];
 };
 
-// near point of the camera ray: M * (screen + disk*blur, -1, 1), divided by w
+// near point of the camera ray: M * (screen + disk*blur, -1, 1), divided by w.
+// WB: the host has bounded |w| < 2^120 for every (a, b) the launch can produce
+// (MarchParams::w_bounded), so rcp_small's one-compare guard suffices.
+template <bool WB = false>
 __device__ __forceinline__ f3 unproject(const float* m, float a, float b, float z) {
   float d[4];
 #pragma unroll
   for (int r = 0; r < 4; r++) d[r] = fmaf(m[12 + r], 1.0f, fmaf(m[8 + r], z, fmaf(m[4 + r], b, m[r] * a)));
-  float iw = rcp(d[3]);
+  float iw = WB ? rcp_small(d[3]) : rcp(d[3]);
   return f3{d[0] * iw, d[1] * iw, d[2] * iw};
 }
 
@@ -229,11 +236,12 @@ __device__ __forceinline__ void photon_reset(const MarchParams& P, Photon& p, fl
 // h1,h2 are the disk draws (already turned into dx, dy), h3,h4 the square,
 // h5 the wavelength.
 // Direction of the new camera ray: normalize(far - near) (unprojectRand.wgsl).
+template <bool WB = false>
 __device__ __forceinline__ f3 ray_dir_from_draws(const MarchParams& P, float sx, float sy, f3 from,
                                                  uint32_t h3, uint32_t h4) {
   float q0 = (float)h3 * 2.3283064365386963e-10f;
   float q1 = (float)h4 * 2.3283064365386963e-10f;
-  f3 to = unproject(P.m, fmaf(fmaf(q0, 2.0f, -1.0f), P.inv_res[0], sx),
+  f3 to = unproject<WB>(P.m, fmaf(fmaf(q0, 2.0f, -1.0f), P.inv_res[0], sx),
                     fmaf(fmaf(q1, 2.0f, -1.0f), P.inv_res[1], sy), 1.0f);
   return norm3(f3{to.x - from.x, to.y - from.y, to.z - from.z});
 }
@@ -286,11 +294,12 @@ __device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p
                                                  bool fixed_from, f3 from, float dx, float dy,
                                                  uint32_t h3, uint32_t h4, uint32_t h5,
                                                  bool slab_hw = false, f3 omf = f3{0.0f, 0.0f, 0.0f}) {
-  // slab_hw (wave-uniform) implies every lane's near point is fixed: a scalar
-  // branch skips the per-lane exec-mask region
-  if (!slab_hw && !fixed_from)
-    from = unproject(P.m, fmaf(dx, P.blur, sx), fmaf(dy, P.blur, sy), -1.0f);
-  p.dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
+  // UNI launches have blur == 0 and an even R, so every near point is fixed
+  // (screen coordinates of pixel centres are never 0 then)
+  if constexpr (!UNI) {
+    if (!fixed_from) from = unproject(P.m, fmaf(dx, P.blur, sx), fmaf(dy, P.blur, sy), -1.0f);
+  }
+  p.dir = ray_dir_from_draws<UNI>(P, sx, sy, from, h3, h4);
   if (slab_hw)  // wave-uniform: every lane's from is slab_generic, omf = 1 - from
     p.pos = ray_start_hw(from, omf, p.dir);
   else

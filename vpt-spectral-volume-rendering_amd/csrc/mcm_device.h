@@ -297,7 +297,8 @@ __device__ __forceinline__ float hw_max3(float a, float b, float c) {
   return r;
 }
 
-__device__ __forceinline__ int clampi(int i, int hi) { return i < 0 ? 0 : (i > hi ? hi : i); }
+// max(min(i, hi), 0) for hi >= 0 (the same value as i < 0 ? 0 : i > hi ? hi : i): one v_med3_i32
+__device__ __forceinline__ int clampi(int i, int hi) { return __builtin_elementwise_max(__builtin_elementwise_min(i, hi), 0); }
 __device__ __forceinline__ float lerp(float a, float b, float f) { return fmaf(f, b - a, a); }
 
 }  // namespace vpt

@@ -250,6 +250,14 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
     P.light_dir[2] = ld[2] * il;
   }
   P.b_rows = h->b_rows;
+  {  // |w| bound for unproject<true>: |a|, |b| <= 1 + max(2/R, |blur|) + 1 (slop)
+    const double A = 2.0 + std::max(2.0 / h->R, std::fabs((double)P.blur));
+    bool fin = true;
+    for (int k = 0; k < 16; k++) fin = fin && std::isfinite(mvp[k]);
+    const double wb = (std::fabs((double)mvp[3]) + std::fabs((double)mvp[7])) * A +
+                      std::fabs((double)mvp[11]) + std::fabs((double)mvp[15]);
+    P.w_bounded = (fin && wb < std::ldexp(1.0, 120)) ? 1u : 0u;
+  }
   P.anisotropy = h->params.anisotropy;
   P.tf_w = h->tf_rgb_w;
   for (int k = 0; k < 4; k++) P.env[k] = h->env[k];
