@@ -21,6 +21,9 @@
 #ifndef VPT_OH_PEND
 #define VPT_OH_PEND 1  // byte one-hot pending bin, zero-weight apply
 #endif
+#ifndef VPT_PIN_PEND
+#define VPT_PIN_PEND 1  // pin the deferred radiance update before the gather wait
+#endif
 #ifndef VPT_SLAB_HW
 #define VPT_SLAB_HW 1  // hardware min/max slab test for generic fixed near points
 #endif
@@ -650,6 +653,13 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       }
       STAMP(1);  // step head: draws, log, advance, gather issue (first step: + state-load wait)
       apply_pending();
+#if VPT_PIN_PEND
+      // keep the update here, in the gather's shadow (the backend otherwise
+      // sinks it past the decision, after the wait)
+      asm volatile("" : "+v"(p.rad[0]), "+v"(p.rad[1]), "+v"(p.rad[2]), "+v"(p.rad[3]),
+                   "+v"(p.rad[4]), "+v"(p.rad[5]), "+v"(p.rad[6]), "+v"(p.rad[7]),
+                   "+v"(p.rad[8]), "+v"(p.rad[9]), "+v"(p.rad[10]), "+v"(p.rad[11]));
+#endif
 
       // Speculative candidates, all derived from the state after the wheel
       // draw and independent of the gather: the reset (draws h1..h5) and the
