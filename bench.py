@@ -59,6 +59,10 @@ def parse():
     ap.add_argument("--unfused-steps", type=int, default=64,
                     help="passes of a second timed region at one launch per pass (reported "
                          "as 'unfused'; 0 = skip; N = 1 only)")
+    ap.add_argument("--api-steps", type=int, default=64,
+                    help="passes of a third timed region through the drop-in render() entry "
+                         "point, one call per pass (lazily fused by the library; reported as "
+                         "'render_api'; 0 = skip; N = 1 only)")
     ap.add_argument("--no-timing", action="store_true",
                     help="diagnostics: no per-launch kernel timestamps (wall clock only; the "
                          "roofline fields are then null)")
@@ -134,7 +138,8 @@ def main():
             rendezvous.cleanup(key)
 
     n_unfused = a.unfused_steps if not multi else 0
-    seeds = cf.seed_stream(a.warmup + a.steps + n_unfused + 1, start=0, rank=rank)
+    n_api = a.api_steps if not multi else 0
+    seeds = cf.seed_stream(a.warmup + a.steps + n_unfused + n_api + 1, start=0, rank=rank)
     F = max(1, min(a.fuse, 32))
     every = max(1, a.allreduce_every)
 
@@ -214,6 +219,22 @@ def main():
                    "achieved": round(ua, 1), "frac": round(ua / HBM_PEAK_GBPS, 4),
                    "algorithmic_bytes_per_launch": ub}
 
+    # the drop-in path: one vptmcm_render() call per pass, as the JS renderer's
+    # render() makes them; the library queues them and launches fused marches
+    render_api = None
+    if n_api > 0:
+        r.synchronize()
+        first = 1 + a.warmup + a.steps + n_unfused
+        t2 = time.perf_counter()
+        for k in range(n_api):
+            r.render(mvp, seeds[first + k])
+        r.synchronize()
+        el2 = time.perf_counter() - t2
+        render_api = {"value": round(R * R * S * n_api / el2 / 1e6, 3),
+                      "ms_per_step": round(el2 * 1e3 / n_api, 5), "steps": n_api,
+                      "note": "one render() call per pass through the C-ABI (ctypes); the "
+                              "library fuses queued passes into multi-pass launches"}
+
     traffic = None
     tp = Path(a.traffic_json)
     if tp.exists():
@@ -249,6 +270,7 @@ def main():
                          "kernel_us_per_pass": round(kern_ms_max * 1e3 / a.steps, 3),
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "unfused": unfused,
+            "render_api": render_api,
             "cpu_baseline": None,
             "volume_gen_s": round(gen_s, 2),
         }

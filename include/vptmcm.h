@@ -151,7 +151,12 @@ int vptmcm_reset(vptmcm* h, const float* mvp_inverse /* 16 */, uint32_t seed_bit
 
 /* _renderFrame (js:262-376) -> render compute_main (wgsl:107-179): one
  * progressive pass of `steps` photon-steps per photon, then the rgba16float
- * render target is rewritten. Asynchronous. */
+ * render target is rewritten. Asynchronous, and lazily fused: consecutive
+ * render() calls with the same matrix are queued (up to 32) and launched as
+ * one multi-pass march (photon state stays in registers between the passes)
+ * as soon as any other entry point is called, so every observable result is
+ * that of the passes run one by one. The no-volume error is still reported
+ * here, synchronously. */
 int vptmcm_render(vptmcm* h, const float* mvp_inverse /* 16 */, uint32_t seed_bits);
 
 /* n back-to-back passes with seeds[0..n) (one enqueue; for progressive

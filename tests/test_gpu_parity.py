@@ -287,6 +287,39 @@ def test_fused_passes_bitexact(layout, R):
     gpu.close()
 
 
+def test_lazily_fused_render_calls():
+    """render() queues passes and launches them fused when anything else is
+    called (here: 40 renders = 32 + 8 with a matrix change in between, a
+    parameter setter and reads): photons and image equal the oracle's passes
+    one by one, and the launch count shows the fusion happened."""
+    gpu, cpu = make_pair(64, cf.two_spheres(48), cf.tf_materials(True), ext=24.0)
+    m1, m2 = cf.golden_mvp("orbit"), cf.golden_mvp("near")
+    seeds = cf.seed_stream(60, start=11)
+    gpu.reset(m1, seeds[0])
+    cpu.reset(m1, seeds[0])
+    gpu.enable_kernel_timing(True)
+    for s in seeds[1:41]:
+        gpu.render(m1, s)
+        cpu.render(m1, s)
+    for s in seeds[41:47]:
+        gpu.render(m2, s)
+        _, want = cpu.render(m2, s)
+    ms, n = gpu.kernel_time()  # flushes the queue
+    assert n == 3, n  # 32 + 8 passes with m1, 6 with m2
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "lazy fused")
+    assert_rgba_equal(gpu.read_rgba16f(), want, "lazy fused")
+    gpu.render(m2, seeds[47])
+    cpu.render(m2, seeds[47])
+    gpu.set_params(extinction=12.0, bounces=8, steps=8)  # flushes with the old params
+    cpu.params.update(extinction=12.0)
+    for s in seeds[48:52]:
+        gpu.render(m2, s)
+        _, want = cpu.render(m2, s)
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "lazy fused after setter")
+    assert_rgba_equal(gpu.read_rgba16f(), want, "lazy fused after setter")
+    gpu.close()
+
+
 def test_schedule_and_fusion_knobs_agree(monkeypatch):
     """The tile schedule (variant bit 1 = raster mapping) and pass fusion
     (variant bit 2 = one launch per pass) only change which wave runs a tile and

@@ -81,6 +81,12 @@ struct vptmcm {
   hipEvent_t comp_ready[2] = {nullptr, nullptr};
   hipEvent_t comp_done[2] = {nullptr, nullptr};
   int comp_next = 0, comp_last = -1;
+  // Lazily fused render() calls: consecutive passes with one matrix are queued
+  // and launched as one multi-pass march when anything observes or changes
+  // the renderer (every other entry point flushes first), or at 32 passes.
+  uint32_t pend_n = 0;
+  uint32_t pend_seeds[kMaxFusedPasses];
+  float pend_mvp[16];
   double* host_scratch = nullptr;
 
   std::string err;
@@ -333,6 +339,15 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   return VPTMCM_OK;
 }
 
+// Launch the queued render() passes (see vptmcm::pend_n).
+int flush_renders(vptmcm* h) {
+  if (h->pend_n == 0) return VPTMCM_OK;
+  const uint32_t n = h->pend_n;
+  h->pend_n = 0;
+  HIPCHK(h, hipSetDevice(h->device));
+  return do_march(h, h->pend_mvp, h->pend_seeds, n);
+}
+
 void free_volume(vptmcm* h) {
   if (h->vol_lin) (void)hipFree(h->vol_lin);
   if (h->vol_c8) (void)hipFree(h->vol_c8);
@@ -473,6 +488,7 @@ void vptmcm_destroy(vptmcm* h) {
 
 int vptmcm_volume_begin(vptmcm* h, uint32_t width, uint32_t height, uint32_t depth) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!width || !height || !depth || width > 8192 || height > 8192 || depth > 8192)
     FAIL(h, VPTMCM_EINVAL, "volume dimensions must be in [1, 8192]");
   HIPCHK(h, hipSetDevice(h->device));
@@ -493,6 +509,7 @@ int vptmcm_volume_begin(vptmcm* h, uint32_t width, uint32_t height, uint32_t dep
 int vptmcm_volume_write_block(vptmcm* h, const uint8_t* data, uint32_t x, uint32_t y, uint32_t z,
                               uint32_t bw, uint32_t bh, uint32_t bd) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!h->vol_lin) FAIL(h, VPTMCM_ESTATE, "volume_write_block before volume_begin");
   if (!data) FAIL(h, VPTMCM_EINVAL, "null block data");
   if ((uint64_t)x + bw > h->W || (uint64_t)y + bh > h->H || (uint64_t)z + bd > h->D)
@@ -517,6 +534,7 @@ int vptmcm_volume_write_block(vptmcm* h, const uint8_t* data, uint32_t x, uint32
 
 int vptmcm_volume_end(vptmcm* h) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!h->vol_lin) FAIL(h, VPTMCM_ESTATE, "volume_end before volume_begin");
   HIPCHK(h, hipSetDevice(h->device));
   if (h->layout == kLayoutCorner8) {
@@ -539,6 +557,7 @@ int vptmcm_volume_end(vptmcm* h) {
 int vptmcm_set_volume(vptmcm* h, const uint8_t* voxels, uint32_t width, uint32_t height,
                       uint32_t depth) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!voxels) FAIL(h, VPTMCM_EINVAL, "set_volume: null voxels");
   int rc = vptmcm_volume_begin(h, width, height, depth);
   if (rc) return rc;
@@ -549,6 +568,7 @@ int vptmcm_set_volume(vptmcm* h, const uint8_t* voxels, uint32_t width, uint32_t
 
 int vptmcm_set_material_tf(vptmcm* h, const uint8_t* rgba) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!rgba) FAIL(h, VPTMCM_EINVAL, "set_material_tf: null data");
   HIPCHK(h, hipSetDevice(h->device));
   // Re-layout for the march: (albedo, alpha) u16 texels (LDS-staged) and the
@@ -583,6 +603,7 @@ int vptmcm_set_material_tf(vptmcm* h, const uint8_t* rgba) {
 
 int vptmcm_set_light(vptmcm* h, const uint8_t* spd, const float dir[3]) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!spd || !dir) FAIL(h, VPTMCM_EINVAL, "set_light: null argument");
   HIPCHK(h, hipSetDevice(h->device));
   memcpy(h->light_host, spd, 256);
@@ -594,6 +615,7 @@ int vptmcm_set_light(vptmcm* h, const uint8_t* spd, const float dir[3]) {
 
 int vptmcm_set_spectrum(vptmcm* h, const float* buf) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!buf) FAIL(h, VPTMCM_EINVAL, "set_spectrum: null buffer");
   float nbf = buf[0] + 0.5f;
   if (!(nbf >= 0.0f) || nbf >= (float)(VPTMCM_MAX_BINS + 1))
@@ -604,6 +626,7 @@ int vptmcm_set_spectrum(vptmcm* h, const float* buf) {
 
 int vptmcm_set_transfer_function(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (h->kind != VPTMCM_RENDERER_RGB)
     FAIL(h, VPTMCM_ESTATE, "set_transfer_function: the spectral renderer uses set_material_tf");
   if (!rgba || width == 0 || height == 0 || width > kRgbTfMax)
@@ -626,6 +649,7 @@ int vptmcm_set_transfer_function(vptmcm* h, const uint8_t* rgba, uint32_t width,
 
 int vptmcm_set_environment(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!rgba || width != 1 || height != 1)
     FAIL(h, VPTMCM_EINVAL, "set_environment: only the 1x1 environment of the rendering context "
                            "(WebGPURenderingContext.js:97-108) is supported");
@@ -635,6 +659,7 @@ int vptmcm_set_environment(vptmcm* h, const uint8_t* rgba, uint32_t width, uint3
 
 int vptmcm_set_params(vptmcm* h, const vptmcm_params* p) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!p) FAIL(h, VPTMCM_EINVAL, "set_params: null params");
   h->params = *p;
   return VPTMCM_OK;
@@ -644,6 +669,7 @@ int vptmcm_set_params(vptmcm* h, const vptmcm_params* p) {
 
 int vptmcm_reset(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!mvp) FAIL(h, VPTMCM_EINVAL, "reset: null matrix");
   HIPCHK(h, hipSetDevice(h->device));
   MarchParams P = make_params(h, mvp, seed_bits);
@@ -657,12 +683,21 @@ int vptmcm_reset(vptmcm* h, const float* mvp, uint32_t seed_bits) {
 int vptmcm_render(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (!mvp) FAIL(h, VPTMCM_EINVAL, "render: null matrix");
-  HIPCHK(h, hipSetDevice(h->device));
-  return do_march(h, mvp, &seed_bits, 1u);
+  if (!h->volume_ready) FAIL(h, VPTMCM_ESTATE, "render: no volume set (setVolume first)");
+  // queue the pass; a different matrix or a full queue launches the queue
+  // first (the launch order, and so every result, is unchanged)
+  if (h->pend_n == kMaxFusedPasses || (h->pend_n && memcmp(h->pend_mvp, mvp, sizeof h->pend_mvp))) {
+    int rc = flush_renders(h);
+    if (rc) return rc;
+  }
+  if (h->pend_n == 0) memcpy(h->pend_mvp, mvp, sizeof h->pend_mvp);
+  h->pend_seeds[h->pend_n++] = seed_bits;
+  return VPTMCM_OK;
 }
 
 int vptmcm_render_passes(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!mvp || (!seeds && n)) FAIL(h, VPTMCM_EINVAL, "render_passes: null argument");
   HIPCHK(h, hipSetDevice(h->device));
   const uint32_t fuse = (h->variant & 4u) ? 1u : kMaxFusedPasses;  // variant bit 2: one pass per launch
@@ -675,6 +710,7 @@ int vptmcm_render_passes(vptmcm* h, const float* mvp, const uint32_t* seeds, uin
 
 int vptmcm_synchronize(vptmcm* h) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   HIPCHK(h, hipSetDevice(h->device));
   int rc = time_close(h);
   if (rc) return rc;
@@ -687,6 +723,7 @@ int vptmcm_synchronize(vptmcm* h) {
 
 int vptmcm_read_rgba16f(vptmcm* h, uint16_t* out) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!out) FAIL(h, VPTMCM_EINVAL, "read_rgba16f: null output");
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipMemcpyAsync(out, h->rgba, (size_t)h->R * h->R * 8, hipMemcpyDeviceToHost,
@@ -697,6 +734,7 @@ int vptmcm_read_rgba16f(vptmcm* h, uint16_t* out) {
 
 int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!params) FAIL(h, VPTMCM_EINVAL, "tonemap_artistic: null params");
   HIPCHK(h, hipSetDevice(h->device));
   const size_t npx = (size_t)h->R * h->R;
@@ -720,6 +758,7 @@ int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out
 
 int vptmcm_read_photons(vptmcm* h, void* out) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!out) FAIL(h, VPTMCM_EINVAL, "read_photons: null output");
   HIPCHK(h, hipSetDevice(h->device));
   std::vector<uint32_t> planes((size_t)kNumPlanes * h->npad);
@@ -763,6 +802,7 @@ int vptmcm_read_photons(vptmcm* h, void* out) {
 
 int vptmcm_write_photons(vptmcm* h, const void* in) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!in) FAIL(h, VPTMCM_EINVAL, "write_photons: null input");
   HIPCHK(h, hipSetDevice(h->device));
   std::vector<uint32_t> planes((size_t)kNumPlanes * h->npad, 0u);
@@ -802,6 +842,7 @@ int vptmcm_write_photons(vptmcm* h, const void* in) {
 
 int vptmcm_enable_kernel_timing(vptmcm* h, int enable) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->timing = enable != 0;
@@ -812,6 +853,7 @@ int vptmcm_enable_kernel_timing(vptmcm* h, int enable) {
 
 int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!total_ms || !launches) FAIL(h, VPTMCM_EINVAL, "kernel_time: null output");
   HIPCHK(h, hipSetDevice(h->device));
   int rc = time_close(h);
@@ -861,6 +903,7 @@ int vptmcm_comm_unique_id(uint8_t* out) {
 
 int vptmcm_comm_init(vptmcm* h, const uint8_t* uid, int nranks, int rank) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!uid || nranks < 1 || rank < 0 || rank >= nranks)
     FAIL(h, VPTMCM_EINVAL, "comm_init: bad arguments (nranks=%d rank=%d)", nranks, rank);
   if (h->comm) FAIL(h, VPTMCM_ESTATE, "comm_init: communicator already initialised");
@@ -884,6 +927,7 @@ int vptmcm_comm_init(vptmcm* h, const uint8_t* uid, int nranks, int rank) {
 
 int vptmcm_comm_allreduce_radiance(vptmcm* h) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!h->comm) FAIL(h, VPTMCM_ECOMM, "comm_allreduce_radiance: no communicator");
   HIPCHK(h, hipSetDevice(h->device));
   int k = h->comp_next;
@@ -903,6 +947,7 @@ int vptmcm_comm_allreduce_radiance(vptmcm* h) {
 
 int vptmcm_comm_read_composite(vptmcm* h, float* rgb, float* counts) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!h->comm || h->comp_last < 0) FAIL(h, VPTMCM_ESTATE, "read_composite: no all-reduce issued");
   if (!rgb) FAIL(h, VPTMCM_EINVAL, "read_composite: null output");
   HIPCHK(h, hipSetDevice(h->device));
@@ -925,6 +970,7 @@ int vptmcm_comm_barrier(vptmcm* h) {
 
 int vptmcm_comm_allreduce_host(vptmcm* h, double* vals, int n, int op) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!h->comm) FAIL(h, VPTMCM_ECOMM, "comm_allreduce_host: no communicator");
   if (!vals || n < 1 || n > 64 || op < 0 || op > 1)
     FAIL(h, VPTMCM_EINVAL, "comm_allreduce_host: bad arguments");
@@ -944,6 +990,7 @@ int vptmcm_comm_allreduce_host(vptmcm* h, double* vals, int n, int op) {
 
 int vptmcm_debug_eval(vptmcm* h, int fn, const uint32_t* in, uint32_t* out, uint32_t n) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (fn < 0 || fn > 4 || (!in && n) || (!out && n)) FAIL(h, VPTMCM_EINVAL, "debug_eval: bad args");
   if (n == 0) return VPTMCM_OK;
   HIPCHK(h, hipSetDevice(h->device));
@@ -966,6 +1013,7 @@ int vptmcm_debug_eval(vptmcm* h, int fn, const uint32_t* in, uint32_t* out, uint
 int vptmcm_debug_verify(vptmcm* h, int fn, uint32_t lo, uint64_t count, uint64_t* mismatches,
                         uint32_t* first_bad, uint32_t nfirst) {
   if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   if (!mismatches || (nfirst && !first_bad)) FAIL(h, VPTMCM_EINVAL, "debug_verify: bad args");
   HIPCHK(h, hipSetDevice(h->device));
   unsigned long long* dbad = nullptr;
