@@ -250,9 +250,11 @@ __device__ __forceinline__ void wave_record(uint32_t tile, bool entered, unsigne
 #endif
 
 // sample_light (wgsl:62-73) for a leaving photon; light_dir is pre-normalised
+// DIRL: the launch's light has a direction (FAST launches), no uniform test.
+template <bool DIRL = false>
 __device__ __forceinline__ float exit_radiance(const MarchParams& P, f3 dir, const WaveConst& wc) {
   float rad = wc.intensity;
-  if (!P.light_iso) {
+  if (DIRL || !P.light_iso) {
     float cosl = fmaf(dir.z, P.light_dir[2], fmaf(dir.y, P.light_dir[1], dir.x * P.light_dir[0]));
     rad = smax(cosl * wc.intensity, 0.0f);
   }
@@ -395,8 +397,9 @@ __device__ __forceinline__ const __attribute__((address_space(4))) float* cmf_ta
 // MODE: 0 generic; 1 every radiance bin in use (nb >= 12); 2 (FAST, the
 // benchmark configuration) additionally equal-width bins (bin_of's arithmetic
 // path), a wavelength-invariant TF blue channel (LDS row table), blur == 0 with
-// an even R (every near point fixed) and a host-bounded |w| (one-compare
-// reciprocal guard): the per-step configuration branches vanish.
+// an even R (every near point fixed), a host-bounded |w| (one-compare
+// reciprocal guard) and a directional light: the per-step configuration
+// branches vanish.
 template <uint32_t L, bool SPEC, uint32_t MODE>
 __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const MarchParams P,
                                                        const TileSched T, float* __restrict__ ph,
@@ -595,7 +598,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         uint32_t h1 = pcg_hash(sw), h2 = pcg_hash(h1), h3 = pcg_hash(h2);
         uint32_t h4 = pcg_hash(h3), h5 = pcg_hash(h4);
         p.samples++;
-        set_pending((float)p.samples, exit_radiance(P, p.dir, wc), p.bin);
+        set_pending((float)p.samples, exit_radiance<FAST>(P, p.dir, wc), p.bin);
         p.dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
         p.bounces = 0u;
         p.lambda = lambda_of(P, h5);
@@ -636,7 +639,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         if (!fixed) disk_of(h1, h2, dx, dy);
         Photon rc;
         reset_from_draws<FAST>(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
-        terminate(exit_radiance(P, p.dir, wc), rc);
+        terminate(exit_radiance<FAST>(P, p.dir, wc), rc);
         wc = wave_const(rc.lambda, s_light);
         st = h5;
         STAMP(1);
@@ -724,7 +727,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 
       if (oob || wheel < pabs) {
         // exit (wgsl:142-150) or absorption (wgsl:151-155): adopt the candidate
-        terminate(oob ? exit_radiance(P, p.dir, wc) : 0.0f, rc);
+        terminate(oob ? exit_radiance<FAST>(P, p.dir, wc) : 0.0f, rc);
         wc = wcr;
         st = h5;
       } else if (wheel < pabs + pscat) {
@@ -783,7 +786,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 
       if (oob || wheel < pabs) {
         // exit (wgsl:142-150) or absorption (wgsl:151-155)
-        float rad = oob ? exit_radiance(P, p.dir, wc) : 0.0f;  // sample_light, wgsl:62-73
+        float rad = oob ? exit_radiance<FAST>(P, p.dir, wc) : 0.0f;  // sample_light, wgsl:62-73
         p.samples++;
         add_radiance<NBF>(P, p.rad, rcp((float)p.samples), p.bin, rad);
         photon_reset(P, p, sx, sy, fixed, from, st);
@@ -1134,7 +1137,7 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   const bool spec = (variant & 1u) == 0u;  // variant bit 0: plain (non-speculative) step
   const bool nbf = P.nb >= (uint32_t)kMaxBins;  // every radiance bin in use
   const bool fast = nbf && P.bins_uniform && P.b_rows && P.w_bounded && P.blur == 0.0f &&
-                    (P.R & 1u) == 0u;
+                    (P.R & 1u) == 0u && !P.light_iso;
   // hipExtLaunchKernelGGL stamps the events from the dispatch packet itself
   // (no extra barrier/marker packets between back-to-back launches)
 #define VPT_LAUNCH(LAY, SP, MO)                                                                \

@@ -253,15 +253,14 @@ __device__ __forceinline__ int axis_floor(float u, float n, float* f) {
   *f = x - fl;
   return (int)fl;
 }
-// clampc for a quiet (arithmetic-result) input: v_max_f32 then v_min_f32
-// with IEEE-mode NaN handling (a quiet NaN yields the other operand, so NaN
-// -> -1 like clampc). Exact equality with clampc on every non-signalling bit
-// pattern is proven exhaustively (tests/test_gpu_fastmath.py, fn 15). The
-// asm keeps the backend from adding canonicalising v_max before fmaxf/fminf.
+// clampc for a quiet (arithmetic-result) input: minNum(maxNum(u, -1), 2), a
+// quiet NaN yielding the other operand (NaN -> -1 like clampc). The backend
+// emits a canonicalising v_max + v_med3_f32 (the earlier inline-asm v_max/
+// v_min pair cost the same plus hazard s_nops). Exact equality with clampc on
+// every non-signalling bit pattern is proven exhaustively
+// (tests/test_gpu_fastmath.py, fn 15).
 __device__ __forceinline__ float clampc_q(float u) {
-  float r;
-  asm("v_max_f32 %0, -1.0, %1\n\tv_min_f32 %0, 2.0, %0" : "=&v"(r) : "v"(u));
-  return r;
+  return __builtin_fminf(__builtin_fmaxf(u, -1.0f), 2.0f);
 }
 __device__ __forceinline__ int axis_floor_q(float u, float n, float* f) {
   float x = fmaf(clampc_q(u), n, -0.5f);
