@@ -264,12 +264,11 @@ __device__ __forceinline__ f3 ray_start_hw(f3 from, f3 omf, f3 dir) {
       rz = bz ? rcp_slow(dir.z) : rz;
     }
   }
-  // (builtin minNum/maxNum on arithmetic results: plain v_min/v_max/v_max3,
-  // no canonicalisation and no inline-asm hazard padding)
-  float t1x = __builtin_fminf(-from.x * rx, omf.x * rx);
-  float t1y = __builtin_fminf(-from.y * ry, omf.y * ry);
-  float t1z = __builtin_fminf(-from.z * rz, omf.z * rz);
-  float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(t1x, t1y), t1z), 0.0f);
+  // (on arithmetic results: plain v_min/v_max/v_max3, no canonicalisation)
+  float t1x = hw_min(-from.x * rx, omf.x * rx);
+  float t1y = hw_min(-from.y * ry, omf.y * ry);
+  float t1z = hw_min(-from.z * rz, omf.z * rz);
+  float tn = hw_max(hw_max3(t1x, t1y, t1z), 0.0f);
   return f3{fmaf(tn, dir.x, from.x), fmaf(tn, dir.y, from.y), fmaf(tn, dir.z, from.z)};
 }
 // A lane whose near point is fixed and has no coordinate equal to 0 or 1.

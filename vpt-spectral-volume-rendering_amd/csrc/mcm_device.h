@@ -276,24 +276,15 @@ __device__ __forceinline__ int axis_floor_in(float u, float n, float* f) {
   *f = x - fl;
   return (int)fl;
 }
-// Hardware min/max (IEEE minNum/maxNum). They equal smin/smax whenever no
-// operand is a signalling NaN and the operands are not a (+0, -0) pair
-// (fn 16 checks the pairing rule over every bit pattern of one operand
-// against special and neighbouring values of the other).
-__device__ __forceinline__ float hw_min(float a, float b) {
-  float r;
-  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ float hw_max(float a, float b) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
+// IEEE minNum/maxNum (v_min_f32 / v_max_f32 / v_max3_f32; the backend adds a
+// canonicalising v_max only for operands it cannot prove quiet). They equal
+// smin/smax whenever no operand is a signalling NaN and the operands are not a
+// (+0, -0) pair (fn 16 checks the pairing rule over every bit pattern of one
+// operand against special and neighbouring values of the other).
+__device__ __forceinline__ float hw_min(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ float hw_max(float a, float b) { return __builtin_fmaxf(a, b); }
 __device__ __forceinline__ float hw_max3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+  return __builtin_fmaxf(__builtin_fmaxf(a, b), c);
 }
 
 // max(min(i, hi), 0) for hi >= 0 (the same value as i < 0 ? 0 : i > hi ? hi : i): one v_med3_i32
