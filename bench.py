@@ -40,8 +40,12 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=192, help="timed passes")
-    ap.add_argument("--warmup", type=int, default=16, help="untimed passes")
+    ap.add_argument("--steps", type=int, default=1024, help="timed passes")
+    # the engine clock ramps up over the first ~30 ms of sustained work (DVFS):
+    # 4096 untimed passes (~65 ms) settle it, so the timed region measures the
+    # sustained rate (measured: 19.8 us/pass after 0 warm-up passes, 18.2 after
+    # 32, 17.4 after 512, 15.6-15.8 after 2048 and 8192)
+    ap.add_argument("--warmup", type=int, default=4096, help="untimed passes")
     ap.add_argument("--resolution", type=int, default=512)
     ap.add_argument("--volume", type=int, default=512)
     ap.add_argument("--photon-steps", type=int, default=8, help="S: steps per pass")
@@ -50,16 +54,16 @@ def parse():
     ap.add_argument("--tf", choices=["spectral", "grey", "zero"], default="spectral")
     ap.add_argument("--camera", choices=["default", "near", "orbit", "orbit_tilted"],
                     default="default", help="golden camera pose (non-default: analysis only)")
-    ap.add_argument("--fuse", type=int, default=16,
+    ap.add_argument("--fuse", type=int, default=32,
                     help="passes per march launch (render_passes; photon state stays in "
                          "registers between them, every pass stores its image); 1 = one launch "
                          "per render() call")
-    ap.add_argument("--allreduce-every", type=int, default=16,
+    ap.add_argument("--allreduce-every", type=int, default=32,
                     help="passes between radiance all-reduces (N > 1)")
     ap.add_argument("--unfused-steps", type=int, default=64,
                     help="passes of a second timed region at one launch per pass (reported "
                          "as 'unfused'; 0 = skip; N = 1 only)")
-    ap.add_argument("--api-steps", type=int, default=64,
+    ap.add_argument("--api-steps", type=int, default=256,
                     help="passes of a third timed region through the drop-in render() entry "
                          "point, one call per pass (lazily fused by the library; reported as "
                          "'render_api'; 0 = skip; N = 1 only)")

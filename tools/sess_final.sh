@@ -14,7 +14,7 @@ timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json; fault $rc && exit $rc
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --cpu-seconds 0 > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err")
 rc=$?; echo "prof rc=$rc"; fault $rc && exit $rc
-for cfg in "bench|--steps 32 --warmup 16 --unfused-steps 0 --cpu-seconds 0" "calib|--steps 32 --warmup 16 --unfused-steps 0 --cpu-seconds 0 --fuse 1 --photon-steps 0"; do
+for cfg in "bench|--steps 32 --warmup 32 --unfused-steps 0 --api-steps 0 --cpu-seconds 0" "calib|--steps 32 --warmup 16 --unfused-steps 0 --api-steps 0 --cpu-seconds 0 --fuse 1 --photon-steps 0"; do
   name=${cfg%%|*}; args=${cfg#*|}
   for c in FETCH_SIZE WRITE_SIZE; do
     (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c -d "$GRAFT_REPO_ROOT/$OUT/pmc_${name}_$c" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" $args > "$GRAFT_REPO_ROOT/$OUT/pmc_${name}_$c.json" 2> "$GRAFT_REPO_ROOT/$OUT/pmc_${name}_$c.err")

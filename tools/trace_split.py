@@ -2,7 +2,7 @@
 """Split a rocprofv3 kernel trace's k_march dispatches into the bench's launch
 kinds (fused multi-pass launches vs one-pass launches) so the per-launch
 average can be compared with bench.py's event-timed kernel_avg_us.
-Usage: python tools/trace_split.py run_kernel_trace.csv [out.json]"""
+Usage: python tools/trace_split.py run_kernel_trace.csv [out.json [W K F]]"""
 import csv
 import json
 import sys
@@ -16,9 +16,19 @@ def main():
     # the one-pass launches of the unfused region
     long_ = [x for x in d if x > 100.0]
     short = [x for x in d if x <= 100.0]
+    # bench order: warm-up launches, timed launches, one-pass launches, then the
+    # render_api launches; counts from the bench defaults unless given
+    W = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
+    K = int(sys.argv[4]) if len(sys.argv) > 4 else 1024
+    F = int(sys.argv[5]) if len(sys.argv) > 5 else 32
+    warm, timed = -(-W // F), -(-K // F)
+    t = long_[warm:warm + timed]
+    api = long_[warm + timed:]
     out = {"k_march_dispatches": len(d),
            "fused_launches": {"n": len(long_), "avg_us": round(sum(long_) / max(1, len(long_)), 3),
-                              "timed_avg_us (excl. warm-up)": round(sum(long_[1:]) / max(1, len(long_) - 1), 3)},
+                              "timed_region_avg_us": round(sum(t) / max(1, len(t)), 3),
+                              "timed_region_n": len(t),
+                              "render_api_avg_us": round(sum(api) / max(1, len(api)), 3) if api else None},
            "one_pass_launches": {"n": len(short), "avg_us": round(sum(short) / max(1, len(short)), 3)}}
     s = json.dumps(out, indent=1)
     print(s)
