@@ -72,6 +72,10 @@ def parse():
                          "roofline fields are then null)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="budget of the CPU-oracle baseline (0 = skip)")
+    ap.add_argument("--general-steps", type=int, default=64,
+                    help="passes of a timed region on the general (non-FAST) march: a UI-like "
+                         "TF with wavelength-varying anisotropy and 8 uneven bins (reported as "
+                         "'general'; 0 = skip; N = 1 only)")
     ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (profiles/), if present")
     return ap.parse_args()
@@ -98,7 +102,7 @@ def cpu_baseline(vol, tf, spec, spd, ldir, mvp, R, S, ext, budget_s):
         if el >= budget_s:
             break
     return {"value": round(R * R * S * passes / el / 1e6, 3), "unit": "Mphoton-steps/s",
-            "cores": threads, "kind": "port",
+            "cores": threads, "kind": "port", "host_cpus": os.cpu_count(),
             "sample": f"C oracle (oracle/mcm_oracle.c), {passes} full passes of the same "
                       f"{R}x{R}x{S} workload after 1 warm-up pass, {el:.1f} s, {threads} pthreads"}
 
@@ -146,6 +150,15 @@ def main():
     seeds = cf.seed_stream(a.warmup + a.steps + n_unfused + n_api + 1, start=0, rank=rank)
     F = max(1, min(a.fuse, 32))
     every = max(1, a.allreduce_every)
+
+    def passes_on(sd, first: int, count: int, F: int = F) -> list:
+        launches, done = [], 0
+        while done < count:
+            n = min(F, count - done)
+            r.render_passes(mvp, sd[first + done:first + done + n])
+            launches.append(n)
+            done += n
+        return launches
 
     def passes(first: int, count: int, F: int = F) -> list:
         """Enqueue `count` passes from seeds[first:] in launches of <= F passes,
@@ -239,16 +252,50 @@ def main():
                       "note": "one render() call per pass through the C-ABI (ctypes); the "
                               "library fuses queued passes into multi-pass launches"}
 
-    traffic = None
+    # The launch shape that actually ran (the last launch of a region can be
+    # shorter than --fuse, and --steps < --fuse gives one short launch).
+    shapes = sorted(set(launches))
+    ppl = shapes[0] if len(shapes) == 1 else shapes
+    # PMC-derived memory-side bytes per launch (profiles/): attached only when a
+    # profile of this exact launch shape (R, S, layout, volume, passes) exists.
+    traffic, traffic_src = None, None
     tp = Path(a.traffic_json)
-    if tp.exists():
+    if tp.exists() and len(shapes) == 1:
         try:
             t = json.loads(tp.read_text())
-            if (t.get("resolution") == R and t.get("steps") == S and t.get("layout") == a.layout
-                    and t.get("passes_per_launch", 1) == F):
-                traffic = t.get("hbm_bytes_per_launch")
+            for e in t.get("entries", [t]):
+                if (e.get("resolution") == R and e.get("steps") == S and e.get("layout") == a.layout
+                        and e.get("volume", 512) == a.volume
+                        and e.get("passes_per_launch", 1) == shapes[0]):
+                    traffic = e.get("hbm_bytes_per_launch")
+                    traffic_src = f"{tp.relative_to(REPO) if tp.is_relative_to(REPO) else tp}"
         except (ValueError, OSError):
             traffic = None
+
+    # The general (non-FAST) march on the same volume: MODE 0 specialisation
+    # (8 uneven bins, wavelength-varying anisotropy from the 4-corner table)
+    general = None
+    if a.general_steps > 0 and not multi:
+        r.synchronize()
+        r.set_material_tf(cf.tf_materials(True))
+        r.set_spectrum(cf.spectrum_buffer("8_uneven"))
+        gseeds = cf.seed_stream(a.general_steps + 33, start=1, rank=rank)
+        r.reset(mvp, gseeds[0])
+        r.render_passes(mvp, gseeds[1:33])
+        r.synchronize()
+        r.enable_kernel_timing(not a.no_timing)
+        t3 = time.perf_counter()
+        gl = passes_on(gseeds, 33, a.general_steps)
+        r.synchronize()
+        el3 = time.perf_counter() - t3
+        gk_ms, gn = r.kernel_time()
+        general = {"value": round(R * R * S * a.general_steps / el3 / 1e6, 3),
+                   "ms_per_step": round(el3 * 1e3 / a.general_steps, 5),
+                   "steps": a.general_steps, "passes_per_launch": sorted(set(gl)),
+                   "kernel_us_per_pass": (round(gk_ms * 1e3 / a.general_steps, 3)
+                                          if not a.no_timing else None),
+                   "workload": "same volume/camera, tf_materials(varying anisotropy), "
+                               "8_uneven bins: the generic march specialisation"}
 
     if rank == 0:
         out = {
@@ -261,20 +308,21 @@ def main():
                             f"(HG g=0.702), R={R}, S={S}, 12 bins, extinction {a.extinction}, "
                             f"{a.camera} camera",
                 "resolution": R, "photon_steps_per_pass": S, "volume": a.volume,
-                "volume_layout": a.layout, "passes_per_launch": F,
+                "volume_layout": a.layout, "passes_per_launch": ppl,
                 "parallelism": (f"photon-parallel replicas x{world}, RCCL all-reduce of (rgb*n, n) "
                                 f"every {every} pass(es)") if multi else "single GPU",
             },
             "hbm_gbps_algorithmic": round(achieved, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_march", "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
-                         "passes_per_launch": F,
+                         "passes_per_launch": ppl,
                          "kernel_us_per_pass": round(kern_ms_max * 1e3 / a.steps, 3),
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "unfused": unfused,
             "render_api": render_api,
+            "general": general,
             "cpu_baseline": None,
             "volume_gen_s": round(gen_s, 2),
         }

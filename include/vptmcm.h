@@ -173,6 +173,19 @@ int vptmcm_synchronize(vptmcm* h);
  * pixel (x, y) at ((y*R)+x)*4 (textureStore(uRadiance, globalId.xy), wgsl:168). */
 int vptmcm_read_rgba16f(vptmcm* h, uint16_t* out);
 
+/* The same image in fp32, before its rgba16float rounding: R*R*3 floats,
+ * pixel (x, y) at ((y*R)+x)*3. These are the values
+ * PhotonSpectral_radiance_to_rgb returns (wgsl:319-326) and textureStore
+ * rounds (wgsl:168); SURVEY 8(a) a13 / 8(b) vptmcm_read_rgb. Written by the
+ * last pass of every march launch (zero before the first render). */
+int vptmcm_read_rgb(vptmcm* h, float* rgb_out);
+
+/* The (rgb * n, n) float4 per pixel that the multi-GPU composite all-reduces
+ * (rgb = the fp32 image above, n = the photon's sample count):
+ * R*R*4 floats, pixel (x, y) at ((y*R)+x)*4. For hosts that composite
+ * replicas with their own transport; the composite is sum(rgb*n)/sum(n). */
+int vptmcm_pack_radiance(vptmcm* h, float* out);
+
 /* The photon buffer in the reference's layout, photon of pixel (x, y) at
  * index y*R + x: the 144-byte PhotonSpectral (wgsl:238-247; out holds R*R*144
  * bytes; the transmittance field, never read by the kernel, is returned as

@@ -57,15 +57,22 @@ def make_pair(R, vol, tf, spec="12", ext=32.0, layout=vptmcm.LAYOUT_CORNER8, lig
     return gpu, cpu
 
 
+def assert_rgb32_equal(got, want, what=""):
+    """a13 before the f16 store: the fp32 radiance_to_rgb result, bit for bit."""
+    ok = same_words(got.view(np.uint32), want.view(np.uint32))
+    assert ok.all(), f"{what}: {int((~ok).sum())} fp32 rgb words differ"
+
+
 def run_and_compare(gpu, cpu, mvp, seeds, what, nthreads=16):
     gpu.reset(mvp, seeds[0])
     cpu.reset(mvp, seeds[0], nthreads=nthreads)
     assert_photons_equal(gpu.read_photons(), cpu.photons, what + " reset")
     for k, s in enumerate(seeds[1:], 1):
         gpu.render(mvp, s)
-        _, want = cpu.render(mvp, s, nthreads=nthreads)
+        rgb, want = cpu.render(mvp, s, nthreads=nthreads)
         assert_photons_equal(gpu.read_photons(), cpu.photons, f"{what} pass {k}")
         assert_rgba_equal(gpu.read_rgba16f(), want, f"{what} pass {k}")
+        assert_rgb32_equal(gpu.read_rgb(), rgb, f"{what} pass {k}")
 
 
 def test_math_primitives_bitexact():
@@ -244,11 +251,11 @@ def test_composite_single_rank():
         gpu.render(mvp, s)
         gpu.allreduce_radiance()
     rgb, n = gpu.read_composite()
-    img = gpu.read_rgba16f()[..., :3].view(np.float16).astype(np.float32)
+    img = gpu.read_rgb()  # the composite weights the fp32 image, not its f16 rounding
     ph = gpu.read_photons()
     assert np.array_equal(n.reshape(-1), ph[:, 7].astype(np.float32))
     m = n > 0
-    np.testing.assert_allclose(rgb[m], img[m], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(rgb[m], img[m], rtol=3e-7, atol=0)  # (rgb*n)/n: <= 2 roundings
     gpu.barrier()
     v = gpu.allreduce_host([1.0, 2.0], op="max")
     assert list(v) == [1.0, 2.0]
@@ -425,4 +432,93 @@ def test_large_frame_rows_against_oracle():
         assert_photons_equal(got[y0:y1].reshape(-1, got.shape[-1]), exp[y0:y1].reshape(-1, exp.shape[-1]),
                              f"R=2048 rows {y0}:{y1}")
         assert_rgba_equal(gpu.read_rgba16f()[y0:y1], want[y0:y1], f"R=2048 rows {y0}:{y1}")
+    gpu.close()
+
+
+def _oracle_pack(cpu, rgb32):
+    """(rgb*n, n) per pixel in f32, as k_pack forms it (n = photon sample count)."""
+    n = cpu.photons[:, 7].astype(np.float32).reshape(cpu.R, cpu.R)
+    return np.concatenate([rgb32 * n[..., None], n[..., None]], axis=-1).astype(np.float32)
+
+
+def test_c4_two_replica_composite_bitexact():
+    """C4's composite on one GPU, without RCCL: two replicas with the rank seed
+    streams seed_bits(k, 0) and seed_bits(k, 1), each packed by k_pack from its
+    fp32 image, summed on the host; bit-exact against two oracle replicas
+    composited the same way (f32 sum of two terms is order-free; the composite
+    divides by the summed count as vptmcm_comm_read_composite does)."""
+    R, passes = 128, 6
+    vol, tf, mvp = cf.fbm_volume(96, 4, nthreads=8), cf.tf_spectral(), cf.default_mvp_inverse()
+    packs, wants = [], []
+    for rank in (0, 1):
+        gpu, cpu = make_pair(R, vol, tf, ext=32.0)
+        seeds = cf.seed_stream(passes + 1, start=0, rank=rank)
+        gpu.reset(mvp, seeds[0])
+        cpu.reset(mvp, seeds[0], nthreads=16)
+        gpu.render_passes(mvp, seeds[1:])
+        for s in seeds[1:]:
+            rgb, _ = cpu.render(mvp, s, nthreads=16)
+        assert_photons_equal(gpu.read_photons(), cpu.photons, f"replica {rank}")
+        got = gpu.pack_radiance()
+        want = _oracle_pack(cpu, rgb)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"k_pack replica {rank}"
+        packs.append(got)
+        wants.append(want)
+        gpu.close()
+    assert not np.array_equal(packs[0], packs[1]), "rank seed streams must differ"
+    tot, wtot = packs[0] + packs[1], wants[0] + wants[1]
+    assert np.array_equal(tot.view(np.uint32), wtot.view(np.uint32))
+    n = tot[..., 3]
+    comp = np.where(n[..., None] > 0, tot[..., :3] / np.where(n > 0, n, 1)[..., None], 0)
+    assert np.isfinite(comp).all() and (n > 0).mean() > 0.99
+
+
+def test_wide_gather_template_bitexact(monkeypatch):
+    """The 64-bit-offset CORNER8 gather (selected for cell arrays >= 4 GiB, e.g.
+    C5's 1024^3) forced on a small volume (variant bit 3): bit-exact."""
+    monkeypatch.setenv("VPTMCM_MARCH_VARIANT", "8")
+    gpu, cpu = make_pair(96, cf.fbm_volume(72, 21, nthreads=8), cf.tf_materials(True), ext=24.0)
+    run_and_compare(gpu, cpu, cf.golden_mvp("orbit"), cf.seed_stream(4, start=2), "wide gather")
+    gpu.close()
+
+
+def test_c5_1024_volume_streamed_rows_against_oracle():
+    """C5 on one GPU: the 1024^3 fBm volume (seed 1024) streamed into HBM in
+    64-slice blocks (WebGPUVolume.readModality's per-placement upload), CORNER8
+    cells > 4 GiB (the 64-bit gather template); R = 512, two fused passes; a
+    band of rows through the cube is bit-exact against the oracle's
+    row-restricted run, and the whole frame satisfies the running-mean bounds."""
+    n, R = 1024, 512
+    vol = cf.fbm_volume(n, 1024)
+    gpu = vptmcm.Renderer(R, device=0)
+    gpu.volume_blocks(vol.shape, (((0, 0, z), vol[z:z + 64]) for z in range(0, n, 64)))
+    cpu = orc.Oracle(R)
+    spec, tf = cf.spectrum_buffer("12"), cf.tf_spectral()
+    spd, ld = cf.light_default()
+    for r in (gpu, cpu):
+        r.set_spectrum(spec)
+    gpu.set_material_tf(tf)
+    gpu.set_light(spd, ld)
+    gpu.set_params(extinction=32.0, bounces=8, steps=8)
+    cpu.volume, cpu.tf, cpu.light, cpu.light_dir = vol, tf, spd, ld
+    cpu.params.update(extinction=32.0, bounces=8, steps=8)
+    mvp = cf.default_mvp_inverse()
+    seeds = cf.seed_stream(3, start=40)
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0], nthreads=16)
+    gpu.render_passes(mvp, seeds[1:])
+    rows = (224, 264)
+    for s in seeds[1:]:
+        rgb, want = cpu.render(mvp, s, nthreads=16, rows=rows)
+    y0, y1 = rows
+    got = gpu.read_photons().reshape(R, R, -1)
+    exp = cpu.photons.reshape(R, R, -1)
+    assert_photons_equal(got[y0:y1].reshape(-1, got.shape[-1]), exp[y0:y1].reshape(-1, exp.shape[-1]),
+                         "C5 rows")
+    assert_rgba_equal(gpu.read_rgba16f()[y0:y1], want[y0:y1], "C5 rows")
+    assert_rgb32_equal(gpu.read_rgb()[y0:y1], rgb[y0:y1], "C5 rows fp32")
+    allp = got.reshape(R * R, -1)
+    rad = allp[:, 10:22].view(np.float32)
+    assert (allp[:, 7] >= 1).all() and np.isfinite(rad).all()
+    assert rad.min() >= 0 and rad.max() <= 5 * 100 / 255 + 1e-6
     gpu.close()

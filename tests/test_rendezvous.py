@@ -33,3 +33,24 @@ def test_env_world_defaults(monkeypatch):
     monkeypatch.setenv("RANK", "3")
     monkeypatch.setenv("WORLD_SIZE", "4")
     assert rendezvous.env_world() == (3, 4, 3)
+
+
+def test_stale_payload_of_another_attempt_is_ignored(monkeypatch):
+    """A file left by a crashed attempt (another restart count) under the same
+    path is not taken: the payload must name the reader's own job key."""
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")
+    key = rendezvous.job_key()
+    path = rendezvous.uid_path(key)
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "0")
+    stale_key = rendezvous.job_key()
+    assert stale_key != key
+    path.write_bytes(rendezvous._payload(stale_key, bytes(128)))  # wrong key inside
+    try:
+        import pytest
+        with pytest.raises(TimeoutError):
+            rendezvous.exchange_unique_id(1, None, key=key, timeout_s=0.2)
+        # rank 0 of the new attempt replaces it; rank 1 then reads the new id
+        rendezvous.exchange_unique_id(0, lambda: bytes(range(128)), key=key)
+        assert rendezvous.exchange_unique_id(1, None, key=key, timeout_s=5) == bytes(range(128))
+    finally:
+        rendezvous.cleanup(key)

@@ -12,7 +12,7 @@ STEPS=${STEPS:-tests bench prof}
 for s in $STEPS; do
   case $s in
   tests)
-    timeout -k 10 ${TEST_T:-900} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
+    timeout -k 10 ${TEST_T:-900} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
     rc=$?; echo "pytest rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc ;;
   smoke)
     timeout -k 10 300 python __graft_entry__.py smoke > $OUT/smoke.log 2>&1
@@ -20,6 +20,9 @@ for s in $STEPS; do
   bench)
     timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err
     rc=$?; echo "bench rc=$rc" | tee -a $OUT/status.txt; cat $OUT/bench.json; fault $rc && exit $rc ;;
+  bench_drv)  # the driver's round-end command line
+    timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_drv.json 2> $OUT/bench_drv.err
+    rc=$?; echo "bench_drv rc=$rc" | tee -a $OUT/status.txt; cat $OUT/bench_drv.json; fault $rc && exit $rc ;;
   prof)
     (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 96 --warmup 16 --unfused-steps 0 --cpu-seconds 0 ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err")
     rc=$?; echo "prof rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc ;;

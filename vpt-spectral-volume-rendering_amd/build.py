@@ -57,24 +57,6 @@ def build_hip(force: bool = False) -> Path:
     return out
 
 
-def build_experiments() -> list[Path]:
-    """Cost-attribution builds, selected with VPTMCM_LIB=exp / exp_stamps:
-    libvptmcm_exp.so — knock-out switches (VPTMCM_MARCH_VARIANT bits 8+; they
-    change results) and per-wave records (VPTMCM_WAVE_DUMP=<file>);
-    libvptmcm_exp_stamps.so — additionally s_memtime segment stamps, which
-    serialise the waves and inflate kernel time (shares only)."""
-    srcs = [CSRC / "kernels.hip", CSRC / "vptmcm.cpp"]
-    hipcc = shutil.which("hipcc") or str(ROCM / "bin" / "hipcc")
-    outs = []
-    for name, defs in (("libvptmcm_exp.so", ["-DVPT_EXPERIMENTS"]),
-                       ("libvptmcm_exp_stamps.so", ["-DVPT_EXPERIMENTS", "-DVPT_STAMPS"])):
-        out = LIB / name
-        _run([hipcc, *HIP_FLAGS, *defs, "-shared", f"-I{REPO / 'include'}", *srcs, "-o", out,
-              "-lrccl", f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}"])
-        outs.append(out)
-    return outs
-
-
 def build_napi(force: bool = False) -> Path | None:
     out = LIB / "vptmcm_napi.node"
     src = PKG / "napi" / "vptmcm_napi.c"

@@ -56,7 +56,7 @@ hipError_t launch_reset(const MarchParams& P, float* ph, hipStream_t s);
 hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P, const PassSeeds& PS,
                         const TileSched& T, float* ph,
                         const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
-                        const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba,
+                        const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba, float* rgb32,
                         hipStream_t s, hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr);
 // Artistic tone mapper uniforms, derived on the host from (low, mid, high,
 // saturation, gamma) (WebGPUArtisticToneMapper.js:81-88, ArtisticToneMapper.wgsl:40-46).
@@ -68,16 +68,12 @@ hipError_t launch_tonemap_artistic(const uint16_t* rgba16, uint32_t n, const Ton
 // RGB sibling renderer (MCMComputeRenderer.wgsl): reset / march kernels.
 hipError_t launch_reset_rgb(const MarchParams& P, float* ph, hipStream_t s);
 hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSeeds& PS, float* ph,
-                            const uint8_t* vol, const float4* tf, uint16_t* rgba, hipStream_t s,
-                            hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr);
+                            const uint8_t* vol, const float4* tf, uint16_t* rgba, float* rgb32,
+                            hipStream_t s, hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr);
 hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, void* out,
                           hipStream_t s);
-hipError_t launch_pack(const MarchParams& P, const float* ph, const uint16_t* rgba, float4* out,
+hipError_t launch_pack(const MarchParams& P, const float* ph, const float* rgb32, float4* out,
                        hipStream_t s);
-// experiment build only: read and clear the per-segment stamp sums (8 counters)
-hipError_t read_stamps(unsigned long long* out8);
-// experiment build only: per-wave records of the last march launch (32 B each)
-hipError_t read_wave_records(void* out, size_t bytes);
 // fn 13 checks bin_of's arithmetic path against the count on the spectrum in P
 hipError_t launch_verify(int fn, const MarchParams& P, uint32_t lo, uint32_t n,
                          unsigned long long* bad, uint32_t* first, uint32_t nfirst, hipStream_t s);

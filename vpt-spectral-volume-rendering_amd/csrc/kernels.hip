@@ -172,83 +172,6 @@ __device__ __forceinline__ float sample_volume(const MarchParams& P, const uint8
 __device__ __forceinline__ float byte_f(uint32_t v, int sh) { return (float)((v >> sh) & 0xffu); }
 
 // ------------------------------------------------------------- march kernel
-// Cost attribution, compiled only into the experiment library
-// (-DVPT_EXPERIMENTS): knock-out switches (they change results) and
-// s_memtime stamps that accumulate per-segment wave cycles (they do not).
-#ifdef VPT_EXPERIMENTS
-__constant__ uint32_t g_ko;
-__device__ unsigned long long g_stamp[16];
-#define KO(bit) ((g_ko >> (bit)) & 1u)
-__device__ __forceinline__ unsigned long long stamp_now() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-// per-wave record of the last launch: HW_ID, XCC_ID, realtime start/end
-// (100 MHz), shader-clock duration, tile, entered flag
-struct WaveRec {
-  uint32_t hwid, xcc, rt0, rt1, cycles, tile, entered, block_wave;
-};
-__device__ WaveRec g_wrec[1 << 16];
-__device__ __forceinline__ unsigned long long realtime_now() {
-  unsigned long long t;
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
-}
-__device__ __forceinline__ void wave_record(uint32_t tile, bool entered, unsigned long long rt0,
-                                            unsigned long long c0) {
-  unsigned long long rt1 = realtime_now(), c1 = stamp_now();
-  uint32_t hwid, xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  uint32_t w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63u) == 0u) {
-    WaveRec r{hwid, xcc, (uint32_t)rt0, (uint32_t)rt1, (uint32_t)(c1 - c0), tile, entered ? 1u : 0u,
-              blockIdx.x * 16u + w};
-    g_wrec[(blockIdx.x * 16u + w) & 0xffffu] = r;
-  }
-}
-#define WAVE_T0 unsigned long long _rt0 = realtime_now(), _c0 = stamp_now();
-#define WAVE_RECORD(tile, entered) wave_record(tile, entered, _rt0, _c0)
-#ifdef VPT_STAMPS
-#define STAMP_DECL unsigned long long _tp = stamp_now(), _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define STAMP(k)                          \
-  do {                                    \
-    unsigned long long _tn = stamp_now(); \
-    _acc[k] += _tn - _tp;                 \
-    _tp = _tn;                            \
-  } while (0)
-#define STAMP_FLUSH()                                                        \
-  do {                                                                       \
-    if ((threadIdx.x & 63u) == 0u)                                           \
-      for (int _k = 0; _k < 8; _k++) atomicAdd(&g_stamp[_k], _acc[_k]);     \
-  } while (0)
-#else
-#define STAMP_DECL
-#define STAMP(k) \
-  do {           \
-  } while (0)
-#define STAMP_FLUSH() \
-  do {                \
-  } while (0)
-#endif
-#else
-#define KO(bit) 0u
-#define WAVE_T0
-#define WAVE_RECORD(tile, entered) \
-  do {                             \
-  } while (0)
-#define STAMP_DECL
-#define STAMP(k) \
-  do {           \
-  } while (0)
-#define STAMP_FLUSH() \
-  do {                \
-  } while (0)
-#endif
-
 // sample_light (wgsl:62-73) for a leaving photon; light_dir is pre-normalised
 // DIRL: the launch's light has a direction (FAST launches), no uniform test.
 template <bool DIRL = false>
@@ -408,7 +331,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
                                                        const uint32_t* __restrict__ tf_b4,
                                                        const uint8_t* __restrict__ tf_brow,
                                                        const uint8_t* __restrict__ light,
-                                                       uint16_t* __restrict__ rgba) {
+                                                       uint16_t* __restrict__ rgba,
+                                                       float* __restrict__ rgb32) {
   constexpr bool NBF = MODE >= 1u;
   constexpr bool FAST = MODE == 2u;
   // (albedo, alpha) of the whole TF in LDS: every step's 4 TF taps become
@@ -423,8 +347,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __shared__ uint32_t s_red[17];
   __shared__ uint32_t s_tile[16];
 
-  WAVE_T0
-  STAMP_DECL
   uint32_t tile;
   if (P.sched == 0u) {
     tile = __builtin_amdgcn_readfirstlane(schedule_tile(P, T.flags_in, s_red, s_tile));
@@ -440,21 +362,12 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   const size_t S = P.npad;
   bool entered = false;  // wave-uniform: some lane of this wave was inside the volume
   Photon p;
-#ifndef VPT_KO_STATE  // cost-attribution variant only (results invalid)
   if (live) load_photon(ph, S, i, p);  // issue the state loads before the LDS fill
-#else
-  p = Photon{};
-  p.pos = f3{0.5f, 0.5f, 0.5f};
-  p.dir = f3{0.0f, 0.0f, 1.0f};
-  p.lambda = 550.0f;
-#endif
 
   const uint4* src = reinterpret_cast<const uint4*>(tf_rg);
-#ifndef VPT_KO_TFFILL  // cost-attribution variant only (results invalid)
 #pragma unroll
   for (uint32_t k = 0; k < 256 * 256 * 2 / 16 / kMarchBlock; k++)
     s_tf4[threadIdx.x + k * kMarchBlock] = src[threadIdx.x + k * kMarchBlock];
-#endif
   if (threadIdx.x < 256u) {
     s_light[threadIdx.x] = (float)light[threadIdx.x];
     s_brow[threadIdx.x] = (float)tf_brow[threadIdx.x];
@@ -462,7 +375,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __syncthreads();
   if (!live) return;
   const uint16_t* s_tf = reinterpret_cast<const uint16_t*>(s_tf4);
-  STAMP(0);  // prologue: state loads issued, TF/light staged in LDS
 
   float sx, sy;
   screen_of(P, x, y, sx, sy);
@@ -642,19 +554,11 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         terminate(exit_radiance<FAST>(P, p.dir, wc), rc);
         wc = wave_const(rc.lambda, s_light);
         st = h5;
-        STAMP(1);
         continue;
       }
 
       entered = true;
-      VolTap vt{0.0f, 0.0f, 0.0f, 0u, 0u};
-      if (KO(1)) {
-        vt.fx = vt.fy = vt.fz = 0.5f;
-        vt.lo = vt.hi = 0x80808080u;
-      } else {
-        vt = vol_fetch<L>(P, vol, p.pos);  // gather in flight from here
-      }
-      STAMP(1);  // step head: draws, log, advance, gather issue (first step: + state-load wait)
+      const VolTap vt = vol_fetch<L>(P, vol, p.pos);  // gather in flight from here
       apply_pending();
 #if VPT_PIN_PEND
       // keep the update here, in the gather's shadow (the backend otherwise
@@ -673,31 +577,14 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       disk_of(h1, h2, dx, dy);
       Photon rc;
       WaveConst wcr = wc;
-      if (KO(3)) {
-        rc.pos = from;
-        rc.dir = f3{dx, dy, 1.0f};
-        rc.lambda = p.lambda;
-        rc.bin = p.bin;
-      } else if (KO(5) | KO(6) | KO(7) | KO(8)) {  // finer knock-outs of the candidate's parts
-        f3 d0 = KO(6) ? f3{dx, dy, 1.0f} : ray_dir_from_draws(P, sx, sy, from, h3, h4);
-        rc.dir = d0;
-        rc.pos = KO(5) ? from : ray_start(from, d0);
-        rc.lambda = lambda_of(P, h5);
-        rc.bin = KO(8) ? p.bin : bin_of<FAST>(P, rc.lambda);
-        if (!KO(7)) wcr = wave_const(rc.lambda, s_light);
-      } else {
-        reset_from_draws<FAST>(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
-        wcr = wave_const(rc.lambda, s_light);
-      }
-      STAMP(2);  // speculative reset candidate
+      reset_from_draws<FAST>(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
+      wcr = wave_const(rc.lambda, s_light);
       float nrm = fmaf(dy, dy, dx * dx);  // sphere.wgsl
       float srad = 2.0f * sqrt_z(1.0f - nrm);
       f3 u{srad * dx, srad * dy, 1.0f - 2.0f * nrm};
       float u3 = (float)h3 * 2.3283064365386963e-10f;
       float ud = dot3(u, p.dir);
-      f3 circle = KO(4) ? u : norm3(f3{fmaf(-ud, p.dir.x, u.x), fmaf(-ud, p.dir.y, u.y),
-                                       fmaf(-ud, p.dir.z, u.z)});
-      STAMP(3);  // speculative scatter half
+      f3 circle = norm3(f3{fmaf(-ud, p.dir.x, u.x), fmaf(-ud, p.dir.y, u.y), fmaf(-ud, p.dir.z, u.z)});
 
       // sample_volume_color (wgsl:75-80) -> probabilities (wgsl:132-139)
       float d = vol_filter(vt);  // in [0, 1]: a lerp of bytes times RN(1/255)
@@ -707,15 +594,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       if (!(FAST || P.b_rows)) b4 = tf_b4[(uint32_t)clampi(ir + 1, 256) * kTfCells + (uint32_t)wc.cc];
       const uint32_t ri0 = (uint32_t)clampi(ir, 255), ri1 = (uint32_t)clampi(ir + 1, 255);
       uint32_t r0 = ri0 * 256u, r1 = ri1 * 256u;
-      uint32_t t00, t10, t01, t11;
-      if (KO(2)) {
-        t00 = t10 = t01 = t11 = 0x8080u + r0;
-      } else {
-        t00 = s_tf[r0 + wc.c0];
-        t10 = s_tf[r0 + wc.c1];
-        t01 = s_tf[r1 + wc.c0];
-        t11 = s_tf[r1 + wc.c1];
-      }
+      const uint32_t t00 = s_tf[r0 + wc.c0], t10 = s_tf[r0 + wc.c1];
+      const uint32_t t01 = s_tf[r1 + wc.c0], t11 = s_tf[r1 + wc.c1];
       float albedo = lerp(lerp(byte_f(t00, 0), byte_f(t10, 0), wc.fc),
                           lerp(byte_f(t01, 0), byte_f(t11, 0), wc.fc), fr) * kInv255;
       float alpha = lerp(lerp(byte_f(t00, 8), byte_f(t10, 8), wc.fc),
@@ -723,7 +603,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       float pnull = 1.0f - alpha;
       float pscat = (p.bounces >= P.max_bounces) ? 0.0f : alpha * albedo;
       float pabs = (1.0f - pnull) - pscat;
-      STAMP(4);  // gather wait + trilinear filter + TF (LDS) + probabilities
 
       if (oob || wheel < pabs) {
         // exit (wgsl:142-150) or absorption (wgsl:151-155): adopt the candidate
@@ -752,7 +631,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       } else {
         st = sw;  // null collision
       }
-      STAMP(5);  // decision + adopt / HG finish
     }
     apply_pending();
   } else {
@@ -826,28 +704,23 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   uint2 px;
   px.x = (uint32_t)f2h(r) | ((uint32_t)f2h(g) << 16);
   px.y = (uint32_t)f2h(bl) | (0x3c00u << 16);
-#ifndef VPT_KO_IMG  // cost-attribution variant only (results invalid)
   reinterpret_cast<uint2*>(rgba)[(size_t)y * P.R + x] = px;
-#else
-  if (px.x == 0x12345u) rgba[0] = 1;
-#endif
+  if (pass + 1u == n_passes) {  // the launch's last image, fp32 before the f16 store (read_rgb, k_pack)
+    float* o = rgb32 + ((size_t)y * P.R + x) * 3u;
+    o[0] = r;
+    o[1] = g;
+    o[2] = bl;
+  }
   }  // pass
 
 #if VPT_ROBUST
   if (stale) p.pos = ray_start(from, p.dir);  // the last robust reset's start point
 #endif
-#ifndef VPT_KO_STATE
   store_state(ph, S, i, p);  // uPhotons[globalIndex] = p (wgsl:165), once per launch
 #pragma unroll
   for (int b = 0; b < kMaxBins; b++) ph[(kRad0 + b) * S + i] = p.rad[b];
-#else
-  if (p.rad[0] == 12345.0f) ph[i] = p.rad[1] + p.rad[5] + p.rad[11] + p.pos.x + p.dir.y;
-#endif
 
   if (lane == 0u) T.flags_out[tile] = entered ? 1u : 0u;  // the next pass's schedule
-  WAVE_RECORD(tile, entered);
-  STAMP(6);  // epilogue: state + image stores issued
-  STAMP_FLUSH();
 }
 
 
@@ -894,7 +767,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
                                                            float* __restrict__ ph,
                                                            const uint8_t* __restrict__ vol,
                                                            const float4* __restrict__ tf,
-                                                           uint16_t* __restrict__ rgba) {
+                                                           uint16_t* __restrict__ rgba,
+                                                           float* __restrict__ rgb32) {
   __shared__ float4 s_tf[kRgbTfMax];
   const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x) * (kMarchBlock / 64) +
                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1005,6 +879,12 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
     px.x = (uint32_t)f2h(rad.x) | ((uint32_t)f2h(rad.y) << 16);
     px.y = (uint32_t)f2h(rad.z) | (0x3c00u << 16);
     reinterpret_cast<uint2*>(rgba)[(size_t)y * P.R + x] = px;
+    if (pass + 1u == PS.n) {
+      float* o = rgb32 + ((size_t)y * P.R + x) * 3u;
+      o[0] = rad.x;
+      o[1] = rad.y;
+      o[2] = rad.z;
+    }
   }
   const float w[kRgbPlanes] = {pos.x, pos.y, pos.z, dir.x, dir.y, dir.z, as_f(bounces), as_f(samples),
                                tr.x, tr.y, tr.z, rad.x, rad.y, rad.z};
@@ -1040,20 +920,20 @@ __global__ __launch_bounds__(256) void k_corner8(const uint8_t* __restrict__ lin
 }
 
 // ----------------------------------------------------- multi-GPU composite
-// (rgb * n, n) per pixel from the rgba16f target and the photon sample count.
+// (rgb * n, n) per pixel from the fp32 image of the last pass (before its f16
+// rounding) and the photon sample count n: the running mean rgb weighted by
+// its sample count, so that sum(rgb*n) / sum(n) over the replicas is the mean
+// over every replica's samples.
 __global__ __launch_bounds__(256) void k_pack(const MarchParams P, const float* __restrict__ ph,
-                                              const uint16_t* __restrict__ rgba,
+                                              const float* __restrict__ rgb32,
                                               float4* __restrict__ out) {
   uint32_t x, y;
   size_t i;
   if (!tile_pixel(P, x, y, i)) return;
-  size_t pix = (size_t)y * P.R + x;
-  uint2 px = reinterpret_cast<const uint2*>(rgba)[pix];
-  float n = (float)as_u(ph[kSamples * (size_t)P.npad + i]);
-  float r = (float)__builtin_bit_cast(_Float16, (uint16_t)(px.x & 0xffffu));
-  float g = (float)__builtin_bit_cast(_Float16, (uint16_t)(px.x >> 16));
-  float b = (float)__builtin_bit_cast(_Float16, (uint16_t)(px.y & 0xffffu));
-  out[pix] = make_float4(r * n, g * n, b * n, n);
+  const size_t pix = (size_t)y * P.R + x;
+  const float n = (float)as_u(ph[kSamples * (size_t)P.npad + i]);
+  const float* c = rgb32 + pix * 3u;
+  out[pix] = make_float4(c[0] * n, c[1] * n, c[2] * n, n);
 }
 
 // ------------------------------------------------------------ tone mapping
@@ -1120,20 +1000,9 @@ hipError_t launch_reset(const MarchParams& P, float* ph, hipStream_t s) {
 
 hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P, const PassSeeds& PS,
                         const TileSched& T, float* ph, const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
-                        const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba,
+                        const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba, float* rgb32,
                         hipStream_t s, hipEvent_t ev_beg, hipEvent_t ev_end) {
   dim3 grid(tile_blocks(P, kMarchBlock));
-#ifdef VPT_EXPERIMENTS
-  {
-    static uint32_t last = 0xffffffffu;
-    uint32_t ko = variant >> 8;  // knock-out bits live above the tuning bits
-    if (ko != last) {
-      hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_ko), &ko, sizeof ko);
-      if (e != hipSuccess) return e;
-      last = ko;
-    }
-  }
-#endif
   const bool spec = (variant & 1u) == 0u;  // variant bit 0: plain (non-speculative) step
   const bool nbf = P.nb >= (uint32_t)kMaxBins;  // every radiance bin in use
   const bool fast = nbf && P.bins_uniform && P.b_rows && P.w_bounded && P.blur == 0.0f &&
@@ -1142,7 +1011,7 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   // (no extra barrier/marker packets between back-to-back launches)
 #define VPT_LAUNCH(LAY, SP, MO)                                                                \
   hipExtLaunchKernelGGL((k_march<LAY, SP, MO>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
-                        PS, P, T, ph, vol, tf_rg, tf_b4, tf_brow, light, rgba)
+                        PS, P, T, ph, vol, tf_rg, tf_b4, tf_brow, light, rgba, rgb32)
 #define VPT_LAUNCH_NB(LAY, SP)        \
   do {                                \
     if (SP && fast)                   \
@@ -1170,18 +1039,18 @@ hipError_t launch_reset_rgb(const MarchParams& P, float* ph, hipStream_t s) {
 }
 
 hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSeeds& PS, float* ph,
-                            const uint8_t* vol, const float4* tf, uint16_t* rgba, hipStream_t s,
-                            hipEvent_t ev_beg, hipEvent_t ev_end) {
+                            const uint8_t* vol, const float4* tf, uint16_t* rgba, float* rgb32,
+                            hipStream_t s, hipEvent_t ev_beg, hipEvent_t ev_end) {
   dim3 grid(tile_blocks(P, kMarchBlock));
   if (layout == kLayoutCorner8 && P.vol32)
     hipExtLaunchKernelGGL((k_march_rgb<kTplCorner8>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end,
-                          0, PS, P, ph, vol, tf, rgba);
+                          0, PS, P, ph, vol, tf, rgba, rgb32);
   else if (layout == kLayoutCorner8)
     hipExtLaunchKernelGGL((k_march_rgb<kTplCorner8Wide>), grid, dim3(kMarchBlock), 0, s, ev_beg,
-                          ev_end, 0, PS, P, ph, vol, tf, rgba);
+                          ev_end, 0, PS, P, ph, vol, tf, rgba, rgb32);
   else
     hipExtLaunchKernelGGL((k_march_rgb<kTplLinear>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end,
-                          0, PS, P, ph, vol, tf, rgba);
+                          0, PS, P, ph, vol, tf, rgba, rgb32);
   return hipGetLastError();
 }
 
@@ -1195,9 +1064,9 @@ hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D
   return hipGetLastError();
 }
 
-hipError_t launch_pack(const MarchParams& P, const float* ph, const uint16_t* rgba, float4* out,
+hipError_t launch_pack(const MarchParams& P, const float* ph, const float* rgb32, float4* out,
                        hipStream_t s) {
-  hipLaunchKernelGGL(k_pack, dim3(march_blocks(P)), dim3(kBlock), 0, s, P, ph, rgba, out);
+  hipLaunchKernelGGL(k_pack, dim3(march_blocks(P)), dim3(kBlock), 0, s, P, ph, rgb32, out);
   return hipGetLastError();
 }
 
@@ -1372,29 +1241,6 @@ __global__ void k_verify(int fn, const MarchParams P, uint32_t lo, uint32_t n,
       if (idx < nfirst) first[idx] = lo + k;
     }
   }
-}
-
-hipError_t read_wave_records(void* out, size_t bytes) {
-#ifdef VPT_EXPERIMENTS
-  if (bytes > sizeof(g_wrec)) bytes = sizeof(g_wrec);
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wrec), bytes);
-#else
-  (void)out;
-  (void)bytes;
-  return hipErrorNotSupported;
-#endif
-}
-
-hipError_t read_stamps(unsigned long long* out8) {
-#ifdef VPT_EXPERIMENTS
-  hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_stamp), 8 * sizeof(unsigned long long));
-  unsigned long long z[16] = {};
-  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof z);
-  return e;
-#else
-  for (int k = 0; k < 8; k++) out8[k] = 0;
-  return hipSuccess;
-#endif
 }
 
 hipError_t launch_verify(int fn, const MarchParams& P, uint32_t lo, uint32_t n,

@@ -41,6 +41,7 @@ struct vptmcm {
 
   float* photons = nullptr;    // kNumPlanes * npad words
   uint16_t* rgba = nullptr;    // R*R*4 halfs
+  float* rgb32 = nullptr;      // R*R*3 floats: the last launch's image before the f16 store
   uint32_t* ldr = nullptr;     // R*R rgba8 of the tone mapper (lazily allocated)
   uint8_t* vol_lin = nullptr;  // W*H*D (staging for CORNER8; the volume for LINEAR)
   void* vol_c8 = nullptr;      // (W+1)(H+1)(D+1) u64
@@ -287,6 +288,7 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
     const uint64_t w1 = h->W + 1ull, h1 = h->H + 1ull, d1 = h->D + 1ull;
     P.vol32 = (w1 * h1 * d1 * 8ull < (1ull << 32) && d1 * h1 < (1ull << 24) && w1 < (1ull << 24))
                   ? 1u : 0u;
+    if (h->variant & 8u) P.vol32 = 0u;  // variant bit 3: force the 64-bit gather (tests)
   }
   return P;
 }
@@ -331,10 +333,11 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf};
   P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : 0u;
   if (h->kind == VPTMCM_RENDERER_RGB)
-    HIPCHK(h, launch_march_rgb(h->layout, P, PS, h->photons, vol, h->tf_rgb, h->rgba, h->stream, eb, ee));
+    HIPCHK(h, launch_march_rgb(h->layout, P, PS, h->photons, vol, h->tf_rgb, h->rgba, h->rgb32,
+                               h->stream, eb, ee));
   else
     HIPCHK(h, launch_march(h->layout, h->variant, P, PS, T, h->photons, vol, h->tf_rg, h->tf_b4,
-                           h->tf_brow, h->light, h->rgba, h->stream, eb, ee));
+                           h->tf_brow, h->light, h->rgba, h->rgb32, h->stream, eb, ee));
   h->sched_cur = c ^ 1u;
   return VPTMCM_OK;
 }
@@ -435,6 +438,8 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   CK(hipMemsetAsync(h->photons, 0, (size_t)kNumPlanes * h->npad * sizeof(float), h->stream));
   CK(hipMalloc(&h->rgba, (size_t)h->R * h->R * 4 * sizeof(uint16_t)));
   CK(hipMemsetAsync(h->rgba, 0, (size_t)h->R * h->R * 4 * sizeof(uint16_t), h->stream));
+  CK(hipMalloc(&h->rgb32, (size_t)h->R * h->R * 3 * sizeof(float)));
+  CK(hipMemsetAsync(h->rgb32, 0, (size_t)h->R * h->R * 3 * sizeof(float), h->stream));
   CK(hipMalloc(&h->tf_rg, 65536 * sizeof(uint16_t)));
   CK(hipMemsetAsync(h->tf_rg, 0, 65536 * sizeof(uint16_t), h->stream));  // zero texture, js:85
   CK(hipMalloc(&h->tf_b4, kTfCells * kTfCells * sizeof(uint32_t)));
@@ -472,6 +477,7 @@ void vptmcm_destroy(vptmcm* h) {
   free_volume(h);
   if (h->photons) (void)hipFree(h->photons);
   if (h->rgba) (void)hipFree(h->rgba);
+  if (h->rgb32) (void)hipFree(h->rgb32);
   if (h->ldr) (void)hipFree(h->ldr);
   if (h->tf_rgb) (void)hipFree(h->tf_rgb);
   if (h->tf_rg) (void)hipFree(h->tf_rg);
@@ -499,7 +505,8 @@ int vptmcm_volume_begin(vptmcm* h, uint32_t width, uint32_t height, uint32_t dep
     h->vol_lin = nullptr;
     FAIL(h, VPTMCM_ENOMEM, "volume allocation of %zu bytes failed", n);
   }
-  HIPCHK(h, hipMemsetAsync(h->vol_lin, 0, n, h->stream));  // fresh texture is zero
+  // a fresh texture is zero; the block copies below run on the same stream, after it
+  HIPCHK(h, hipMemsetAsync(h->vol_lin, 0, n, h->stream));
   h->W = width;
   h->H = height;
   h->D = depth;
@@ -516,9 +523,12 @@ int vptmcm_volume_write_block(vptmcm* h, const uint8_t* data, uint32_t x, uint32
     FAIL(h, VPTMCM_EINVAL, "block [%u,%u,%u]+[%u,%u,%u] exceeds volume %ux%ux%u", x, y, z, bw, bh,
          bd, h->W, h->H, h->D);
   HIPCHK(h, hipSetDevice(h->device));
+  // Every copy is ordered behind volume_begin's zero-fill on the handle's
+  // stream and completes before returning (the caller keeps the block buffer).
   if (bw == h->W && bh == h->H && x == 0 && y == 0) {  // whole slices: one contiguous copy
-    HIPCHK(h, hipMemcpy(h->vol_lin + (size_t)z * h->W * h->H, data, (size_t)bw * bh * bd,
-                        hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpyAsync(h->vol_lin + (size_t)z * h->W * h->H, data, (size_t)bw * bh * bd,
+                             hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
     return VPTMCM_OK;
   }
   hipMemcpy3DParms p;
@@ -528,7 +538,8 @@ int vptmcm_volume_write_block(vptmcm* h, const uint8_t* data, uint32_t x, uint32
   p.dstPos = make_hipPos(x, y, z);
   p.extent = make_hipExtent(bw, bh, bd);
   p.kind = hipMemcpyHostToDevice;
-  HIPCHK(h, hipMemcpy3D(&p));
+  HIPCHK(h, hipMemcpy3DAsync(&p, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
   return VPTMCM_OK;
 }
 
@@ -732,6 +743,34 @@ int vptmcm_read_rgba16f(vptmcm* h, uint16_t* out) {
   return VPTMCM_OK;
 }
 
+int vptmcm_read_rgb(vptmcm* h, float* out) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
+  if (!out) FAIL(h, VPTMCM_EINVAL, "read_rgb: null output");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipMemcpyAsync(out, h->rgb32, (size_t)h->R * h->R * 3 * sizeof(float),
+                           hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return VPTMCM_OK;
+}
+
+int vptmcm_pack_radiance(vptmcm* h, float* out) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
+  if (!out) FAIL(h, VPTMCM_EINVAL, "pack_radiance: null output");
+  HIPCHK(h, hipSetDevice(h->device));
+  const size_t bytes = (size_t)h->R * h->R * sizeof(float4);
+  float4* d = nullptr;
+  HIPCHK(h, hipMalloc(&d, bytes));
+  MarchParams P = make_params(h, kNoMatrix, 0);
+  hipError_t e = launch_pack(P, h->photons, h->rgb32, d, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d, bytes, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) FAIL(h, VPTMCM_EHIP, "pack_radiance: %s", hipGetErrorString(e));
+  return VPTMCM_OK;
+}
+
 int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
@@ -863,27 +902,6 @@ int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
   if (h->timing && h->launches) HIPCHK(h, hipEventElapsedTime(&ms, h->region.beg, h->region.end));
   *total_ms = ms;
   *launches = h->timing ? h->launches : 0;
-#ifdef VPT_EXPERIMENTS
-  unsigned long long st[8];
-  if (read_stamps(st) == hipSuccess) {
-    unsigned long long tot = 0;
-    for (int k = 0; k < 8; k++) tot += st[k];
-    const char* names[8] = {"prologue", "head", "reset", "scatter", "sample+tf", "decide", "epilogue", "-"};
-    fprintf(stderr, "stamps:");
-    for (int k = 0; k < 7; k++) fprintf(stderr, " %s=%.1f%%", names[k], tot ? 100.0 * st[k] / tot : 0.0);
-    fprintf(stderr, " (wave-cycles/launch/wave %.0f)\n",
-            h->launches ? (double)tot / h->launches / (h->npad / 64) : 0.0);
-  }
-  if (const char* path = getenv("VPTMCM_WAVE_DUMP")) {
-    std::vector<uint8_t> buf((size_t)32 << 16);
-    if (read_wave_records(buf.data(), buf.size()) == hipSuccess) {
-      if (FILE* f = fopen(path, "wb")) {
-        fwrite(buf.data(), 1, buf.size(), f);
-        fclose(f);
-      }
-    }
-  }
-#endif
   return VPTMCM_OK;
 }
 
@@ -934,7 +952,7 @@ int vptmcm_comm_allreduce_radiance(vptmcm* h) {
   // the buffer must be free of the all-reduce issued two passes ago
   HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[k], 0));
   MarchParams P = make_params(h, kNoMatrix, 0);
-  HIPCHK(h, launch_pack(P, h->photons, h->rgba, h->comp[k], h->stream));
+  HIPCHK(h, launch_pack(P, h->photons, h->rgb32, h->comp[k], h->stream));
   HIPCHK(h, hipEventRecord(h->comp_ready[k], h->stream));
   HIPCHK(h, hipStreamWaitEvent(h->comm_stream, h->comp_ready[k], 0));
   NCCLCHK(h, ncclAllReduce(h->comp[k], h->comp[k], (size_t)h->R * h->R * 4, ncclFloat32, ncclSum,

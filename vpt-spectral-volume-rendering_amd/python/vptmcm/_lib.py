@@ -28,7 +28,7 @@ EXPORTS = [
     "vptmcm_volume_begin", "vptmcm_volume_write_block", "vptmcm_volume_end",
     "vptmcm_set_material_tf", "vptmcm_set_light", "vptmcm_set_spectrum", "vptmcm_set_params",
     "vptmcm_reset", "vptmcm_render", "vptmcm_render_passes", "vptmcm_synchronize",
-    "vptmcm_read_rgba16f", "vptmcm_read_photons", "vptmcm_write_photons",
+    "vptmcm_read_rgba16f", "vptmcm_read_rgb", "vptmcm_pack_radiance", "vptmcm_read_photons", "vptmcm_write_photons",
     "vptmcm_tonemap_artistic", "vptmcm_set_transfer_function", "vptmcm_set_environment",
     "vptmcm_enable_kernel_timing", "vptmcm_kernel_time", "vptmcm_comm_unique_id",
     "vptmcm_comm_init", "vptmcm_comm_allreduce_radiance", "vptmcm_comm_read_composite",
@@ -95,6 +95,8 @@ def load() -> C.CDLL:
         "vptmcm_render_passes": (C.c_int, [vp, f32p, u32p, C.c_uint32]),
         "vptmcm_synchronize": (C.c_int, [vp]),
         "vptmcm_read_rgba16f": (C.c_int, [vp, vp]),
+        "vptmcm_read_rgb": (C.c_int, [vp, vp]),
+        "vptmcm_pack_radiance": (C.c_int, [vp, vp]),
         "vptmcm_tonemap_artistic": (C.c_int, [vp, vp, vp]),
         "vptmcm_set_transfer_function": (C.c_int, [vp, vp, C.c_uint32, C.c_uint32]),
         "vptmcm_set_environment": (C.c_int, [vp, vp, C.c_uint32, C.c_uint32]),
@@ -236,6 +238,18 @@ class Renderer:
     def read_rgba16f(self) -> np.ndarray:
         out = np.empty((self.R, self.R, 4), np.uint16)
         self._ck(self.L.vptmcm_read_rgba16f(self.h, _ptr(out)))
+        return out
+
+    def read_rgb(self) -> np.ndarray:
+        """fp32 RGB of the last pass before the f16 store, [R, R, 3]."""
+        out = np.empty((self.R, self.R, 3), np.float32)
+        self._ck(self.L.vptmcm_read_rgb(self.h, _ptr(out)))
+        return out
+
+    def pack_radiance(self) -> np.ndarray:
+        """(rgb*n, n) per pixel, [R, R, 4] float32 (what the composite all-reduces)."""
+        out = np.empty((self.R, self.R, 4), np.float32)
+        self._ck(self.L.vptmcm_pack_radiance(self.h, _ptr(out)))
         return out
 
     def tonemap_artistic(self, low=0.0, mid=0.5, high=1.0, saturation=1.0, gamma=2.2) -> np.ndarray:

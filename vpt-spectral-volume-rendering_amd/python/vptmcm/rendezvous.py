@@ -24,8 +24,11 @@ def env_world() -> tuple[int, int, int]:
 
 
 def job_key() -> str:
+    """(agent pid, MASTER_PORT, run id, restart count): unique per elastic attempt,
+    so a restarted job never reads an id a crashed attempt left behind."""
     parts = [str(os.getppid()), os.environ.get("MASTER_PORT", "0"),
-             os.environ.get("TORCHELASTIC_RUN_ID", "none")]
+             os.environ.get("TORCHELASTIC_RUN_ID", "none"),
+             os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")]
     return "-".join(p.replace("/", "_") for p in parts)
 
 
@@ -33,23 +36,46 @@ def uid_path(key: str) -> Path:
     return Path(tempfile.gettempdir()) / f"vptmcm-uid-{key}.bin"
 
 
+_MAGIC = b"VPTMCMUID1"
+
+
+def _payload(key: str, uid: bytes) -> bytes:
+    k = key.encode()
+    return _MAGIC + len(k).to_bytes(2, "little") + k + uid
+
+
+def _parse(key: str, data: bytes) -> bytes | None:
+    """The uid if data is a complete payload published for exactly this key."""
+    k = key.encode()
+    head = _MAGIC + len(k).to_bytes(2, "little") + k
+    if data.startswith(head) and len(data) == len(head) + 128:
+        return data[len(head):]
+    return None
+
+
 def exchange_unique_id(rank: int, make_uid, key: str | None = None,
                        timeout_s: float = 180.0) -> bytes:
-    """Rank 0 calls make_uid() and publishes it; others wait for it."""
-    path = uid_path(key or job_key())
+    """Rank 0 calls make_uid() and publishes it; others wait for a payload that
+    names their own job key (a stale file of another attempt is ignored)."""
+    key = key or job_key()
+    path = uid_path(key)
     if rank == 0:
         uid = make_uid()
         assert len(uid) == 128
+        try:
+            path.unlink()  # whatever an earlier crashed attempt left
+        except FileNotFoundError:
+            pass
         tmp = path.with_name(path.name + f".{os.getpid()}.tmp")
-        tmp.write_bytes(uid)
+        tmp.write_bytes(_payload(key, uid))
         os.replace(tmp, path)
         return uid
     deadline = time.monotonic() + timeout_s
     while time.monotonic() < deadline:
         try:
-            data = path.read_bytes()
-            if len(data) == 128:
-                return data
+            uid = _parse(key, path.read_bytes())
+            if uid is not None:
+                return uid
         except FileNotFoundError:
             pass
         time.sleep(0.02)
