@@ -519,6 +519,10 @@ def test_c5_1024_volume_streamed_rows_against_oracle():
     assert_rgb32_equal(gpu.read_rgb()[y0:y1], rgb[y0:y1], "C5 rows fp32")
     allp = got.reshape(R * R, -1)
     rad = allp[:, 10:22].view(np.float32)
-    assert (allp[:, 7] >= 1).all() and np.isfinite(rad).all()
-    assert rad.min() >= 0 and rad.max() <= 5 * 100 / 255 + 1e-6
+    # a photon that scattered or null-collided through all 16 steps has no
+    # sample yet (samples 0, bins still the reset's 1.0)
+    smp = allp[:, 7]
+    assert (smp <= 16).all() and (smp >= 1).mean() > 0.9 and np.isfinite(rad).all()
+    assert rad.min() >= 0 and rad[smp >= 1].max() <= 5 * 100 / 255 + 1e-6
+    assert (rad[smp == 0] == 1.0).all()
     gpu.close()

@@ -1,0 +1,95 @@
+// gather_calib.hip — known-bytes calibration of the memory-side counters for
+// the march's access pattern (measurement aid, not product): scattered 8-B
+// loads (one u64 per lane, the CORNER8 cell gather) from a table of T bytes.
+//
+// Every lane issues N independent gathers at PCG-hashed cell indices, so the
+// gather count is known exactly (grid * N) and the bytes the program asks for
+// are 8 per gather. Run once plainly (rate: gathers/s and the implied bytes per
+// gather for 64-B and 128-B fills against the HBM peak) and under
+//   rocprofv3 --kernel-trace --pmc FETCH_SIZE
+// (FETCH_SIZE per gather = the counter's tally for one scattered 8-B load).
+//   hipcc -O3 --offload-arch=gfx950 tools/gather_calib.hip -o tools/gather_calib
+//   tools/gather_calib <table MiB> [gathers per lane] [blocks]
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+__device__ __forceinline__ uint32_t pcg(uint32_t v) {
+  uint32_t s = v * 747796405u + 2891336453u;
+  uint32_t w = ((s >> ((s >> 28u) + 4u)) ^ s) * 277803737u;
+  return (w >> 22u) ^ w;
+}
+
+// 8 gathers in flight per lane per round; `mask` = cells - 1 (power of two)
+__global__ __launch_bounds__(256) void k_gather(const uint2* __restrict__ tab, uint32_t mask,
+                                                uint32_t rounds, uint32_t* __restrict__ out) {
+  const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
+  uint32_t h = pcg(gid * 2654435761u + 12345u), acc = 0u;
+  for (uint32_t r = 0; r < rounds; r++) {
+    uint2 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      h = pcg(h);
+      v[k] = tab[h & mask];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc += v[k].x ^ v[k].y;
+  }
+  out[gid] = acc;
+}
+
+__global__ void k_fill(uint2* tab, size_t n) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (size_t)gridDim.x * blockDim.x) tab[i] = make_uint2((uint32_t)i, (uint32_t)(i >> 7));
+}
+
+int main(int argc, char** argv) {
+  const size_t mib = argc > 1 ? strtoull(argv[1], 0, 10) : 1024;
+  const uint32_t per_lane = argc > 2 ? (uint32_t)atoi(argv[2]) : 256;
+  const uint32_t blocks = argc > 3 ? (uint32_t)atoi(argv[3]) : 4096;
+  size_t cells = mib * 1024 * 1024 / 8;
+  if (cells & (cells - 1)) {
+    fprintf(stderr, "table size must be a power of two MiB\n");
+    return 2;
+  }
+  if (cells > (1ull << 32)) {
+    fprintf(stderr, "table too large for 32-bit cell indices\n");
+    return 2;
+  }
+  uint2* tab;
+  uint32_t* out;
+  CK(hipMalloc(&tab, cells * 8));
+  CK(hipMalloc(&out, (size_t)blocks * 256 * 4));
+  k_fill<<<4096, 256>>>(tab, cells);
+  CK(hipDeviceSynchronize());
+  const uint32_t rounds = per_lane / 8;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  k_gather<<<blocks, 256>>>(tab, (uint32_t)(cells - 1), rounds, out);  // warm-up
+  const int reps = 5;
+  CK(hipEventRecord(a));
+  for (int r = 0; r < reps; r++) k_gather<<<blocks, 256>>>(tab, (uint32_t)(cells - 1), rounds, out);
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms;
+  CK(hipEventElapsedTime(&ms, a, b));
+  const double g = (double)blocks * 256 * rounds * 8;  // gathers per launch
+  const double s = ms * 1e-3 / reps;
+  printf("{\"table_bytes\": %zu, \"gathers_per_launch\": %.0f, \"launch_us\": %.2f, "
+         "\"ggathers_per_s\": %.2f, \"tbps_if_64B\": %.2f, \"tbps_if_128B\": %.2f}\n",
+         cells * 8, g, s * 1e6, g / s * 1e-9, g * 64 / s * 1e-12, g * 128 / s * 1e-12);
+  CK(hipFree(tab));
+  CK(hipFree(out));
+  return 0;
+}

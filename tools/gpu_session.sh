@@ -26,6 +26,15 @@ for s in $STEPS; do
   prof)
     (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 96 --warmup 16 --unfused-steps 0 --cpu-seconds 0 ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err")
     rc=$?; echo "prof rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc ;;
+  calib)  # known-bytes scattered 8-B gather: rate, then FETCH_SIZE per gather
+    for mib in ${CALIB_MIB:-2048 1024 64}; do
+      timeout -k 10 120 tools/gather_calib $mib > $OUT/calib_$mib.json 2>&1
+      rc=$?; echo "calib $mib rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$GRAFT_REPO_ROOT/$OUT/calib_pmc_$mib" -o run --output-format csv -- "$GRAFT_REPO_ROOT/tools/gather_calib" $mib > /dev/null 2> "$GRAFT_REPO_ROOT/$OUT/calib_pmc_$mib.err")
+      rc=$?; echo "calib pmc $mib rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
+    done ;;
+  counters)
+    timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)
     for c in FETCH_SIZE WRITE_SIZE; do
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --pmc $c -d "$GRAFT_REPO_ROOT/$OUT/pmc_$c" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 32 --warmup 16 --unfused-steps 0 --cpu-seconds 0 ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/$OUT/pmc_$c.json" 2> "$GRAFT_REPO_ROOT/$OUT/pmc_$c.err")
