@@ -35,6 +35,8 @@ from vptmcm import rendezvous  # noqa: E402
 
 METRIC = "Mphoton-steps/sec (+ achieved HBM GB/s), 512³ spectral MCM, 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# 1024 SIMD-32 units x 2.4 GHz / 2 cycles per wave64 VALU instruction
+VALU_PEAK_G = 1024 * 2.4 / 2
 
 
 def parse():
@@ -50,7 +52,7 @@ def parse():
     ap.add_argument("--volume", type=int, default=512)
     ap.add_argument("--photon-steps", type=int, default=8, help="S: steps per pass")
     ap.add_argument("--extinction", type=float, default=32.0)
-    ap.add_argument("--layout", choices=["corner8", "linear"], default="corner8")
+    ap.add_argument("--layout", choices=["corner8", "brick8", "linear"], default="corner8")
     ap.add_argument("--tf", choices=["spectral", "grey", "zero"], default="spectral")
     ap.add_argument("--camera", choices=["default", "near", "orbit", "orbit_tilted"],
                     default="default", help="golden camera pose (non-default: analysis only)")
@@ -82,12 +84,29 @@ def parse():
 
 
 def cpu_baseline(vol, tf, spec, spd, ldir, mvp, R, S, ext, budget_s):
-    """The C oracle (the 'port') on this host's cores: full R^2 frames, S steps,
-    passes until the time budget is spent."""
+    """The north_star's CPU baseline: the scalar JavaScript re-execution of the
+    same march (oracle/mcm_march.js, bit-exact with the C oracle) under
+    worker_threads on this host's cores, full R^2 frames until the budget is
+    spent. The C oracle on the same threads is reported beside it ('c_port')."""
     sys.path.insert(0, str(REPO / "oracle"))
-    import oracle as orc  # test-infrastructure checker, timed here as the CPU baseline
+    import js_march  # test-infrastructure restatement, timed here as the CPU baseline
+    import oracle as orc  # test-infrastructure checker, timed as the secondary baseline
 
+    # the GPU box's per-GPU CPU share is 16 cores (OMP_NUM_THREADS there); the
+    # machine reports many more, which belong to the other GPUs' jobs
     threads = cf.host_threads()
+    share = f"{threads} of {os.cpu_count()} host CPUs (the per-GPU CPU share)"
+    out = None
+    if js_march.node():
+        j = js_march.run_bench(R, vol, tf, spd, ldir, spec, mvp, cf.seed_stream(64, start=0),
+                               threads, budget_s, extinction=ext, bounces=8, steps=S)
+        out = {"value": round(j["photon_steps_per_s"] / 1e6, 3), "unit": "Mphoton-steps/s",
+               "cores": threads, "kind": "port", "host_cpus": os.cpu_count(),
+               "sample": f"JavaScript re-execution (oracle/mcm_march.js, Math.fround, node "
+                         f"{j['node']} worker_threads x{j['threads']}), {j['passes']} full passes "
+                         f"of the same {R}x{R}x{S} workload after 1 warm-up pass, "
+                         f"{j['seconds']:.1f} s, {share}"}
+
     o = orc.Oracle(R)
     o.set_spectrum(spec)
     o.volume, o.tf, o.light, o.light_dir = vol, tf, spd, ldir
@@ -101,10 +120,15 @@ def cpu_baseline(vol, tf, spec, spd, ldir, mvp, R, S, ext, budget_s):
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
-    return {"value": round(R * R * S * passes / el / 1e6, 3), "unit": "Mphoton-steps/s",
-            "cores": threads, "kind": "port", "host_cpus": os.cpu_count(),
-            "sample": f"C oracle (oracle/mcm_oracle.c), {passes} full passes of the same "
-                      f"{R}x{R}x{S} workload after 1 warm-up pass, {el:.1f} s, {threads} pthreads"}
+    c_port = {"value": round(R * R * S * passes / el / 1e6, 3), "unit": "Mphoton-steps/s",
+              "cores": threads, "kind": "port",
+              "sample": f"C oracle (oracle/mcm_oracle.c), {passes} full passes after 1 warm-up "
+                        f"pass, {el:.1f} s, {threads} pthreads"}
+    if out is None:  # no node on this host: the C port is the baseline
+        out = dict(c_port, host_cpus=os.cpu_count())
+    else:
+        out["c_port"] = c_port
+    return out
 
 
 def main():
@@ -115,7 +139,8 @@ def main():
             raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
         world = 1
     R, S = a.resolution, a.photon_steps
-    layout = vptmcm.LAYOUT_CORNER8 if a.layout == "corner8" else vptmcm.LAYOUT_LINEAR
+    layout = {"corner8": vptmcm.LAYOUT_CORNER8, "brick8": vptmcm.LAYOUT_BRICK8,
+              "linear": vptmcm.LAYOUT_LINEAR}[a.layout]
 
     # ---- inputs (synthetic)
     t = time.perf_counter()
@@ -258,7 +283,7 @@ def main():
     ppl = shapes[0] if len(shapes) == 1 else shapes
     # PMC-derived memory-side bytes per launch (profiles/): attached only when a
     # profile of this exact launch shape (R, S, layout, volume, passes) exists.
-    traffic, traffic_src = None, None
+    traffic, traffic_src, issue = None, None, None
     tp = Path(a.traffic_json)
     if tp.exists() and len(shapes) == 1:
         try:
@@ -266,11 +291,24 @@ def main():
             for e in t.get("entries", [t]):
                 if (e.get("resolution") == R and e.get("steps") == S and e.get("layout") == a.layout
                         and e.get("volume", 512) == a.volume
-                        and e.get("passes_per_launch", 1) == shapes[0]):
+                        and e.get("passes_per_launch", 1) == shapes[0]
+                        and a.tf == "spectral" and a.camera == "default"):
                     traffic = e.get("hbm_bytes_per_launch")
                     traffic_src = f"{tp.relative_to(REPO) if tp.is_relative_to(REPO) else tp}"
-        except (ValueError, OSError):
-            traffic = None
+                    # VALU issue roofline: the launch's VALU wave-instructions
+                    # (PMC, same launch shape) over its live duration, against
+                    # 1024 SIMD-32s issuing one wave64 VALU instruction per 2
+                    # cycles at the 2.4 GHz peak clock
+                    iv = e.get("issue")
+                    if iv and not a.no_timing:
+                        ach = iv["valu_insts"] / (kern_avg_ms * 1e-3) / 1e9
+                        issue = {"bound": "valu-issue", "achieved": round(ach, 1),
+                                 "peak": VALU_PEAK_G, "unit": "G wave-instructions/s",
+                                 "frac": round(ach / VALU_PEAK_G, 4),
+                                 "valu_per_photon_step": iv["valu_per_photon_step"],
+                                 "source": traffic_src}
+        except (ValueError, OSError, KeyError):
+            traffic, issue = None, None
 
     # The general (non-FAST) march on the same volume: MODE 0 specialisation
     # (8 uneven bins, wavelength-varying anisotropy from the 4-corner table)
@@ -316,6 +354,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic_ratio": (round(traffic / bytes_per_launch, 2) if traffic else None),
+                         "issue": issue,
                          "kernel": "k_march", "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                          "passes_per_launch": ppl,
                          "kernel_us_per_pass": round(kern_ms_max * 1e3 / a.steps, 3),

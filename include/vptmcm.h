@@ -57,6 +57,7 @@ extern "C" {
 /* Volume layouts in HBM (see DESIGN.md "Data layout"). */
 #define VPTMCM_LAYOUT_LINEAR 0   /* x-fastest u8, as writeTexture lays it out */
 #define VPTMCM_LAYOUT_CORNER8 1  /* one u64 of the 8 trilinear corners per cell */
+#define VPTMCM_LAYOUT_BRICK8 2   /* CORNER8 cells in 4x4x4-cell bricks (512 B), Z-ordered inside */
 
 typedef struct vptmcm vptmcm;
 

@@ -15,7 +15,7 @@ from vptmcm import configs as cf
 
 pytestmark = pytest.mark.gpu
 
-LAYOUTS = [vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_LINEAR]
+LAYOUTS = [vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_LINEAR, vptmcm.LAYOUT_BRICK8]
 
 
 def same_words(a: np.ndarray, b: np.ndarray) -> np.ndarray:
@@ -473,12 +473,26 @@ def test_c4_two_replica_composite_bitexact():
     assert np.isfinite(comp).all() and (n > 0).mean() > 0.99
 
 
-def test_wide_gather_template_bitexact(monkeypatch):
-    """The 64-bit-offset CORNER8 gather (selected for cell arrays >= 4 GiB, e.g.
-    C5's 1024^3) forced on a small volume (variant bit 3): bit-exact."""
+@pytest.mark.parametrize("layout", [vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_BRICK8])
+def test_wide_gather_template_bitexact(layout, monkeypatch):
+    """The 64-bit-offset CORNER8 / BRICK8 gathers (selected for cell arrays >= 4
+    GiB, e.g. C5's 1024^3) forced on a small volume (variant bit 3): bit-exact."""
     monkeypatch.setenv("VPTMCM_MARCH_VARIANT", "8")
-    gpu, cpu = make_pair(96, cf.fbm_volume(72, 21, nthreads=8), cf.tf_materials(True), ext=24.0)
+    gpu, cpu = make_pair(96, cf.fbm_volume(72, 21, nthreads=8), cf.tf_materials(True), ext=24.0,
+                         layout=layout)
     run_and_compare(gpu, cpu, cf.golden_mvp("orbit"), cf.seed_stream(4, start=2), "wide gather")
+    gpu.close()
+
+
+@pytest.mark.parametrize("shape", [(37, 50, 23), (5, 4, 130), (1, 1, 1)])
+def test_brick8_ragged_volume_bitexact(shape):
+    """BRICK8 on volumes whose cell grid (W+1, H+1, D+1) is not a whole number of
+    4x4x4 bricks (padding bricks, a 1-voxel volume): bit-exact against the oracle."""
+    rng = np.random.default_rng(sum(shape))
+    vol = rng.integers(0, 256, size=shape[::-1], dtype=np.uint8)
+    gpu, cpu = make_pair(64, vol, cf.tf_materials(True), ext=20.0, layout=vptmcm.LAYOUT_BRICK8)
+    run_and_compare(gpu, cpu, cf.golden_mvp("orbit_tilted"), cf.seed_stream(3, start=9),
+                    f"brick8 {shape}")
     gpu.close()
 
 

@@ -122,7 +122,20 @@ __device__ __forceinline__ VolTap vol_fetch(const MarchParams& P, const uint8_t*
   int ix = axis_floor_q(q.x, (float)P.W, &t.fx);
   int iy = axis_floor_q(q.y, (float)P.H, &t.fy);
   int iz = axis_floor_q(q.z, (float)P.D, &t.fz);
-  if constexpr (L == kTplCorner8 || L == kTplCorner8Wide) {
+  if constexpr (L == kTplBrick8 || L == kTplBrick8Wide) {
+    const uint32_t cx = (uint32_t)(clampi(ix + 1, (int)P.W));
+    const uint32_t cy = (uint32_t)(clampi(iy + 1, (int)P.H));
+    const uint32_t cz = (uint32_t)(clampi(iz + 1, (int)P.D));
+    const uint32_t brick = __umul24(mad_u24(cz >> 2, P.BH, cy >> 2), P.BW) + (cx >> 2);
+    const uint32_t inner = brick_inner(cx, cy, cz) << 3;
+    uint2 c;
+    if constexpr (L == kTplBrick8)
+      c = *reinterpret_cast<const uint2*>(vol + ((brick << 9) | inner));
+    else
+      c = *reinterpret_cast<const uint2*>(vol + (((size_t)brick << 9) | inner));
+    t.lo = c.x;
+    t.hi = c.y;
+  } else if constexpr (L == kTplCorner8 || L == kTplCorner8Wide) {
     const uint32_t W1 = P.W + 1u, H1 = P.H + 1u;
     uint32_t cx = (uint32_t)(clampi(ix + 1, (int)P.W));
     uint32_t cy = (uint32_t)(clampi(iy + 1, (int)P.H));
@@ -421,7 +434,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     // add_radiance of a termination is deferred into the next step's gather
     // shadow (it only touches the radiance bins, applied in the same order).
     float pend_n = 0.0f, pend_l = 0.0f;
-    uint32_t pend_bin = 0u;
 #if VPT_OH_PEND
     // The pending bin as a byte one-hot: byte (bin & 3) of word bin >> 2 is 1,
     // so each bin's 0/1 factor is one v_cvt_f32_ubyteN (no per-bin compare
@@ -436,6 +448,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       pend_oh[2] = wi == 2u ? one : 0u;
     };
 #else
+    uint32_t pend_bin = 0u;
     auto set_pending = [&](float n, float l, uint32_t bin) {
       pend_n = n;
       pend_l = l;
@@ -895,8 +908,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
 // --------------------------------------------------------- volume relayout
 // cell (cx,cy,cz) in [0,W]x[0,H]x[0,D] holds voxels clamp(c-1), clamp(c) per axis;
 // byte (dz*4 + dy*2 + dx) of the u64 = voxel (x0+dx, y0+dy, z0+dz).
+// BW == 0: raster cell order (CORNER8); else 4x4x4-cell bricks (BRICK8), BW x BH bricks per slab
 __global__ __launch_bounds__(256) void k_corner8(const uint8_t* __restrict__ lin, uint32_t W,
-                                                 uint32_t H, uint32_t D, uint2* __restrict__ out) {
+                                                 uint32_t H, uint32_t D, uint32_t BW, uint32_t BH,
+                                                 uint2* __restrict__ out) {
   const uint32_t W1 = W + 1u, H1 = H + 1u;
   const size_t ncell = (size_t)W1 * H1 * (D + 1u);
   for (size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncell;
@@ -915,7 +930,12 @@ __global__ __launch_bounds__(256) void k_corner8(const uint8_t* __restrict__ lin
           ((uint32_t)lin[r10 + x0] << 16) | ((uint32_t)lin[r10 + x1] << 24);
     v.y = (uint32_t)lin[r01 + x0] | ((uint32_t)lin[r01 + x1] << 8) |
           ((uint32_t)lin[r11 + x0] << 16) | ((uint32_t)lin[r11 + x1] << 24);
-    out[c] = v;
+    if (BW == 0u) {
+      out[c] = v;
+    } else {
+      const size_t brick = ((size_t)(cz >> 2) * BH + (cy >> 2)) * BW + (cx >> 2);
+      out[(brick << 6) | brick_inner(cx, cy, cz)] = v;
+    }
   }
 }
 
@@ -1021,7 +1041,11 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
     else                              \
       VPT_LAUNCH(LAY, SP, 0u);        \
   } while (0)
-  if (layout == kLayoutCorner8 && P.vol32) {
+  if (layout == kLayoutBrick8 && P.vol32) {
+    if (spec) VPT_LAUNCH_NB(kTplBrick8, true); else VPT_LAUNCH_NB(kTplBrick8, false);
+  } else if (layout == kLayoutBrick8) {
+    if (spec) VPT_LAUNCH_NB(kTplBrick8Wide, true); else VPT_LAUNCH_NB(kTplBrick8Wide, false);
+  } else if (layout == kLayoutCorner8 && P.vol32) {
     if (spec) VPT_LAUNCH_NB(kTplCorner8, true); else VPT_LAUNCH_NB(kTplCorner8, false);
   } else if (layout == kLayoutCorner8) {
     if (spec) VPT_LAUNCH_NB(kTplCorner8Wide, true); else VPT_LAUNCH_NB(kTplCorner8Wide, false);
@@ -1042,7 +1066,13 @@ hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSee
                             const uint8_t* vol, const float4* tf, uint16_t* rgba, float* rgb32,
                             hipStream_t s, hipEvent_t ev_beg, hipEvent_t ev_end) {
   dim3 grid(tile_blocks(P, kMarchBlock));
-  if (layout == kLayoutCorner8 && P.vol32)
+  if (layout == kLayoutBrick8 && P.vol32)
+    hipExtLaunchKernelGGL((k_march_rgb<kTplBrick8>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end,
+                          0, PS, P, ph, vol, tf, rgba, rgb32);
+  else if (layout == kLayoutBrick8)
+    hipExtLaunchKernelGGL((k_march_rgb<kTplBrick8Wide>), grid, dim3(kMarchBlock), 0, s, ev_beg,
+                          ev_end, 0, PS, P, ph, vol, tf, rgba, rgb32);
+  else if (layout == kLayoutCorner8 && P.vol32)
     hipExtLaunchKernelGGL((k_march_rgb<kTplCorner8>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end,
                           0, PS, P, ph, vol, tf, rgba, rgb32);
   else if (layout == kLayoutCorner8)
@@ -1054,12 +1084,12 @@ hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSee
   return hipGetLastError();
 }
 
-hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, void* out,
-                          hipStream_t s) {
+hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, uint32_t BW,
+                          uint32_t BH, void* out, hipStream_t s) {
   size_t ncell = (size_t)(W + 1) * (H + 1) * (D + 1);
   size_t blocks = (ncell + 255) / 256;
   if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(k_corner8, dim3((uint32_t)blocks), dim3(256), 0, s, lin, W, H, D,
+  hipLaunchKernelGGL(k_corner8, dim3((uint32_t)blocks), dim3(256), 0, s, lin, W, H, D, BW, BH,
                      reinterpret_cast<uint2*>(out));
   return hipGetLastError();
 }

@@ -26,10 +26,20 @@
 
 namespace vpt {
 
-enum : uint32_t { kLayoutLinear = 0, kLayoutCorner8 = 1 };
-// Kernel template layouts: CORNER8 with 32-bit cell offsets (MarchParams::vol32)
-// or with 64-bit ones (volumes whose cell array exceeds 4 GiB, e.g. 1024^3).
-enum : uint32_t { kTplLinear = 0, kTplCorner8 = 1, kTplCorner8Wide = 2 };
+enum : uint32_t { kLayoutLinear = 0, kLayoutCorner8 = 1, kLayoutBrick8 = 2 };
+// Kernel template layouts: CORNER8 / BRICK8 with 32-bit byte offsets
+// (MarchParams::vol32) or with 64-bit ones (cell arrays over 4 GiB, e.g. 1024^3).
+enum : uint32_t {
+  kTplLinear = 0, kTplCorner8 = 1, kTplCorner8Wide = 2, kTplBrick8 = 3, kTplBrick8Wide = 4
+};
+// BRICK8: the CORNER8 cells grouped into 4x4x4-cell bricks of 512 B (bricks in
+// raster order, x fastest); inside a brick the cell index interleaves the
+// coordinate bits as (x0 x1 y0 z0 y1 z1), so one 128-B line holds a 4x2x2 cell
+// block (5x3x3 voxels) instead of a 16x1x1 row.
+constexpr uint32_t kBrickCells = 4;  // cells per brick edge
+__host__ __device__ __forceinline__ uint32_t brick_inner(uint32_t cx, uint32_t cy, uint32_t cz) {
+  return (cx & 3u) | ((cy & 1u) << 2) | ((cz & 1u) << 3) | ((cy & 2u) << 3) | ((cz & 2u) << 4);
+}
 
 // Plane indices of the SoA photon buffer.
 enum Plane : uint32_t {
@@ -74,6 +84,7 @@ struct MarchParams {
   // (D+1)(H+1) < 2^24): the gather address is u24 multiply-adds on a 32-bit
   // offset from the SGPR base instead of a 64-bit multiply chain
   uint32_t vol32;
+  uint32_t BW, BH;  // BRICK8: bricks along x and y (ceil((W+1)/4), ceil((H+1)/4))
   // |w| of every unprojected point < 2^120 (host bound from the matrix, the
   // resolution and blur): a precondition of the FAST march specialisation
   uint32_t w_bounded;

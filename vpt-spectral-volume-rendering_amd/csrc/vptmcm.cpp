@@ -286,8 +286,15 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
   P.D = h->D;
   {
     const uint64_t w1 = h->W + 1ull, h1 = h->H + 1ull, d1 = h->D + 1ull;
-    P.vol32 = (w1 * h1 * d1 * 8ull < (1ull << 32) && d1 * h1 < (1ull << 24) && w1 < (1ull << 24))
-                  ? 1u : 0u;
+    const uint64_t bw = (w1 + kBrickCells - 1) / kBrickCells, bh = (h1 + kBrickCells - 1) / kBrickCells,
+                   bd = (d1 + kBrickCells - 1) / kBrickCells;
+    P.BW = (uint32_t)bw;
+    P.BH = (uint32_t)bh;
+    if (h->layout == kLayoutBrick8)
+      P.vol32 = (bw * bh * bd * 512ull < (1ull << 32) && bd * bh < (1ull << 24)) ? 1u : 0u;
+    else
+      P.vol32 = (w1 * h1 * d1 * 8ull < (1ull << 32) && d1 * h1 < (1ull << 24) && w1 < (1ull << 24))
+                    ? 1u : 0u;
     if (h->variant & 8u) P.vol32 = 0u;  // variant bit 3: force the 64-bit gather (tests)
   }
   return P;
@@ -328,7 +335,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   hipEvent_t eb = nullptr, ee = nullptr;
   int rc = time_slot(h, &eb);
   if (rc) return rc;
-  const uint8_t* vol = h->layout == kLayoutCorner8 ? (const uint8_t*)h->vol_c8 : h->vol_lin;
+  const uint8_t* vol = h->layout != kLayoutLinear ? (const uint8_t*)h->vol_c8 : h->vol_lin;
   const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
   TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf};
   P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : 0u;
@@ -389,7 +396,7 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
     g_create_error = "vptmcm_create: unknown renderer kind";
     return VPTMCM_EINVAL;
   }
-  if (cfg->volume_layout > VPTMCM_LAYOUT_CORNER8) {
+  if (cfg->volume_layout > VPTMCM_LAYOUT_BRICK8) {
     g_create_error = "vptmcm_create: unknown volume layout";
     return VPTMCM_EINVAL;
   }
@@ -548,13 +555,20 @@ int vptmcm_volume_end(vptmcm* h) {
   if (int rc_ = flush_renders(h)) return rc_;
   if (!h->vol_lin) FAIL(h, VPTMCM_ESTATE, "volume_end before volume_begin");
   HIPCHK(h, hipSetDevice(h->device));
-  if (h->layout == kLayoutCorner8) {
-    size_t ncell = (size_t)(h->W + 1) * (h->H + 1) * (h->D + 1);
+  if (h->layout != kLayoutLinear) {
+    // CORNER8: (W+1)(H+1)(D+1) cells in raster order; BRICK8: the same cells
+    // in 4x4x4-cell bricks (the brick grid rounds each edge up to whole bricks)
+    const bool brick = h->layout == kLayoutBrick8;
+    const size_t bw = (h->W + kBrickCells) / kBrickCells, bh = (h->H + kBrickCells) / kBrickCells,
+                 bd = (h->D + kBrickCells) / kBrickCells;
+    size_t ncell = brick ? bw * bh * bd * 64 : (size_t)(h->W + 1) * (h->H + 1) * (h->D + 1);
     if (hipMalloc(&h->vol_c8, ncell * 8) != hipSuccess) {
       h->vol_c8 = nullptr;
-      FAIL(h, VPTMCM_ENOMEM, "corner8 volume allocation of %zu bytes failed", ncell * 8);
+      FAIL(h, VPTMCM_ENOMEM, "%s volume allocation of %zu bytes failed", brick ? "brick8" : "corner8",
+           ncell * 8);
     }
-    HIPCHK(h, launch_corner8(h->vol_lin, h->W, h->H, h->D, h->vol_c8, h->stream));
+    HIPCHK(h, launch_corner8(h->vol_lin, h->W, h->H, h->D, brick ? (uint32_t)bw : 0u,
+                             brick ? (uint32_t)bh : 0u, h->vol_c8, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipFree(h->vol_lin));
     h->vol_lin = nullptr;

@@ -35,7 +35,7 @@ function native() {
   return addon;
 }
 
-const LAYOUTS = { linear: 0, corner8: 1 };
+const LAYOUTS = { linear: 0, corner8: 1, brick8: 2 };
 const RESET_ON = ['extinction', 'anisotropy', 'bounces', 'materialTransferFunction',
   'spectrumRepresentation', 'lightEditor'];  // js:116-125
 
