@@ -63,6 +63,16 @@ typedef struct { float x, y; } v2;
 /* correctly rounded reciprocal: the only true division of the spec */
 static inline float rcp(float x) { return 1.0f / x; }
 
+/* ORC_ALT (liboracle_alt.so, tests/test_statistical_parity.py only): a second,
+ * equally legal WGSL arithmetic — libm logf/sinf/cosf, true division, no fused
+ * products — whose converged image must agree statistically with the spec's. */
+#ifdef ORC_ALT
+#define DIVF(a, b) ((a) / (b))
+#define fmaf(a, b, c) ((a) * (b) + (c))
+#else
+#define DIVF(a, b) ((a) * rcp(b)) /* WGSL a / b := a * RN(1/b) */
+#endif
+
 static inline float bitsf(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 static inline uint32_t fbits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 
@@ -83,6 +93,9 @@ static inline float smax(float a, float b) {
 /* log(x): reduce x = 2^e * m, m in [sqrt(1/2), sqrt(2)), s = f/(2+f) with
  * f = m-1, log(m) = 2 atanh(s) = 2s + s*z*(2/3 + z*(2/5 + ...)), z = s*s. */
 float orc_log(float x) {
+#ifdef ORC_ALT
+    return logf(x);
+#endif
     uint32_t b = fbits(x);
     if (x != x || (b >> 31)) return (x == 0.0f) ? -INFINITY : NAN; /* -0 -> -inf */
     if (x == 0.0f) return -INFINITY;
@@ -113,6 +126,11 @@ float orc_log(float x) {
 /* sin/cos: k = nearest(x * 2/pi); r = x - k*pi/2 (3-part Cody-Waite);
  * Taylor polynomials on |r| <= pi/4; quadrant select. */
 static void spec_sincos(float x, float* so, float* co) {
+#ifdef ORC_ALT
+    *so = sinf(x);
+    *co = cosf(x);
+    return;
+#endif
     float kf = floorf(fmaf(x, 0.6366197466850281f, 0.5f));
     float r = fmaf(-kf, 7.549790126404332e-08f,
                    fmaf(-kf, 0.0004837512969970703f, fmaf(-kf, 1.5703125f, x)));
@@ -154,8 +172,8 @@ uint16_t orc_f2h(float f) {
 static inline float dot3(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 static inline float len3(v3 a) { return sqrtf(dot3(a, a)); }
 static inline v3 norm3(v3 a) {
-    float il = rcp(len3(a));
-    v3 r = {a.x * il, a.y * il, a.z * il};
+    float l = len3(a);
+    v3 r = {DIVF(a.x, l), DIVF(a.y, l), DIVF(a.z, l)};
     return r;
 }
 
@@ -178,7 +196,7 @@ static inline float rnd_uniform(uint32_t* st) {
 }
 /* exponential.wgsl:3-5 */
 static inline float rnd_exponential(uint32_t* st, float rate) {
-    return -orc_log(rnd_uniform(st)) * rcp(rate);
+    return DIVF(-orc_log(rnd_uniform(st)), rate);
 }
 /* disk.wgsl:3-7 */
 static inline v2 rnd_disk(uint32_t* st) {
@@ -316,7 +334,7 @@ typedef struct ctx {
 
 /* sample_light, wgsl:62-73 */
 static float sample_light(const ctx* c, v3 d, float wavelength) {
-    float t = (wavelength - 400.0f) * rcp(700.0f - 400.0f);
+    float t = DIVF(wavelength - 400.0f, 700.0f - 400.0f);
     float intensity = orc_sample_light(c->light, t) * 5.0f;
     v3 ld = {c->u->light_dir[0], c->u->light_dir[1], c->u->light_dir[2]};
     if (len3(ld) < EPS) return intensity;
@@ -329,8 +347,8 @@ static v3 sample_hg(uint32_t* st, float g, v3 dir) {
     v3 u = rnd_sphere(st);
     if (fabsf(g) < EPS) return u;
     float g2 = g * g;
-    float c = (1.0f - g2) * rcp(fmaf(2.0f * g, rnd_uniform(st), 1.0f - g));
-    float hgcos = fmaf(-c, c, 1.0f + g2) * rcp(2.0f * g);
+    float c = DIVF(1.0f - g2, fmaf(2.0f * g, rnd_uniform(st), 1.0f - g));
+    float hgcos = DIVF(fmaf(-c, c, 1.0f + g2), 2.0f * g);
     float ud = dot3(u, dir);
     v3 w = {fmaf(-ud, dir.x, u.x), fmaf(-ud, dir.y, u.y), fmaf(-ud, dir.z, u.z)};
     v3 circle = norm3(w);
@@ -357,17 +375,14 @@ static void unproject_rand(uint32_t* st, v2 screen, const float* m, const float*
     float fd[4], td[4];
     mat_vec(m, nearp, fd);
     mat_vec(m, farp, td);
-    float iw = rcp(fd[3]);
-    from->x = fd[0] * iw; from->y = fd[1] * iw; from->z = fd[2] * iw;
-    iw = rcp(td[3]);
-    to->x = td[0] * iw; to->y = td[1] * iw; to->z = td[2] * iw;
+    from->x = DIVF(fd[0], fd[3]); from->y = DIVF(fd[1], fd[3]); from->z = DIVF(fd[2], fd[3]);
+    to->x = DIVF(td[0], td[3]); to->y = DIVF(td[1], td[3]); to->z = DIVF(td[2], td[3]);
 }
 
 /* intersectCube.wgsl:3-11 (only tnear is used by the caller) */
 static float intersect_cube_near(v3 o, v3 d) {
-    float rx = rcp(d.x), ry = rcp(d.y), rz = rcp(d.z);
-    float tminx = (0.0f - o.x) * rx, tminy = (0.0f - o.y) * ry, tminz = (0.0f - o.z) * rz;
-    float tmaxx = (1.0f - o.x) * rx, tmaxy = (1.0f - o.y) * ry, tmaxz = (1.0f - o.z) * rz;
+    float tminx = DIVF(0.0f - o.x, d.x), tminy = DIVF(0.0f - o.y, d.y), tminz = DIVF(0.0f - o.z, d.z);
+    float tmaxx = DIVF(1.0f - o.x, d.x), tmaxy = DIVF(1.0f - o.y, d.y), tmaxz = DIVF(1.0f - o.z, d.z);
     float t1x = smin(tminx, tmaxx), t1y = smin(tminy, tmaxy), t1z = smin(tminz, tmaxz);
     return smax(smax(t1x, t1y), t1z);
 }
@@ -420,10 +435,13 @@ static void photon_full_reset(const ctx* c, orc_photon* p, v2 screen, uint32_t* 
 /* PhotonSpectral_add_radiance, wgsl:292-302 */
 static void add_radiance(const ctx* c, orc_photon* p, float radiance) {
     uint32_t nb = n_bins_of(c->spec);
-    float in = rcp((float)p->samples);
     for (uint32_t i = 0u; i < nb && i < MAX_N_BINS; i++) {
         float tgt = (i == p->bin) ? radiance : 0.0f;
-        p->radiance[i] = fmaf(tgt - p->radiance[i], in, p->radiance[i]);
+#ifdef ORC_ALT
+        p->radiance[i] = p->radiance[i] + (tgt - p->radiance[i]) / (float)p->samples;
+#else
+        p->radiance[i] = fmaf(tgt - p->radiance[i], rcp((float)p->samples), p->radiance[i]);
+#endif
     }
 }
 
@@ -468,7 +486,7 @@ static void render_pixel(const ctx* c, uint32_t R, uint32_t x, uint32_t y, orc_p
 
         float dens = orc_sample_volume(c->vol, c->W, c->H, c->D, p.position);
         float smp[3];
-        orc_sample_tf(c->tf, (p.wavelength - 400.0f) * rcp(700.0f - 400.0f), dens, smp);
+        orc_sample_tf(c->tf, DIVF(p.wavelength - 400.0f, 700.0f - 400.0f), dens, smp);
         float albedo = smp[0], alpha = smp[1];
         float aniso = smp[2] * 2.0f - 1.0f;
 

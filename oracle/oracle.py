@@ -22,50 +22,61 @@ class Uniforms(C.Structure):  # orc_uniforms (render UBO, wgsl:8-18)
 
 
 _L = None
+_L_ALT = None
 
 
-def load() -> C.CDLL:
-    global _L
+def load(alt: bool = False) -> C.CDLL:
+    """liboracle.so (the arithmetic specification) or, with alt=True,
+    liboracle_alt.so (libm transcendentals, true division, no fused products:
+    the statistical parity test's alternative legal WGSL arithmetic)."""
+    global _L, _L_ALT
+    if alt:
+        if _L_ALT is None:
+            _L_ALT = _bind(HERE / "liboracle_alt.so")
+        return _L_ALT
     if _L is None:
-        p = HERE / "liboracle.so"
-        if not p.exists():
-            raise RuntimeError(f"{p} not built (make -C oracle)")
-        L = C.CDLL(str(p))
-        vp = C.c_void_p
-        L.orc_reset.argtypes = [C.c_uint32, C.POINTER(Uniforms), vp, vp, C.c_int]
-        L.orc_reset.restype = None
-        L.orc_render.argtypes = [C.c_uint32, C.POINTER(Uniforms), vp, vp, C.c_uint32, C.c_uint32,
-                                 C.c_uint32, vp, vp, vp, vp, vp, C.c_int, C.c_uint32, C.c_uint32]
-        L.orc_render.restype = None
-        L.orc_hash.argtypes = [C.c_uint32]
-        L.orc_hash.restype = C.c_uint32
-        L.orc_hash3.argtypes = [C.c_uint32] * 3
-        L.orc_hash3.restype = C.c_uint32
-        for f in ("orc_log", "orc_sin", "orc_cos"):
-            getattr(L, f).argtypes = [C.c_float]
-            getattr(L, f).restype = C.c_float
-        L.orc_f2h.argtypes = [C.c_float]
-        L.orc_f2h.restype = C.c_uint16
-        L.orc_sample_volume.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32,
-                                        C.POINTER(C.c_float)]
-        L.orc_sample_volume.restype = C.c_float
-        L.orc_sample_tf.argtypes = [vp, C.c_float, C.c_float, C.POINTER(C.c_float)]
-        L.orc_sample_tf.restype = None
-        L.orc_sample_light.argtypes = [vp, C.c_float]
-        L.orc_sample_light.restype = C.c_float
-        L.orc_reset_rgb.argtypes = [C.c_uint32, C.POINTER(Uniforms), vp, C.c_int]
-        L.orc_reset_rgb.restype = None
-        L.orc_render_rgb.argtypes = [C.c_uint32, C.POINTER(Uniforms), vp, C.c_uint32, C.c_uint32,
-                                     C.c_uint32, vp, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_int]
-        L.orc_render_rgb.restype = None
-        L.orc_srgb_to_linear.argtypes = [C.c_uint8]
-        L.orc_srgb_to_linear.restype = C.c_float
-        L.orc_tonemap_artistic.argtypes = [vp, C.c_uint32, vp, vp]
-        L.orc_tonemap_artistic.restype = None
-        L.orc_eval_batch.argtypes = [C.c_int, vp, vp, C.c_uint32]
-        L.orc_eval_batch.restype = None
-        _L = L
+        _L = _bind(HERE / "liboracle.so")
     return _L
+
+
+def _bind(p: Path) -> C.CDLL:
+    if not p.exists():
+        raise RuntimeError(f"{p} not built (make -C oracle)")
+    L = C.CDLL(str(p))
+    vp = C.c_void_p
+    L.orc_reset.argtypes = [C.c_uint32, C.POINTER(Uniforms), vp, vp, C.c_int]
+    L.orc_reset.restype = None
+    L.orc_render.argtypes = [C.c_uint32, C.POINTER(Uniforms), vp, vp, C.c_uint32, C.c_uint32,
+                             C.c_uint32, vp, vp, vp, vp, vp, C.c_int, C.c_uint32, C.c_uint32]
+    L.orc_render.restype = None
+    L.orc_hash.argtypes = [C.c_uint32]
+    L.orc_hash.restype = C.c_uint32
+    L.orc_hash3.argtypes = [C.c_uint32] * 3
+    L.orc_hash3.restype = C.c_uint32
+    for f in ("orc_log", "orc_sin", "orc_cos"):
+        getattr(L, f).argtypes = [C.c_float]
+        getattr(L, f).restype = C.c_float
+    L.orc_f2h.argtypes = [C.c_float]
+    L.orc_f2h.restype = C.c_uint16
+    L.orc_sample_volume.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32,
+                                    C.POINTER(C.c_float)]
+    L.orc_sample_volume.restype = C.c_float
+    L.orc_sample_tf.argtypes = [vp, C.c_float, C.c_float, C.POINTER(C.c_float)]
+    L.orc_sample_tf.restype = None
+    L.orc_sample_light.argtypes = [vp, C.c_float]
+    L.orc_sample_light.restype = C.c_float
+    L.orc_reset_rgb.argtypes = [C.c_uint32, C.POINTER(Uniforms), vp, C.c_int]
+    L.orc_reset_rgb.restype = None
+    L.orc_render_rgb.argtypes = [C.c_uint32, C.POINTER(Uniforms), vp, C.c_uint32, C.c_uint32,
+                                 C.c_uint32, vp, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_int]
+    L.orc_render_rgb.restype = None
+    L.orc_srgb_to_linear.argtypes = [C.c_uint8]
+    L.orc_srgb_to_linear.restype = C.c_float
+    L.orc_tonemap_artistic.argtypes = [vp, C.c_uint32, vp, vp]
+    L.orc_tonemap_artistic.restype = None
+    L.orc_eval_batch.argtypes = [C.c_int, vp, vp, C.c_uint32]
+    L.orc_eval_batch.restype = None
+    return L
 
 
 def _vp(a: np.ndarray):
@@ -75,8 +86,8 @@ def _vp(a: np.ndarray):
 class Oracle:
     """Stateful mirror of one renderer: photon buffer + inputs, CPU only."""
 
-    def __init__(self, R: int):
-        self.L = load()
+    def __init__(self, R: int, alt: bool = False):
+        self.L = load(alt)
         self.R = R
         self.photons = np.zeros((R * R, PHOTON_WORDS), np.uint32)
         self.spectrum = np.zeros(64, np.float32)
