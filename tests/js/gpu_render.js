@@ -49,6 +49,7 @@ const V = require(path.join(ROOT, 'vpt-spectral-volume-rendering_amd', 'js'));
   const tex = renderer.getTexture();
   fs.writeFileSync(path.join(out, 'photons.bin'), Buffer.from(renderer.readPhotons().buffer));
   fs.writeFileSync(path.join(out, 'rgba.bin'), Buffer.from(tex.data.buffer));
+  fs.writeFileSync(path.join(out, 'rgb32.bin'), Buffer.from(renderer.getRadianceRGB().data.buffer));
   if (c.tonemap) {                            // WebGPURenderingContext.js:156-188: tone map the target
     const tm = new (V.ToneMapperFactory('artistic'))(V.createDevice(0), renderer, null,
       { resolution: c.R });

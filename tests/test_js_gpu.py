@@ -40,7 +40,9 @@ def run_case(tmp_path, vol, tf, R=64, passes=3, ext=32.0, layout="corner8", stre
     assert r.returncode == 0, r.stdout + r.stderr
     ph = np.frombuffer((tmp_path / "photons.bin").read_bytes(), np.uint32).reshape(R * R, 36)
     rgba = np.frombuffer((tmp_path / "rgba.bin").read_bytes(), np.uint16).reshape(R, R, 4)
+    rgb32 = np.frombuffer((tmp_path / "rgb32.bin").read_bytes(), np.float32).reshape(R, R, 3)
     used = json.loads((tmp_path / "meta.json").read_text())["seeds_used"]
+    run_case.rgb32 = rgb32
     return ph, rgba, seeds, used
 
 
@@ -54,7 +56,7 @@ def oracle_replay(vol, tf, R, seeds, passes, ext, change_event=False):
     o.set_spectrum(cf.spectrum_buffer("12"))     # uploaded by the first render
     rgba = None
     for k in range(passes):
-        _, rgba = o.render(mvp, bits(seeds[1 + k]))
+        oracle_replay.rgb32, rgba = o.render(mvp, bits(seeds[1 + k]))
     if change_event:
         o.reset(mvp, bits(seeds[1 + passes]))
     return o.photons, rgba
@@ -66,7 +68,7 @@ def same(a, b):
 
 
 @pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
-@pytest.mark.parametrize("layout,stream", [("corner8", True), ("linear", False)])
+@pytest.mark.parametrize("layout,stream", [("corner8", True), ("linear", False), ("brick8", True)])
 def test_js_renderer_bitexact(tmp_path, layout, stream):
     vol, tf = cf.sphere_in_cube(64), cf.tf_spectral()
     ph, rgba, seeds, used = run_case(tmp_path, vol, tf, layout=layout, stream=stream)
@@ -74,6 +76,8 @@ def test_js_renderer_bitexact(tmp_path, layout, stream):
     want_ph, want_rgba = oracle_replay(vol, tf, 64, seeds, 3, 32.0)
     assert same(ph[:, :34], want_ph[:, :34])
     assert np.array_equal(rgba, want_rgba)
+    # getRadianceRGB(): the fp32 image before the f16 store (a13)
+    assert same(run_case.rgb32.view(np.uint32), oracle_replay.rgb32.view(np.uint32))
 
 
 @pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")

@@ -202,6 +202,15 @@ class MCMSpectralComputeRenderer extends PropertyBag {
     return { width: R, height: R, format: 'rgba16float', data };
   }
 
+  // The last pass's fp32 RGB (radiance_to_rgb before the rgba16float store,
+  // wgsl:304-326): not part of the reference surface, used for fp32 parity checks.
+  getRadianceRGB() {
+    const R = this._resolution;
+    const data = new Float32Array(R * R * 3);
+    native().readRGB(this._h, data, R);
+    return { width: R, height: R, format: 'rgb32float', data };
+  }
+
   getTextureSampler() {
     return { addressModeU: 'clamp-to-edge', addressModeV: 'clamp-to-edge', magFilter: 'nearest',
       minFilter: 'nearest' };  // base :102-107

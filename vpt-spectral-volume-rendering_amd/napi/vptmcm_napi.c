@@ -315,6 +315,19 @@ static napi_value js_read_rgba16f(napi_env env, napi_callback_info info) {
     return check(env, h, vptmcm_read_rgba16f(h, p));
 }
 
+/* readRGB(h, Float32Array(R*R*3), R): the last pass's fp32 radiance_to_rgb
+ * image before the f16 store (wgsl:304-326; vptmcm_read_rgb) */
+static napi_value js_read_rgb(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (get_args(env, info, 3, argv)) return NULL;
+    vptmcm* h = get_handle(env, argv[0]);
+    if (!h) return NULL;
+    uint32_t R = get_u32(env, argv[2]);
+    float* p = get_typed(env, argv[1], 4, (size_t)R * R * 3, NULL);
+    if (!p) return NULL;
+    return check(env, h, vptmcm_read_rgb(h, p));
+}
+
 /* setTransferFunction(h, Uint8Array(w*h*4), w, h) / setEnvironment(h, Uint8Array(4), 1, 1) */
 static napi_value image_call(napi_env env, napi_callback_info info, int env_map) {
     napi_value argv[4];
@@ -472,6 +485,7 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("renderPasses", js_render_passes);
     EXPORT("synchronize", js_synchronize);
     EXPORT("readRGBA16F", js_read_rgba16f);
+    EXPORT("readRGB", js_read_rgb);
     EXPORT("readPhotons", js_read_photons);
     EXPORT("tonemapArtistic", js_tonemap_artistic);
     EXPORT("setTransferFunction", js_set_transfer_function);
