@@ -187,8 +187,9 @@ def main():
 
     def passes(first: int, count: int, F: int = F) -> list:
         """Enqueue `count` passes from seeds[first:] in launches of <= F passes,
-        compositing across ranks whenever `every` passes have completed.
-        Returns the pass count of every march launch."""
+        compositing across ranks whenever `every` passes have completed and
+        after the region's last pass (so every region ends with a composite
+        the display could show). Returns the pass count of every march launch."""
         launches, done = [], 0
         while done < count:
             n = min(F, count - done)
@@ -197,7 +198,7 @@ def main():
             r.render_passes(mvp, seeds[first + done:first + done + n])
             launches.append(n)
             done += n
-            if multi and (first - 1 + done) % every == 0:
+            if multi and ((first - 1 + done) % every == 0 or done == count):
                 r.allreduce_radiance()
         return launches
 

@@ -1,0 +1,110 @@
+"""bench.py's N > 1 control flow (C4) on CPU: two ranks launched like the
+driver's torch.distributed.run, with the renderer replaced by a recording fake
+whose barrier / max-over-ranks / all-reduce run over gloo. Checks that the
+driver's command line (--steps 20 --warmup 5, fewer passes than the composite
+interval) still ends the timed region with a radiance all-reduce and a
+composite read, that ranks use distinct seed streams, that the rendezvous
+hands every rank the same unique id, and that rank 0 prints one JSON line with
+the whole-job value."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+
+DRIVER = textwrap.dedent('''
+    import importlib.util, json, os, sys, time
+    sys.argv = ["bench.py"] + json.loads(os.environ["BENCH_ARGV"])
+    spec = importlib.util.spec_from_file_location("bench", os.environ["BENCH_PATH"])
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    import numpy as np
+    import torch.distributed as dist
+
+    LOG = []
+
+    class Fake:
+        def __init__(self, R, device=0, layout=1):
+            LOG.append(["create", R, device, layout])
+            self.t0, self.launches = None, 0
+        def set_volume(self, v): LOG.append(["volume", list(v.shape)])
+        def set_material_tf(self, tf): pass
+        def set_light(self, spd, d): pass
+        def set_spectrum(self, s): pass
+        def set_params(self, **kw): pass
+        def comm_init(self, uid, world, rank):
+            LOG.append(["comm_init", bytes(uid).hex()[:16], world, rank])
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        def barrier(self): dist.barrier()
+        def reset(self, mvp, seed): LOG.append(["reset", int(seed)])
+        def render_passes(self, mvp, seeds):
+            LOG.append(["passes", [int(s) for s in seeds]])
+            self.launches += 1
+        def synchronize(self): pass
+        def enable_kernel_timing(self, on):
+            self.t0, self.launches = time.perf_counter(), 0
+            LOG.append(["timing"])
+        def kernel_time(self):
+            return (time.perf_counter() - self.t0) * 1e3 + 1e-3, self.launches
+        def allreduce_radiance(self): LOG.append(["allreduce"])
+        def read_composite(self):
+            LOG.append(["composite"])
+            return np.zeros((4, 4, 3), np.float32), np.zeros((4, 4), np.float32)
+        def allreduce_host(self, vals, op="sum"):
+            t = __import__("torch").tensor(np.asarray(vals, np.float64))
+            dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+            return t.numpy()
+        def close(self): dist.destroy_process_group()
+
+    bench.vptmcm.Renderer = Fake
+    bench.vptmcm.unique_id = lambda: os.urandom(128)
+    bench.main()
+    Path = __import__("pathlib").Path
+    Path(os.environ["LOG_OUT"]).write_text(json.dumps(LOG))
+''')
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks_driver_command_line(tmp_path):
+    port = _free_port()
+    argv = ["--gpus", "2", "--steps", "20", "--warmup", "5", "--volume", "16", "--resolution", "16",
+            "--cpu-seconds", "0"]
+    procs = []
+    for rank in (0, 1):
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BENCH_ARGV=json.dumps(argv),
+                   BENCH_PATH=str(REPO / "bench.py"), LOG_OUT=str(tmp_path / f"log{rank}.json"),
+                   TORCHELASTIC_RUN_ID=f"t{port}")
+        procs.append(subprocess.Popen([sys.executable, "-c", DRIVER], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True, cwd=str(tmp_path)))
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, o + e
+    line = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
+    assert len(line) == 1 and not [ln for ln in outs[1][0].splitlines() if ln.startswith("{")]
+    rec = json.loads(line[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 20 and rec["warmup"] == 5
+    assert rec["value"] > 0 and rec["config"]["workload"].startswith("C4")
+    logs = [json.loads((tmp_path / f"log{r}.json").read_text()) for r in (0, 1)]
+    uids = {e[1] for lg in logs for e in lg if e[0] == "comm_init"}
+    assert len(uids) == 1, "ranks must share rank 0's unique id"
+    for r, lg in enumerate(logs):
+        assert ["create", 16, r, 1] in lg  # one GPU per local rank
+        t = [e[0] for e in lg].index("timing")
+        timed = lg[t + 1:]
+        kinds = [e[0] for e in timed]
+        assert sum(len(e[1]) for e in timed if e[0] == "passes") == 20
+        last_pass = max(i for i, k in enumerate(kinds) if k == "passes")
+        assert "allreduce" in kinds[last_pass:], "timed region must end with a composite"
+        assert kinds.index("composite") > last_pass
+    seeds = [[s for e in lg if e[0] == "passes" for s in e[1]] for lg in logs]
+    assert not set(seeds[0]) & set(seeds[1]), "ranks must use distinct seed streams"

@@ -121,6 +121,14 @@ class MCMComputeRenderer extends PropertyBag {
     return { width: R, height: R, format: 'rgba16float', data };
   }
 
+  // The last pass's fp32 radiance (before the rgba16float store): parity checks.
+  getRadianceRGB() {
+    const R = this._resolution;
+    const data = new Float32Array(R * R * 3);
+    native().readRGB(this._h, data, R);
+    return { width: R, height: R, format: 'rgb32float', data };
+  }
+
   getTextureSampler() {
     return { addressModeU: 'clamp-to-edge', addressModeV: 'clamp-to-edge', magFilter: 'nearest',
       minFilter: 'nearest' };
