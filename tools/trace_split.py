@@ -2,7 +2,9 @@
 """Split a rocprofv3 kernel trace's k_march dispatches into the bench's launch
 kinds (fused multi-pass launches vs one-pass launches) so the per-launch
 average can be compared with bench.py's event-timed kernel_avg_us.
-Usage: python tools/trace_split.py run_kernel_trace.csv [out.json [W K F]]"""
+Usage: python tools/trace_split.py run_kernel_trace.csv [out.json [W K F [SETTLE]]]
+(SETTLE = config.clock_settle_passes of the profiled bench line: untimed
+clock-settling launches of F passes that precede the warm-up)"""
 import csv
 import json
 import sys
@@ -21,7 +23,8 @@ def main():
     W = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
     K = int(sys.argv[4]) if len(sys.argv) > 4 else 1024
     F = int(sys.argv[5]) if len(sys.argv) > 5 else 32
-    warm, timed = -(-W // F), -(-K // F)
+    settle = int(sys.argv[6]) if len(sys.argv) > 6 else 0
+    warm, timed = settle // F + -(-W // F), -(-K // F)
     t = long_[warm:warm + timed]
     api = long_[warm + timed:]
     out = {"k_march_dispatches": len(d),
