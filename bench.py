@@ -59,7 +59,9 @@ def parse():
     ap.add_argument("--photon-steps", type=int, default=8, help="S: steps per pass")
     ap.add_argument("--extinction", type=float, default=32.0)
     ap.add_argument("--layout", choices=["corner8", "brick8", "linear"], default="corner8")
-    ap.add_argument("--tf", choices=["spectral", "grey", "zero"], default="spectral")
+    ap.add_argument("--tf", choices=["spectral", "grey", "zero", "materials", "materials_const"],
+                    default="spectral", help="TF (non-spectral: analysis only)")
+    ap.add_argument("--bins", default="12", help="spectrum bin layout (non-12: analysis only)")
     ap.add_argument("--camera", choices=["default", "near", "orbit", "orbit_tilted"],
                     default="default", help="golden camera pose (non-default: analysis only)")
     ap.add_argument("--fuse", type=int, default=32,
@@ -152,9 +154,11 @@ def main():
     t = time.perf_counter()
     vol = cf.fbm_volume(a.volume, 512 if a.volume == 512 else a.volume)
     gen_s = time.perf_counter() - t
-    tf = {"spectral": cf.tf_spectral, "grey": cf.tf_grey, "zero": cf.tf_zero}[a.tf]()
+    tf = {"spectral": cf.tf_spectral, "grey": cf.tf_grey, "zero": cf.tf_zero,
+          "materials": lambda: cf.tf_materials(True),
+          "materials_const": lambda: cf.tf_materials(False)}[a.tf]()
     spd, ldir = cf.light_default()
-    spec = cf.spectrum_buffer("12")
+    spec = cf.spectrum_buffer(a.bins)
     mvp = cf.default_mvp_inverse() if a.camera == "default" else cf.golden_mvp(a.camera)
 
     # VPTMCM_BENCH_DEVICE pins every rank to one ordinal (rehearsing the N > 1
@@ -310,7 +314,7 @@ def main():
                 if (e.get("resolution") == R and e.get("steps") == S and e.get("layout") == a.layout
                         and e.get("volume", 512) == a.volume
                         and e.get("passes_per_launch", 1) == shapes[0]
-                        and a.tf == "spectral" and a.camera == "default"):
+                        and a.tf == "spectral" and a.camera == "default" and a.bins == "12"):
                     traffic = e.get("hbm_bytes_per_launch")
                     traffic_src = f"{tp.relative_to(REPO) if tp.is_relative_to(REPO) else tp}"
                     # VALU issue roofline: the launch's VALU wave-instructions
@@ -361,7 +365,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {
                 "workload": f"C{'4' if multi else '3'}: {a.volume}^3 fBm volume (seed 512), spectral TF "
-                            f"(HG g=0.702), R={R}, S={S}, 12 bins, extinction {a.extinction}, "
+                            f"(HG g=0.702), R={R}, S={S}, {a.bins} bins, extinction {a.extinction}, "
                             f"{a.camera} camera",
                 "resolution": R, "photon_steps_per_pass": S, "volume": a.volume,
                 "volume_layout": a.layout, "passes_per_launch": ppl,

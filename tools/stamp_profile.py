@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--layout", default="corner8")
     ap.add_argument("--volume", type=int, default=512)
     ap.add_argument("--samples", type=int, default=8, help="one-pass launches averaged")
+    ap.add_argument("--tf", default="spectral", choices=["spectral", "materials", "materials_const"])
+    ap.add_argument("--bins", default="12")
     ap.add_argument("--fused", type=int, default=32,
                     help="passes of a final fused launch whose clock is reported")
     a = ap.parse_args()
@@ -39,10 +41,11 @@ def main():
     layout = {"corner8": vptmcm.LAYOUT_CORNER8, "brick8": vptmcm.LAYOUT_BRICK8}[a.layout]
     r = vptmcm.Renderer(R, device=0, layout=layout)
     r.set_volume(cf.fbm_volume(a.volume, 512 if a.volume == 512 else a.volume))
-    r.set_material_tf(cf.tf_spectral())
+    r.set_material_tf({"spectral": cf.tf_spectral, "materials": lambda: cf.tf_materials(True),
+                       "materials_const": lambda: cf.tf_materials(False)}[a.tf]())
     spd, ldir = cf.light_default()
     r.set_light(spd, ldir)
-    r.set_spectrum(cf.spectrum_buffer("12"))
+    r.set_spectrum(cf.spectrum_buffer(a.bins))
     r.set_params(extinction=32.0, bounces=8, steps=S)
     mvp = cf.default_mvp_inverse() if a.camera == "default" else cf.golden_mvp(a.camera)
     seeds = cf.seed_stream(32, start=0)
@@ -75,6 +78,7 @@ def main():
         walls.append(w[:, 4].astype(np.float64))
     seg = np.concatenate(segs)
     out = {"volume_waves": int(seg.shape[0] // a.samples), "camera": a.camera, "layout": a.layout,
+           "tf": a.tf, "bins": a.bins,
            "volume": a.volume,
            "cycles_per_volume_step_median": {s: round(float(np.median(seg[:, i])), 1) for i, s in enumerate(SEG)},
            "cycles_per_volume_step_mean": {s: round(float(seg[:, i].mean()), 1) for i, s in enumerate(SEG)},

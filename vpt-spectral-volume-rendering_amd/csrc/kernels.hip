@@ -27,6 +27,9 @@
 #ifndef VPT_SLAB_HW
 #define VPT_SLAB_HW 1  // hardware min/max slab test for generic fixed near points
 #endif
+#ifndef VPT_NB_ZERO
+#define VPT_NB_ZERO 1  // nb < 12: unguarded 12-bin loops over zeroed unused bins
+#endif
 #ifndef VPT_PRIO
 #define VPT_PRIO 1  // s_setprio level of volume waves (0 = off); 11 % faster passes
 #endif
@@ -404,6 +407,19 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 #endif
   Photon p;
   if (live) load_photon(ph, S, i, p);  // issue the state loads before the LDS fill
+#if VPT_NB_ZERO
+  // Bins past nb (nb < 12) are never read or written by the reference
+  // (wgsl:296, :310): their registers start at 0 and are left out of the final
+  // store, so every per-step and per-pass bin loop below runs over all 12 bins
+  // without per-bin nb guards: the deferred update keeps them finite (0 decays
+  // to 0; their one-hot weight is 0) and their CMF means are 0 past nb, so
+  // fma(rad, 0, X) == X adds nothing (X >= +0).
+  if constexpr (!NBF) {
+#pragma unroll
+    for (int b = 0; b < kMaxBins; b++)
+      if ((uint32_t)b >= P.nb) p.rad[b] = 0.0f;
+  }
+#endif
 
   const uint4* src = reinterpret_cast<const uint4*>(tf_rg);
 #pragma unroll
@@ -495,7 +511,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       const float inv = on ? rcp_in_range(on ? pend_n : 1.0f) : 0.0f;
 #pragma unroll
       for (int b = 0; b < kMaxBins; b++) {
-        if (NBF || (uint32_t)b < P.nb) {
+        if (NBF || VPT_NB_ZERO || (uint32_t)b < P.nb) {
           const float oh = (float)((pend_oh[b >> 2] >> ((b & 3) * 8)) & 0xffu);
           p.rad[b] = fmaf(fmaf(oh, pend_l, -p.rad[b]), inv, p.rad[b]);
         }
@@ -748,7 +764,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     const auto cmf = cmf_table();  // xb[12], yb[12], zb[12]
 #pragma unroll
     for (int b = 0; b < kMaxBins; b++) {
-      if (NBF || (uint32_t)b < P.nb) {
+      if (NBF || VPT_NB_ZERO || (uint32_t)b < P.nb) {
         X = fmaf(p.rad[b], cmf[b], X);
         Y = fmaf(p.rad[b], cmf[kMaxBins + b], Y);
         Z = fmaf(p.rad[b], cmf[2 * kMaxBins + b], Z);
@@ -775,7 +791,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 #endif
   store_state(ph, S, i, p);  // uPhotons[globalIndex] = p (wgsl:165), once per launch
 #pragma unroll
-  for (int b = 0; b < kMaxBins; b++) ph[(kRad0 + b) * S + i] = p.rad[b];
+  for (int b = 0; b < kMaxBins; b++)
+    if (NBF || !VPT_NB_ZERO || (uint32_t)b < P.nb) ph[(kRad0 + b) * S + i] = p.rad[b];
 
   if (lane == 0u) T.flags_out[tile] = entered ? 1u : 0u;  // the next pass's schedule
 #if VPT_STAMP
@@ -1080,10 +1097,13 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba, float* rgb32,
                         hipStream_t s, hipEvent_t ev_beg, hipEvent_t ev_end) {
   dim3 grid(tile_blocks(P, kMarchBlock));
-  const bool spec = (variant & 1u) == 0u;  // variant bit 0: plain (non-speculative) step
-  const bool nbf = P.nb >= (uint32_t)kMaxBins;  // every radiance bin in use
+  // variant bits (analysis; results identical; bits 1-3 are the host's):
+  // 0 plain (non-speculative) step, 4 no FAST specialisation (MODE 1), 5 the
+  // generic MODE 0 even with nb = 12
+  const bool spec = (variant & 1u) == 0u;
+  const bool nbf = P.nb >= (uint32_t)kMaxBins && (variant & 32u) == 0u;  // every radiance bin in use
   const bool fast = nbf && P.bins_uniform && P.b_rows && P.w_bounded && P.blur == 0.0f &&
-                    (P.R & 1u) == 0u && !P.light_iso;
+                    (P.R & 1u) == 0u && !P.light_iso && (variant & 16u) == 0u;
   // hipExtLaunchKernelGGL stamps the events from the dispatch packet itself
   // (no extra barrier/marker packets between back-to-back launches)
 #define VPT_LAUNCH(LAY, SP, MO)                                                                \
