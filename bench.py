@@ -332,8 +332,9 @@ def main():
         except (ValueError, OSError, KeyError):
             traffic, issue = None, None
 
-    # The general (non-FAST) march on the same volume: MODE 0 specialisation
-    # (8 uneven bins, wavelength-varying anisotropy from the 4-corner table)
+    # The march on a UI-like configuration of the same volume: 8 uneven bins and
+    # a materials TF with wavelength-varying anisotropy (MODE 4: FAST geometry,
+    # the TF's distinct rows in LDS, the general bin search)
     general = None
     if a.general_steps > 0 and not multi:
         r.synchronize()
@@ -355,7 +356,8 @@ def main():
                    "kernel_us_per_pass": (round(gk_ms * 1e3 / a.general_steps, 3)
                                           if not a.no_timing else None),
                    "workload": "same volume/camera, tf_materials(varying anisotropy), "
-                               "8_uneven bins: the generic march specialisation"}
+                               "8_uneven bins: a UI-like TF (row-deduplicated in LDS) and "
+                               "uneven bins, march MODE 4 (MODE 2 is the headline's)"}
 
     if rank == 0:
         out = {

@@ -124,6 +124,33 @@ def test_march_variants_bitexact(variant, layout, tfname, monkeypatch):
     gpu.close()
 
 
+def _tf_many_rows_varying_b():
+    """> kTfRowsMax distinct rows AND a wavelength-varying anisotropy channel:
+    neither the LDS row table nor the deduplicated TF applies (tf_b4 gather)."""
+    t = cf.tf_spectral()
+    t[..., 2] = (40 + (np.arange(256) * 0.6)).astype(np.uint8)[None, :]
+    return t
+
+
+@pytest.mark.parametrize("variant", ["0", "16", "32"])
+@pytest.mark.parametrize("spec", ["12", "8_uneven", "3", "12_wide"])
+@pytest.mark.parametrize("tfname", ["materials", "materials_const_b", "many_rows_b"])
+def test_tf_modes_bitexact(variant, spec, tfname, monkeypatch):
+    """The march specialisations chosen per launch — MODE 2 (FAST: row-invariant
+    anisotropy), 3 (row-deduplicated LDS TF, 12 equal bins), 4 (deduplicated TF,
+    any bins), 1/0 (generic; variant bits 4/5 force them) — against the oracle,
+    bit for bit, over TFs with few distinct rows (the UI's materials, with
+    constant and wavelength-varying anisotropy) and many rows with varying
+    anisotropy (tf_b4 gather), for equal, uneven, few and wide bin layouts."""
+    monkeypatch.setenv("VPTMCM_MARCH_VARIANT", variant)
+    tf = {"materials": cf.tf_materials(True), "materials_const_b": cf.tf_materials(False),
+          "many_rows_b": _tf_many_rows_varying_b()}[tfname]
+    gpu, cpu = make_pair(64, cf.fbm_volume(64, 7, nthreads=8), tf, spec=spec, ext=24.0)
+    run_and_compare(gpu, cpu, cf.default_mvp_inverse(), cf.seed_stream(4, start=0),
+                    f"variant {variant} bins {spec} tf {tfname}")
+    gpu.close()
+
+
 @pytest.mark.parametrize("camera", ["near", "orbit", "orbit_tilted"])
 def test_cameras_and_bins(camera):
     for spec in ("6", "3", "8_uneven", "12_wide"):

@@ -23,6 +23,7 @@ inline uint32_t march_blocks(const MarchParams& P) { return tile_blocks(P, kBloc
 //   tf_b4  u32[257*257]: the 4 anisotropy corners of each bilinear cell
 //   tf_brow u8[256]: anisotropy per row when it does not vary with wavelength
 constexpr uint32_t kTfCells = 257;
+constexpr uint32_t kTfRowsMax = 128;  // distinct TF rows the LDS holds as u32 texels (128 KB)
 
 // Per-pass tile schedule of the march (see schedule_tile in kernels.hip): one
 // byte per tile, written by the pass ("its wave entered the volume") and read
@@ -57,7 +58,8 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
                         const TileSched& T, float* ph,
                         const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba, float* rgb32,
-                        hipStream_t s, hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr);
+                        hipStream_t s, hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr,
+                        const uint32_t* tf_rows = nullptr, const uint8_t* tf_rowmap = nullptr);
 // Artistic tone mapper uniforms, derived on the host from (low, mid, high,
 // saturation, gamma) (WebGPUArtisticToneMapper.js:81-88, ArtisticToneMapper.wgsl:40-46).
 struct ToneParams {

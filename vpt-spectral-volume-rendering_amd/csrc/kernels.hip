@@ -357,7 +357,9 @@ __device__ __forceinline__ const __attribute__((address_space(4))) float* cmf_ta
 // path), a wavelength-invariant TF blue channel (LDS row table), blur == 0 with
 // an even R (every near point fixed), a host-bounded |w| (one-compare
 // reciprocal guard) and a directional light: the per-step configuration
-// branches vanish.
+// branches vanish. 3: MODE 2's geometry, light and bins with a general TF
+// held row-deduplicated in LDS (wavelength-varying anisotropy: the UI's
+// materials, MaterialTransferFunction.js:56-75). 4: MODE 3 with any bin layout.
 template <uint32_t L, bool SPEC, uint32_t MODE>
 __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const MarchParams P,
                                                        const TileSched T, float* __restrict__ ph,
@@ -367,9 +369,13 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
                                                        const uint8_t* __restrict__ tf_brow,
                                                        const uint8_t* __restrict__ light,
                                                        uint16_t* __restrict__ rgba,
-                                                       float* __restrict__ rgb32) {
-  constexpr bool NBF = MODE >= 1u;
-  constexpr bool FAST = MODE == 2u;
+                                                       float* __restrict__ rgb32,
+                                                       const uint8_t* __restrict__ tf_rowmap) {
+  constexpr bool NBF = MODE >= 1u && MODE <= 3u;
+  constexpr bool GEO = MODE >= 2u;    // FAST geometry and light (MODE 2, 3, 4)
+  constexpr bool UNIB = MODE == 2u || MODE == 3u;  // ... and 12 equal-width bins
+  constexpr bool FAST = MODE == 2u;   // ... and a row-invariant anisotropy channel
+  constexpr bool DEDUP = MODE >= 3u;  // ... or a row-deduplicated LDS TF (P.tf_dedup)
   // (albedo, alpha) of the whole TF in LDS: every step's 4 TF taps become
   // ds_read_u16 instead of divergent L2 gathers. When the anisotropy channel
   // does not vary with wavelength (P.b_rows), its 256 row values sit in LDS
@@ -378,6 +384,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __shared__ uint4 s_tf4[256 * 256 * 2 / 16];
   __shared__ float s_light[256];
   __shared__ float s_brow[256];
+  __shared__ uint32_t s_rowmap[256];  // P.tf_dedup: density row -> first texel of its distinct row
 
   __shared__ uint32_t s_red[17];
   __shared__ uint32_t s_tile[16];
@@ -428,6 +435,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   if (threadIdx.x < 256u) {
     s_light[threadIdx.x] = (float)light[threadIdx.x];
     s_brow[threadIdx.x] = (float)tf_brow[threadIdx.x];
+    if (DEDUP || (!FAST && P.tf_dedup)) s_rowmap[threadIdx.x] = (uint32_t)tf_rowmap[threadIdx.x] * 256u;
   }
   __syncthreads();
   if (!live) return;
@@ -570,11 +578,11 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         uint32_t h1 = pcg_hash(sw), h2 = pcg_hash(h1), h3 = pcg_hash(h2);
         uint32_t h4 = pcg_hash(h3), h5 = pcg_hash(h4);
         p.samples++;
-        set_pending((float)p.samples, exit_radiance<FAST>(P, p.dir, wc), p.bin);
+        set_pending((float)p.samples, exit_radiance<GEO>(P, p.dir, wc), p.bin);
         p.dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
         p.bounces = 0u;
         p.lambda = lambda_of(P, h5);
-        p.bin = bin_of<FAST>(P, p.lambda);
+        p.bin = bin_of<UNIB>(P, p.lambda);
         wc = wave_const(p.lambda, s_light);
         st = h5;
         stale = true;
@@ -611,8 +619,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         float dx = 0.0f, dy = 0.0f;
         if (!fixed) disk_of(h1, h2, dx, dy);
         Photon rc;
-        reset_from_draws<FAST>(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
-        terminate(exit_radiance<FAST>(P, p.dir, wc), rc);
+        reset_from_draws<GEO, UNIB>(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
+        terminate(exit_radiance<GEO>(P, p.dir, wc), rc);
         wc = wave_const(rc.lambda, s_light);
         st = h5;
         STAMP_AT(5);
@@ -640,7 +648,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       disk_of(h1, h2, dx, dy);
       Photon rc;
       WaveConst wcr = wc;
-      reset_from_draws<FAST>(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
+      reset_from_draws<GEO, UNIB>(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
       wcr = wave_const(rc.lambda, s_light);
       float nrm = fmaf(dy, dy, dx * dx);  // sphere.wgsl
       float srad = 2.0f * sqrt_z(1.0f - nrm);
@@ -659,11 +667,27 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       float fr;
       int ir = axis_floor_in(d, 256.0f, &fr);
       uint32_t b4 = 0u;
-      if (!(FAST || P.b_rows)) b4 = tf_b4[(uint32_t)clampi(ir + 1, 256) * kTfCells + (uint32_t)wc.cc];
+      const bool dedup = DEDUP || (!FAST && P.tf_dedup);
+      if (!(FAST || DEDUP || P.b_rows || P.tf_dedup))
+        b4 = tf_b4[(uint32_t)clampi(ir + 1, 256) * kTfCells + (uint32_t)wc.cc];
       const uint32_t ri0 = (uint32_t)clampi(ir, 255), ri1 = (uint32_t)clampi(ir + 1, 255);
-      uint32_t r0 = ri0 * 256u, r1 = ri1 * 256u;
-      const uint32_t t00 = s_tf[r0 + wc.c0], t10 = s_tf[r0 + wc.c1];
-      const uint32_t t01 = s_tf[r1 + wc.c0], t11 = s_tf[r1 + wc.c1];
+      uint32_t t00, t10, t01, t11;
+      if (dedup) {  // u32 texels of the distinct rows: albedo, alpha and anisotropy in one read
+        const uint32_t* s_t32 = reinterpret_cast<const uint32_t*>(s_tf4);
+        const uint32_t r0 = s_rowmap[ri0], r1 = s_rowmap[ri1];
+        t00 = s_t32[r0 + wc.c0];
+        t10 = s_t32[r0 + wc.c1];
+        t01 = s_t32[r1 + wc.c0];
+        t11 = s_t32[r1 + wc.c1];
+        // the 4-corner anisotropy cell tf_b4 would hold: (r0,c0) (r0,c1) (r1,c0) (r1,c1)
+        b4 = ((t00 >> 16) & 0xffu) | ((t10 >> 8) & 0xff00u) | (t01 & 0xff0000u) | ((t11 << 8) & 0xff000000u);
+      } else {
+        const uint32_t r0 = ri0 * 256u, r1 = ri1 * 256u;
+        t00 = s_tf[r0 + wc.c0];
+        t10 = s_tf[r0 + wc.c1];
+        t01 = s_tf[r1 + wc.c0];
+        t11 = s_tf[r1 + wc.c1];
+      }
       float albedo = lerp(lerp(byte_f(t00, 0), byte_f(t10, 0), wc.fc),
                           lerp(byte_f(t01, 0), byte_f(t11, 0), wc.fc), fr) * kInv255;
       float alpha = lerp(lerp(byte_f(t00, 8), byte_f(t10, 8), wc.fc),
@@ -675,12 +699,12 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       STAMP_AT(3);
       if (oob || wheel < pabs) {
         // exit (wgsl:142-150) or absorption (wgsl:151-155): adopt the candidate
-        terminate(oob ? exit_radiance<FAST>(P, p.dir, wc) : 0.0f, rc);
+        terminate(oob ? exit_radiance<GEO>(P, p.dir, wc) : 0.0f, rc);
         wc = wcr;
         st = h5;
       } else if (wheel < pabs + pscat) {
         // HG scatter (wgsl:82-97, :156-160) with g from the TF blue channel
-        float bch = (FAST || P.b_rows) ? lerp(s_brow[ri0], s_brow[ri1], fr) * kInv255
+        float bch = (FAST || (!DEDUP && P.b_rows)) ? lerp(s_brow[ri0], s_brow[ri1], fr) * kInv255
                              : lerp(lerp(byte_f(b4, 0), byte_f(b4, 8), wc.fc),
                                     lerp(byte_f(b4, 16), byte_f(b4, 24), wc.fc), fr) * kInv255;
         float g = bch * 2.0f - 1.0f;
@@ -737,7 +761,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 
       if (oob || wheel < pabs) {
         // exit (wgsl:142-150) or absorption (wgsl:151-155)
-        float rad = oob ? exit_radiance<FAST>(P, p.dir, wc) : 0.0f;  // sample_light, wgsl:62-73
+        float rad = oob ? exit_radiance<GEO>(P, p.dir, wc) : 0.0f;  // sample_light, wgsl:62-73
         p.samples++;
         add_radiance<NBF>(P, p.rad, rcp((float)p.samples), p.bin, rad);
         photon_reset(P, p, sx, sy, fixed, from, st);
@@ -1095,24 +1119,37 @@ hipError_t launch_reset(const MarchParams& P, float* ph, hipStream_t s) {
 hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P, const PassSeeds& PS,
                         const TileSched& T, float* ph, const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba, float* rgb32,
-                        hipStream_t s, hipEvent_t ev_beg, hipEvent_t ev_end) {
+                        hipStream_t s, hipEvent_t ev_beg, hipEvent_t ev_end,
+                        const uint32_t* tf_rows, const uint8_t* tf_rowmap) {
   dim3 grid(tile_blocks(P, kMarchBlock));
   // variant bits (analysis; results identical; bits 1-3 are the host's):
-  // 0 plain (non-speculative) step, 4 no FAST specialisation (MODE 1), 5 the
-  // generic MODE 0 even with nb = 12
+  // 0 plain (non-speculative) step, 4 none of the GEO specialisations (MODE 1
+  // or 0), 5 the generic MODE 0 even with nb = 12
   const bool spec = (variant & 1u) == 0u;
   const bool nbf = P.nb >= (uint32_t)kMaxBins && (variant & 32u) == 0u;  // every radiance bin in use
-  const bool fast = nbf && P.bins_uniform && P.b_rows && P.w_bounded && P.blur == 0.0f &&
-                    (P.R & 1u) == 0u && !P.light_iso && (variant & 16u) == 0u;
+  const bool geom = P.w_bounded && P.blur == 0.0f && (P.R & 1u) == 0u && !P.light_iso &&
+                    (variant & 48u) == 0u;
+  const bool geo = geom && nbf && P.bins_uniform;
+  const bool fast = geo && P.b_rows;
+  // the row-deduplicated LDS TF serves the speculative non-FAST marches
+  // (P.tf_dedup on entry: the host found <= kTfRowsMax distinct rows)
+  MarchParams Q = P;
+  Q.tf_dedup = (P.tf_dedup && tf_rows && tf_rowmap && spec && !fast) ? 1u : 0u;
+  const uint16_t* tf_lds = Q.tf_dedup ? reinterpret_cast<const uint16_t*>(tf_rows) : tf_rg;
+  const uint8_t* rowmap = tf_rowmap ? tf_rowmap : tf_brow;
   // hipExtLaunchKernelGGL stamps the events from the dispatch packet itself
   // (no extra barrier/marker packets between back-to-back launches)
 #define VPT_LAUNCH(LAY, SP, MO)                                                                \
   hipExtLaunchKernelGGL((k_march<LAY, SP, MO>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
-                        PS, P, T, ph, vol, tf_rg, tf_b4, tf_brow, light, rgba, rgb32)
+                        PS, Q, T, ph, vol, tf_lds, tf_b4, tf_brow, light, rgba, rgb32, rowmap)
 #define VPT_LAUNCH_NB(LAY, SP)        \
   do {                                \
     if (SP && fast)                   \
       VPT_LAUNCH(LAY, SP, SP ? 2u : 1u); \
+    else if (SP && geo && Q.tf_dedup) \
+      VPT_LAUNCH(LAY, SP, SP ? 3u : 1u); \
+    else if (SP && geom && Q.tf_dedup) \
+      VPT_LAUNCH(LAY, SP, SP ? 4u : 1u); \
     else if (nbf)                     \
       VPT_LAUNCH(LAY, SP, 1u);        \
     else                              \

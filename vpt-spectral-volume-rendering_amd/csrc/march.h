@@ -88,6 +88,11 @@ struct MarchParams {
   // |w| of every unprojected point < 2^120 (host bound from the matrix, the
   // resolution and blur): a precondition of the FAST march specialisation
   uint32_t w_bounded;
+  // Row-deduplicated TF (set by launch_march for non-FAST launches): the LDS TF
+  // holds the TF's distinct density rows as u32 texels (albedo | alpha << 8 |
+  // anisotropy << 16) and s_rowmap maps a density row to its distinct row, so
+  // the anisotropy taps come from LDS with albedo and alpha (no tf_b4 gather).
+  uint32_t tf_dedup;
 };
 
 // ---------------------------------------------------------------- RNG draws
@@ -301,7 +306,9 @@ __device__ __forceinline__ float lambda_of(const MarchParams& P, uint32_t h5) {
   return fmaf((float)h5 * 2.3283064365386963e-10f, P.max_lam - P.min_lam, P.min_lam);
 }
 
-template <bool UNI = false>
+// UNI: blur 0, even R and a host-bounded |w| (fixed near points, one-compare
+// reciprocal guard); UNIB: equal-width bins (bin_of's arithmetic path).
+template <bool UNI = false, bool UNIB = UNI>
 __device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p, float sx, float sy,
                                                  bool fixed_from, f3 from, float dx, float dy,
                                                  uint32_t h3, uint32_t h4, uint32_t h5,
@@ -317,7 +324,7 @@ __device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p
   else
     p.pos = ray_start(from, p.dir);
   p.lambda = lambda_of(P, h5);
-  p.bin = bin_of<UNI>(P, p.lambda);
+  p.bin = bin_of<UNIB>(P, p.lambda);
 }
 
 __device__ __forceinline__ void screen_of(const MarchParams& P, uint32_t x, uint32_t y, float& sx,

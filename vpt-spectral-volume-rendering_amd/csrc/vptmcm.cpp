@@ -50,6 +50,9 @@ struct vptmcm {
   uint16_t* tf_rg = nullptr;   // 65536 (albedo | alpha << 8) texels
   uint32_t* tf_b4 = nullptr;   // 257*257 anisotropy corner cells
   uint8_t* tf_brow = nullptr;  // 256 anisotropy rows (valid when b_rows)
+  uint32_t* tf_rows = nullptr;   // kTfRowsMax distinct TF rows, u32 texels (valid when tf_dedup)
+  uint8_t* tf_rowmap = nullptr;  // density row -> distinct row
+  uint32_t tf_dedup = 0;
   uint32_t b_rows = 1;         // zero TF: column-invariant
   uint8_t* light = nullptr;    // 256 bytes
   float4* tf_rgb = nullptr;    // RGB sibling: decoded TF row 0 (kRgbTfMax texels)
@@ -257,6 +260,7 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
     P.light_dir[2] = ld[2] * il;
   }
   P.b_rows = h->b_rows;
+  P.tf_dedup = h->tf_dedup;
   {  // |w| bound for unproject<true>: |a|, |b| <= 1 + max(2/R, |blur|) + 1 (slop)
     const double A = 2.0 + std::max(2.0 / h->R, std::fabs((double)P.blur));
     bool fin = true;
@@ -344,7 +348,8 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
                                h->stream, eb, ee));
   else
     HIPCHK(h, launch_march(h->layout, h->variant, P, PS, T, h->photons, vol, h->tf_rg, h->tf_b4,
-                           h->tf_brow, h->light, h->rgba, h->rgb32, h->stream, eb, ee));
+                           h->tf_brow, h->light, h->rgba, h->rgb32, h->stream, eb, ee, h->tf_rows,
+                           h->tf_rowmap));
   h->sched_cur = c ^ 1u;
   return VPTMCM_OK;
 }
@@ -453,6 +458,10 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   CK(hipMemsetAsync(h->tf_b4, 0, kTfCells * kTfCells * sizeof(uint32_t), h->stream));
   CK(hipMalloc(&h->tf_brow, 256));
   CK(hipMemsetAsync(h->tf_brow, 0, 256, h->stream));
+  CK(hipMalloc(&h->tf_rows, kTfRowsMax * 256 * sizeof(uint32_t)));
+  CK(hipMemsetAsync(h->tf_rows, 0, kTfRowsMax * 256 * sizeof(uint32_t), h->stream));
+  CK(hipMalloc(&h->tf_rowmap, 256));
+  CK(hipMemsetAsync(h->tf_rowmap, 0, 256, h->stream));
   CK(hipMalloc(&h->light, 256));
   CK(hipMemsetAsync(h->light, 0, 256, h->stream));
   CK(hipMalloc(&h->tf_rgb, kRgbTfMax * sizeof(float4)));
@@ -490,6 +499,8 @@ void vptmcm_destroy(vptmcm* h) {
   if (h->tf_rg) (void)hipFree(h->tf_rg);
   if (h->tf_b4) (void)hipFree(h->tf_b4);
   if (h->tf_brow) (void)hipFree(h->tf_brow);
+  if (h->tf_rows) (void)hipFree(h->tf_rows);
+  if (h->tf_rowmap) (void)hipFree(h->tf_rowmap);
   if (h->light) (void)hipFree(h->light);
   if (h->sched) (void)hipFree(h->sched);
   if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
@@ -622,6 +633,37 @@ int vptmcm_set_material_tf(vptmcm* h, const uint8_t* rgba) {
   }
   HIPCHK(h, hipMemcpyAsync(h->tf_brow, brow, 256, hipMemcpyHostToDevice, h->stream));
   h->b_rows = inv;
+  // Distinct density rows over (albedo, alpha, anisotropy): a UI TF paints one
+  // material's wavelength arrays into every row of a density range
+  // (MaterialTransferFunction.js:56-75), so it has few; with <= kTfRowsMax of
+  // them the non-FAST marches keep all three channels in LDS (P.tf_dedup).
+  std::vector<uint32_t> rows;
+  uint8_t rowmap[256];
+  uint32_t n_rows = 0;
+  for (int r = 0; r < 256 && n_rows <= kTfRowsMax; r++) {
+    uint32_t texel[256];
+    for (int c = 0; c < 256; c++) {
+      const uint8_t* t = rgba + (r * 256 + c) * 4;
+      texel[c] = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16);
+    }
+    uint32_t k = 0;
+    while (k < n_rows && memcmp(&rows[(size_t)k * 256], texel, sizeof texel) != 0) k++;
+    if (k == n_rows) {
+      if (n_rows == kTfRowsMax) {
+        n_rows++;  // too many: no deduplicated table
+        break;
+      }
+      rows.insert(rows.end(), texel, texel + 256);
+      n_rows++;
+    }
+    rowmap[r] = (uint8_t)k;
+  }
+  h->tf_dedup = n_rows <= kTfRowsMax ? 1u : 0u;
+  if (h->tf_dedup) {
+    HIPCHK(h, hipMemcpyAsync(h->tf_rows, rows.data(), rows.size() * sizeof(uint32_t),
+                             hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->tf_rowmap, rowmap, 256, hipMemcpyHostToDevice, h->stream));
+  }
   HIPCHK(h, hipStreamSynchronize(h->stream));  // the host copies are freed on return
   return VPTMCM_OK;
 }
