@@ -380,6 +380,12 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "traffic_ratio": (round(traffic / bytes_per_launch, 2) if traffic else None),
+                         # the same PMC bytes over this run's launch time: L2-miss line
+                         # traffic (128-B fills; Infinity Cache hits included) per second
+                         "traffic_gbps": (round(traffic / (kern_avg_ms * 1e-3) / 1e9, 1)
+                                          if traffic and not a.no_timing else None),
+                         "traffic_frac": (round(traffic / (kern_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+                                          if traffic and not a.no_timing else None),
                          "issue": issue,
                          "kernel": "k_march", "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                          "passes_per_launch": ppl,
