@@ -82,6 +82,10 @@ def parse():
                          "roofline fields are then null)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="budget of the CPU-oracle baseline (0 = skip)")
+    ap.add_argument("--rgb-steps", type=int, default=256,
+                    help="passes of a timed region on the RGB sibling renderer ('mcm-compute', "
+                         "MCMComputeRenderer.wgsl) on the same volume (reported as 'rgb'; "
+                         "0 = skip; N = 1 only)")
     ap.add_argument("--general-steps", type=int, default=64,
                     help="passes of a timed region on the general (non-FAST) march: a UI-like "
                          "TF with wavelength-varying anisotropy and 8 uneven bins (reported as "
@@ -359,6 +363,43 @@ def main():
                                "8_uneven bins: a UI-like TF (row-deduplicated in LDS) and "
                                "uneven bins, march MODE 4 (MODE 2 is the headline's)"}
 
+    # The RGB sibling ('mcm-compute') on the same volume and camera:
+    # a 256 x 1 sRGB TF ramp, HG anisotropy 0.7, white 1x1 environment
+    rgb = None
+    if a.rgb_steps > 0 and not multi:
+        r.synchronize()
+        q = vptmcm.Renderer(R, device=device, layout=layout, renderer=vptmcm.RENDERER_RGB)
+        x = np.arange(256)
+        ttf = np.zeros((1, 256, 4), np.uint8)
+        ttf[0, :, 0], ttf[0, :, 1], ttf[0, :, 2] = 255 - x // 2, 128 + x // 4, x
+        ttf[0, :, 3] = np.clip((x - 40) * 2, 0, 255)
+        q.set_volume(vol)
+        q.set_transfer_function(ttf)
+        q.set_environment((255, 255, 255, 255))
+        q.set_params(extinction=a.extinction, anisotropy=0.7, bounces=8, steps=S)
+        rseeds = cf.seed_stream(a.rgb_steps + 65, start=2, rank=rank)
+        q.reset(mvp, rseeds[0])
+        for k in range(2):
+            q.render_passes(mvp, rseeds[1 + 32 * k:33 + 32 * k])
+        q.synchronize()
+        q.enable_kernel_timing(not a.no_timing)
+        t4 = time.perf_counter()
+        done = 0
+        while done < a.rgb_steps:
+            n = min(F, a.rgb_steps - done)
+            q.render_passes(mvp, rseeds[65 + done:65 + done + n])
+            done += n
+        q.synchronize()
+        el4 = time.perf_counter() - t4
+        qk_ms, _ = q.kernel_time()
+        rgb = {"value": round(R * R * S * a.rgb_steps / el4 / 1e6, 3),
+               "ms_per_step": round(el4 * 1e3 / a.rgb_steps, 5), "steps": a.rgb_steps,
+               "kernel_us_per_pass": (round(qk_ms * 1e3 / a.rgb_steps, 3)
+                                      if not a.no_timing else None),
+               "workload": "RGB sibling renderer (MCMComputeRenderer.wgsl) on the same volume and "
+                           "camera: 256x1 sRGB TF ramp, anisotropy 0.7, white environment"}
+        q.close()
+
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mphoton-steps/s",
@@ -394,6 +435,7 @@ def main():
             "unfused": unfused,
             "render_api": render_api,
             "general": general,
+            "rgb": rgb,
             "cpu_baseline": None,
             "volume_gen_s": round(gen_s, 2),
         }

@@ -69,9 +69,10 @@ hipError_t launch_tonemap_artistic(const uint16_t* rgba16, uint32_t n, const Ton
                                    uint32_t* out, hipStream_t s);
 // RGB sibling renderer (MCMComputeRenderer.wgsl): reset / march kernels.
 hipError_t launch_reset_rgb(const MarchParams& P, float* ph, hipStream_t s);
-hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSeeds& PS, float* ph,
-                            const uint8_t* vol, const float4* tf, uint16_t* rgba, float* rgb32,
-                            hipStream_t s, hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr);
+hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSeeds& PS,
+                            const TileSched& T, float* ph, const uint8_t* vol, const float4* tf,
+                            uint16_t* rgba, float* rgb32, hipStream_t s,
+                            hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr);
 hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, uint32_t BW,
                           uint32_t BH, void* out, hipStream_t s);
 hipError_t launch_pack(const MarchParams& P, const float* ph, const float* rgb32, float4* out,

@@ -873,21 +873,48 @@ __global__ __launch_bounds__(kBlock) void k_reset_rgb(const MarchParams P, float
   for (uint32_t k = 0; k < kRgbPlanes; k++) ph[k * S + i] = w[k];
 }
 
-template <uint32_t L>
+// GEO (host-checked: blur 0, even R, host-bounded |w|): every near point is the
+// fixed per-pixel one, the far point takes the one-compare reciprocal guard and,
+// when every lane's near point is slab-generic, the slab test is the hardware
+// min/max3 form (ray_start_hw) — the same proven-exact forms as k_march's FAST.
+template <bool GEO>
+__device__ __forceinline__ void rgb_reset_fast(const MarchParams& P, float sx, float sy, bool fixed,
+                                               f3 from, bool slab_hw, f3 omf, uint32_t h1,
+                                               uint32_t h2, uint32_t h3, uint32_t h4, f3& pos,
+                                               f3& dir) {
+  if constexpr (!GEO) {
+    rgb_reset_draws(P, sx, sy, fixed, from, h1, h2, h3, h4, pos, dir);
+  } else {
+    dir = ray_dir_from_draws<true>(P, sx, sy, from, h3, h4);
+    pos = slab_hw ? ray_start_hw(from, omf, dir) : ray_start(from, dir);
+  }
+}
+
+template <uint32_t L, bool GEO>
 __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, const MarchParams P,
+                                                           const TileSched T,
                                                            float* __restrict__ ph,
                                                            const uint8_t* __restrict__ vol,
                                                            const float4* __restrict__ tf,
                                                            uint16_t* __restrict__ rgba,
                                                            float* __restrict__ rgb32) {
   __shared__ float4 s_tf[kRgbTfMax];
-  const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x) * (kMarchBlock / 64) +
-                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __shared__ uint32_t s_red[17];
+  __shared__ uint32_t s_tile[16];
+  // the SIMD-balanced tile schedule and volume-wave priority of k_march
+  uint32_t tile;
+  if (P.sched == 0u) {
+    tile = __builtin_amdgcn_readfirstlane(schedule_tile(P, T.flags_in, s_red, s_tile));
+  } else {
+    tile = xcd_swizzle(blockIdx.x, gridDim.x) * (kMarchBlock / 64) +
+           __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (tile >= P.n_tiles) tile = 0xffffffffu;
+  }
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
   const uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
   const size_t i = (size_t)tile * 64u + lane;
-  const bool live = tile < P.n_tiles && x < P.R && y < P.R;
+  const bool live = tile != 0xffffffffu && x < P.R && y < P.R;
   const size_t S = P.npad;
   f3 pos{0.0f, 0.0f, 0.0f}, dir{0.0f, 0.0f, 0.0f}, tr{0.0f, 0.0f, 0.0f}, rad{0.0f, 0.0f, 0.0f};
   uint32_t bounces = 0u, samples = 0u;
@@ -907,12 +934,20 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
   screen_of(P, x, y, sx, sy);
   f3 from{0.0f, 0.0f, 0.0f};
   const bool fixed = near_fixed(P, sx, sy, from);
+  const bool slab_hw = GEO && __builtin_amdgcn_ballot_w64(!slab_generic(fixed, from)) == 0ull;
+  f3 omf{1.0f - from.x, 1.0f - from.y, 1.0f - from.z};
   const float g = P.anisotropy;
   const bool iso = __builtin_fabsf(g) < kEps;  // uniform
   const float tfw = (float)P.tf_w;
   const int tfm = (int)P.tf_w - 1;
+  bool hot = (P.sched == 0u) ? (T.flags_in[tile] != 0u) : true;
+  bool entered = false;
 
   for (uint32_t pass = 0; pass < PS.n; pass++) {
+    if (pass > 0u) hot = entered;
+    if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) __builtin_amdgcn_s_setprio(VPT_PRIO);
+    else __builtin_amdgcn_s_setprio(0);
+    entered = false;
     uint32_t st = hash3(x, y, pass_seed(pass));  // MCMComputeRenderer.wgsl:112
     for (uint32_t step = 0; step < P.steps; step++) {
       uint32_t s1 = pcg_hash(st);
@@ -928,16 +963,17 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
         float inv = rcp_in_range((float)samples);
         rad = f3{fmaf(tr.x * P.env[0] - rad.x, inv, rad.x), fmaf(tr.y * P.env[1] - rad.y, inv, rad.y),
                  fmaf(tr.z * P.env[2] - rad.z, inv, rad.z)};
-        rgb_reset_draws(P, sx, sy, fixed, from, h1, h2, h3, h4, pos, dir);
+        rgb_reset_fast<GEO>(P, sx, sy, fixed, from, slab_hw, omf, h1, h2, h3, h4, pos, dir);
         bounces = 0u;
         tr = f3{1.0f, 1.0f, 1.0f};
         st = h4;
         continue;
       }
+      entered = true;
       VolTap vt = vol_fetch<L>(P, vol, pos);  // gather in flight from here
       // speculative reset candidate (draws h1..h4) and the g-independent HG half
       f3 rpos, rdir;
-      rgb_reset_draws(P, sx, sy, fixed, from, h1, h2, h3, h4, rpos, rdir);
+      rgb_reset_fast<GEO>(P, sx, sy, fixed, from, slab_hw, omf, h1, h2, h3, h4, rpos, rdir);
       float dx, dy;
       disk_of(h1, h2, dx, dy);
       float nrm = fmaf(dy, dy, dx * dx);  // sphere.wgsl
@@ -1001,6 +1037,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
                                tr.x, tr.y, tr.z, rad.x, rad.y, rad.z};
 #pragma unroll
   for (uint32_t k = 0; k < kRgbPlanes; k++) ph[k * S + i] = w[k];
+  if (lane == 0u) T.flags_out[tile] = entered ? 1u : 0u;  // the next launch's schedule
 }
 
 // --------------------------------------------------------- volume relayout
@@ -1176,25 +1213,32 @@ hipError_t launch_reset_rgb(const MarchParams& P, float* ph, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSeeds& PS, float* ph,
-                            const uint8_t* vol, const float4* tf, uint16_t* rgba, float* rgb32,
-                            hipStream_t s, hipEvent_t ev_beg, hipEvent_t ev_end) {
+hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSeeds& PS,
+                            const TileSched& T, float* ph, const uint8_t* vol, const float4* tf,
+                            uint16_t* rgba, float* rgb32, hipStream_t s, hipEvent_t ev_beg,
+                            hipEvent_t ev_end) {
   dim3 grid(tile_blocks(P, kMarchBlock));
+  const bool geo = P.w_bounded && P.blur == 0.0f && (P.R & 1u) == 0u;
+#define VPT_LAUNCH_RGB(LAY)                                                                       \
+  do {                                                                                            \
+    if (geo)                                                                                      \
+      hipExtLaunchKernelGGL((k_march_rgb<LAY, true>), grid, dim3(kMarchBlock), 0, s, ev_beg,      \
+                            ev_end, 0, PS, P, T, ph, vol, tf, rgba, rgb32);                       \
+    else                                                                                          \
+      hipExtLaunchKernelGGL((k_march_rgb<LAY, false>), grid, dim3(kMarchBlock), 0, s, ev_beg,     \
+                            ev_end, 0, PS, P, T, ph, vol, tf, rgba, rgb32);                       \
+  } while (0)
   if (layout == kLayoutBrick8 && P.vol32)
-    hipExtLaunchKernelGGL((k_march_rgb<kTplBrick8>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end,
-                          0, PS, P, ph, vol, tf, rgba, rgb32);
+    VPT_LAUNCH_RGB(kTplBrick8);
   else if (layout == kLayoutBrick8)
-    hipExtLaunchKernelGGL((k_march_rgb<kTplBrick8Wide>), grid, dim3(kMarchBlock), 0, s, ev_beg,
-                          ev_end, 0, PS, P, ph, vol, tf, rgba, rgb32);
+    VPT_LAUNCH_RGB(kTplBrick8Wide);
   else if (layout == kLayoutCorner8 && P.vol32)
-    hipExtLaunchKernelGGL((k_march_rgb<kTplCorner8>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end,
-                          0, PS, P, ph, vol, tf, rgba, rgb32);
+    VPT_LAUNCH_RGB(kTplCorner8);
   else if (layout == kLayoutCorner8)
-    hipExtLaunchKernelGGL((k_march_rgb<kTplCorner8Wide>), grid, dim3(kMarchBlock), 0, s, ev_beg,
-                          ev_end, 0, PS, P, ph, vol, tf, rgba, rgb32);
+    VPT_LAUNCH_RGB(kTplCorner8Wide);
   else
-    hipExtLaunchKernelGGL((k_march_rgb<kTplLinear>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end,
-                          0, PS, P, ph, vol, tf, rgba, rgb32);
+    VPT_LAUNCH_RGB(kTplLinear);
+#undef VPT_LAUNCH_RGB
   return hipGetLastError();
 }
 

@@ -344,7 +344,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf};
   P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : 0u;
   if (h->kind == VPTMCM_RENDERER_RGB)
-    HIPCHK(h, launch_march_rgb(h->layout, P, PS, h->photons, vol, h->tf_rgb, h->rgba, h->rgb32,
+    HIPCHK(h, launch_march_rgb(h->layout, P, PS, T, h->photons, vol, h->tf_rgb, h->rgba, h->rgb32,
                                h->stream, eb, ee));
   else
     HIPCHK(h, launch_march(h->layout, h->variant, P, PS, T, h->photons, vol, h->tf_rg, h->tf_b4,
