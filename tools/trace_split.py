@@ -11,7 +11,7 @@ import sys
 
 
 def main():
-    rows = [r for r in csv.DictReader(open(sys.argv[1])) if "k_march" in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(sys.argv[1])) if "k_march<" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
     # bench order: 1 warm-up launch (16 passes), K/16 timed fused launches, then
