@@ -422,6 +422,9 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
       return fail(VPTMCM_EINVAL);
     }
     h->device = cfg->device;
+    // VPTMCM_SYNC_SPIN=1 (analysis): host waits spin instead of yielding
+    if (const char* v = getenv("VPTMCM_SYNC_SPIN"))
+      if (v[0] == '1') (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
     if (hipSetDevice(h->device) != hipSuccess) {
       h->err = "vptmcm_create: hipSetDevice failed";
       return fail(VPTMCM_EHIP);

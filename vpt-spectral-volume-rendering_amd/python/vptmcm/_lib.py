@@ -91,8 +91,9 @@ def load() -> C.CDLL:
         "vptmcm_set_spectrum": (C.c_int, [vp, f32p]),
         "vptmcm_set_params": (C.c_int, [vp, C.POINTER(Params)]),
         "vptmcm_reset": (C.c_int, [vp, f32p, C.c_uint32]),
-        "vptmcm_render": (C.c_int, [vp, f32p, C.c_uint32]),
-        "vptmcm_render_passes": (C.c_int, [vp, f32p, u32p, C.c_uint32]),
+        # the per-pass calls take raw addresses (c_void_p): no ctypes pointer objects
+        "vptmcm_render": (C.c_int, [vp, vp, C.c_uint32]),
+        "vptmcm_render_passes": (C.c_int, [vp, vp, vp, C.c_uint32]),
         "vptmcm_synchronize": (C.c_int, [vp]),
         "vptmcm_read_rgba16f": (C.c_int, [vp, vp]),
         "vptmcm_read_rgb": (C.c_int, [vp, vp]),
@@ -224,12 +225,12 @@ class Renderer:
 
     def render(self, mvp, seed_bits: int) -> None:
         m = mat_f32(mvp)
-        self._ck(self.L.vptmcm_render(self.h, _f32p(m), int(seed_bits) & 0xFFFFFFFF))
+        self._ck(self.L.vptmcm_render(self.h, m.ctypes.data, int(seed_bits) & 0xFFFFFFFF))
 
     def render_passes(self, mvp, seeds) -> None:
         m = mat_f32(mvp)
         s = np.ascontiguousarray(seeds, dtype=np.uint32)
-        self._ck(self.L.vptmcm_render_passes(self.h, _f32p(m), _u32p(s), s.size))
+        self._ck(self.L.vptmcm_render_passes(self.h, m.ctypes.data, s.ctypes.data, s.size))
 
     def synchronize(self) -> None:
         self._ck(self.L.vptmcm_synchronize(self.h))
