@@ -70,6 +70,10 @@ def parse():
                          "per render() call")
     ap.add_argument("--allreduce-every", type=int, default=32,
                     help="passes between radiance all-reduces (N > 1)")
+    ap.add_argument("--per-pass-steps", type=int, default=64,
+                    help="N > 1: passes of a second timed region compositing after EVERY pass "
+                         "(north_star's 'all-reduce each progressive pass'; one launch per pass; "
+                         "reported as 'per_pass_allreduce'; 0 = skip)")
     ap.add_argument("--unfused-steps", type=int, default=64,
                     help="passes of a second timed region at one launch per pass (reported "
                          "as 'unfused'; 0 = skip; N = 1 only)")
@@ -186,7 +190,8 @@ def main():
 
     n_unfused = a.unfused_steps if not multi else 0
     n_api = a.api_steps if not multi else 0
-    seeds = cf.seed_stream(a.warmup + a.steps + n_unfused + n_api + 1, start=0, rank=rank)
+    n_pp = a.per_pass_steps if multi else 0
+    seeds = cf.seed_stream(a.warmup + a.steps + n_unfused + n_api + n_pp + 1, start=0, rank=rank)
     F = max(1, min(a.fuse, 32))
     every = max(1, a.allreduce_every)
 
@@ -199,7 +204,7 @@ def main():
             done += n
         return launches
 
-    def passes(first: int, count: int, F: int = F) -> list:
+    def passes(first: int, count: int, F: int = F, every: int = every) -> list:
         """Enqueue `count` passes from seeds[first:] in launches of <= F passes,
         compositing across ranks whenever `every` passes have completed and
         after the region's last pass (so every region ends with a composite
@@ -267,6 +272,24 @@ def main():
 
     # the same workload at one launch per render() call (photon state stored and
     # reloaded every pass), continuing the pass sequence; N = 1 only
+    # N > 1: the same march compositing after every pass (one launch + one RCCL
+    # all-reduce of the (rgb*n, n) buffer per pass), bracketed like the main region
+    per_pass = None
+    if n_pp > 0:
+        r.synchronize()
+        r.barrier()
+        t5 = time.perf_counter()
+        passes(1 + a.warmup + a.steps, n_pp, F=1, every=1)
+        r.synchronize()
+        r.read_composite()
+        el5 = time.perf_counter() - t5
+        r.barrier()
+        el5 = float(r.allreduce_host(np.array([el5, 0.0]), op="max")[0])
+        per_pass = {"value": round(world * R * R * S * n_pp / el5 / 1e6, 3),
+                    "ms_per_step": round(el5 * 1e3 / n_pp, 5), "steps": n_pp,
+                    "note": "one march launch and one RCCL all-reduce of the R^2 float4 "
+                            "(rgb*n, n) buffer per pass (north_star's per-pass composite)"}
+
     unfused = None
     if n_unfused > 0:
         r.synchronize()
@@ -436,6 +459,7 @@ def main():
             "render_api": render_api,
             "general": general,
             "rgb": rgb,
+            "per_pass_allreduce": per_pass,
             "cpu_baseline": None,
             "volume_gen_s": round(gen_s, 2),
         }

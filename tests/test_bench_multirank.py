@@ -94,17 +94,24 @@ def test_bench_two_ranks_driver_command_line(tmp_path):
     rec = json.loads(line[0])
     assert rec["n_gpus"] == 2 and rec["steps"] == 20 and rec["warmup"] == 5
     assert rec["value"] > 0 and rec["config"]["workload"].startswith("C4")
+    assert rec["per_pass_allreduce"]["steps"] == 64 and rec["per_pass_allreduce"]["value"] > 0
     logs = [json.loads((tmp_path / f"log{r}.json").read_text()) for r in (0, 1)]
     uids = {e[1] for lg in logs for e in lg if e[0] == "comm_init"}
     assert len(uids) == 1, "ranks must share rank 0's unique id"
     for r, lg in enumerate(logs):
         assert ["create", 16, r, 1] in lg  # one GPU per local rank
         t = [e[0] for e in lg].index("timing")
-        timed = lg[t + 1:]
+        after = lg[t + 1:]
+        c1 = [e[0] for e in after].index("composite")
+        timed, rest = after[:c1 + 1], after[c1 + 1:]  # the main region, then the per-pass one
         kinds = [e[0] for e in timed]
         assert sum(len(e[1]) for e in timed if e[0] == "passes") == 20
         last_pass = max(i for i, k in enumerate(kinds) if k == "passes")
         assert "allreduce" in kinds[last_pass:], "timed region must end with a composite"
         assert kinds.index("composite") > last_pass
+        # per-pass compositing region: 64 one-pass launches, each followed by an all-reduce
+        rk = [e[0] for e in rest if e[0] in ("passes", "allreduce")]
+        assert rk[:128] == ["passes", "allreduce"] * 64
+        assert all(len(e[1]) == 1 for e in rest if e[0] == "passes")
     seeds = [[s for e in lg if e[0] == "passes" for s in e[1]] for lg in logs]
     assert not set(seeds[0]) & set(seeds[1]), "ranks must use distinct seed streams"
