@@ -84,3 +84,35 @@ def test_rgb_environment_and_tf_validation():
         s.set_transfer_function(np.zeros((1, 4, 4), np.uint8))
     g.close()
     s.close()
+
+
+@pytest.mark.parametrize("camera", ["default", "near", "orbit_tilted"])
+def test_rgb_fused_schedule_robust(camera):
+    """Fused multi-pass launches of the RGB march at R = 128: the tile schedule
+    (volume flags carried between launches), the volume-wave priority, the
+    robust-miss path (start points materialised at the end of the launch) and
+    the FAST geometry, bit-exact against the oracle after every launch."""
+    R = 128
+    vol = cf.fbm_volume(64, 21)
+    gpu = vptmcm.Renderer(R, device=0, renderer=vptmcm.RENDERER_RGB)
+    cpu = orc.OracleRGB(R)
+    tf = tf_rgb("ramp")
+    gpu.set_transfer_function(tf)
+    gpu.set_environment((255, 230, 200, 255))
+    gpu.set_volume(vol)
+    gpu.set_params(extinction=24.0, anisotropy=0.7, bounces=8, steps=8)
+    cpu.volume, cpu.tf, cpu.env = vol, tf, np.array((255, 230, 200, 255), np.uint8)
+    cpu.params.update(extinction=24.0, anisotropy=0.7, bounces=8, steps=8)
+    mvp = cf.default_mvp_inverse() if camera == "default" else cf.golden_mvp(camera)
+    seeds = cf.seed_stream(13, start=70)
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0])
+    for launch in range(3):
+        ss = seeds[1 + 4 * launch:5 + 4 * launch]
+        gpu.render_passes(mvp, ss)
+        for s in ss:
+            _, want = cpu.render(mvp, s)
+        ok = same_words(gpu.read_photons(), cpu.photons)
+        assert ok.all(), f"{camera} launch {launch}: {int((~ok).sum())} photon words differ"
+        assert np.array_equal(gpu.read_rgba16f(), want), f"{camera} launch {launch}: image"
+    gpu.close()

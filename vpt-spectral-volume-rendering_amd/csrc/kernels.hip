@@ -942,6 +942,11 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
   const int tfm = (int)P.tf_w - 1;
   bool hot = (P.sched == 0u) ? (T.flags_in[tile] != 0u) : true;
   bool entered = false;
+  // robust-miss pixels, as in k_march: once reset with this launch's matrix
+  // their rays miss the cube by a margin, so every later step is an exit
+  const bool rbpix = P.robust != 0u && fixed &&
+                     (sx < P.rb_x0 || sx > P.rb_x1 || sy < P.rb_y0 || sy > P.rb_y1);
+  bool rb = false, stale = false;
 
   for (uint32_t pass = 0; pass < PS.n; pass++) {
     if (pass > 0u) hot = entered;
@@ -950,6 +955,24 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
     entered = false;
     uint32_t st = hash3(x, y, pass_seed(pass));  // MCMComputeRenderer.wgsl:112
     for (uint32_t step = 0; step < P.steps; step++) {
+      if (__builtin_amdgcn_ballot_w64(!rb) == 0ull) {
+        // robust path: the exit and the reset of wgsl:126-139 without the
+        // distance (it only moves the photon along a ray that misses the cube)
+        // and without the slab test (the start point is materialised once, at
+        // the end of the launch)
+        uint32_t h1 = pcg_hash(pcg_hash(pcg_hash(st)));
+        uint32_t h2 = pcg_hash(h1), h3 = pcg_hash(h2), h4 = pcg_hash(h3);
+        samples++;
+        float inv = rcp_in_range((float)samples);
+        rad = f3{fmaf(tr.x * P.env[0] - rad.x, inv, rad.x), fmaf(tr.y * P.env[1] - rad.y, inv, rad.y),
+                 fmaf(tr.z * P.env[2] - rad.z, inv, rad.z)};
+        dir = ray_dir_from_draws<GEO>(P, sx, sy, from, h3, h4);
+        bounces = 0u;
+        tr = f3{1.0f, 1.0f, 1.0f};
+        st = h4;
+        stale = true;
+        continue;
+      }
       uint32_t s1 = pcg_hash(st);
       float dist = -spec_log_unit(s1) * P.rcp_extinction;  // exponential.wgsl
       pos = f3{fmaf(dist, dir.x, pos.x), fmaf(dist, dir.y, pos.y), fmaf(dist, dir.z, pos.z)};
@@ -967,6 +990,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
         bounces = 0u;
         tr = f3{1.0f, 1.0f, 1.0f};
         st = h4;
+        rb = rbpix;
         continue;
       }
       entered = true;
@@ -1002,6 +1026,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
         bounces = 0u;
         tr = f3{1.0f, 1.0f, 1.0f};
         st = h4;
+        rb = rbpix;
       } else if (wheel < pabs + pscat) {  // scattering (wgsl:140-144)
         tr = f3{tr.x * cr, tr.y * cg, tr.z * cb};
         if (iso) {
@@ -1033,6 +1058,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
       o[2] = rad.z;
     }
   }
+  if (stale) pos = ray_start(from, dir);  // the last robust reset's start point
   const float w[kRgbPlanes] = {pos.x, pos.y, pos.z, dir.x, dir.y, dir.z, as_f(bounces), as_f(samples),
                                tr.x, tr.y, tr.z, rad.x, rad.y, rad.z};
 #pragma unroll
