@@ -181,13 +181,21 @@ def test_edge_cases():
         gpu.close()
 
 
-def test_first_reset_quirk_and_spectrum_change():
-    """reset() before the first spectrum upload, then renders with it."""
-    gpu, cpu = make_pair(32, cf.sphere_in_cube(32), cf.tf_spectral(), upload_spectrum=False)
+@pytest.mark.parametrize("tfname", ["spectral", "materials"])
+def test_first_reset_quirk_and_spectrum_change(tfname):
+    """reset() before the first spectrum upload, a C-ABI render with
+    no bins at all (nb = 0: every specialisation, incl. the deduplicated-TF
+    MODE 4, leaves the bins untouched), then renders with 12 and 6 bins."""
+    tf = cf.tf_spectral() if tfname == "spectral" else cf.tf_materials(True)
+    gpu, cpu = make_pair(32, cf.sphere_in_cube(32), tf, upload_spectrum=False)
     mvp = cf.default_mvp_inverse()
     gpu.reset(mvp, cf.seed_bits(0))
     cpu.reset(mvp, cf.seed_bits(0))
     assert_photons_equal(gpu.read_photons(), cpu.photons, "zero-spectrum reset")
+    gpu.render(mvp, cf.seed_bits(9))
+    _, want = cpu.render(mvp, cf.seed_bits(9))
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "zero-spectrum render")
+    assert_rgba_equal(gpu.read_rgba16f(), want, "zero-spectrum render")
     for k, spec in [(1, "12"), (2, "12"), (3, "6"), (4, "6")]:
         buf = cf.spectrum_buffer(spec)
         gpu.set_spectrum(buf)
