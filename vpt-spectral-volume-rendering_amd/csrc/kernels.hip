@@ -9,24 +9,6 @@
 //   k_debug_eval  spec-math primitives, for device-vs-oracle parity tests
 #include "kernels.h"
 
-#ifndef VPT_PK_RAD
-#define VPT_PK_RAD 0  // 1: packed (v_pk_*) 12-bin radiance update (measured 5 % slower)
-#endif
-#ifndef VPT_BF_PEND
-#define VPT_BF_PEND 1  // branch-free deferred radiance update
-#endif
-#ifndef VPT_ROBUST
-#define VPT_ROBUST 1  // robust-miss background path
-#endif
-#ifndef VPT_OH_PEND
-#define VPT_OH_PEND 1  // byte one-hot pending bin, zero-weight apply
-#endif
-#ifndef VPT_PIN_PEND
-#define VPT_PIN_PEND 1  // pin the deferred radiance update before the gather wait
-#endif
-#ifndef VPT_SLAB_HW
-#define VPT_SLAB_HW 1  // hardware min/max slab test for generic fixed near points
-#endif
 #ifndef VPT_NB_ZERO
 #define VPT_NB_ZERO 1  // nb < 12: unguarded 12-bin loops over zeroed unused bins
 #endif
@@ -220,28 +202,17 @@ __device__ __forceinline__ float exit_radiance(const MarchParams& P, f3 dir, con
 }
 
 // PhotonSpectral_add_radiance (wgsl:292-302) with 1/samples precomputed:
-// rad[b] += (target - rad[b]) * inv_n over the first nb bins. NBF (nb >= 12)
-// drops the per-bin guards and pairs the bins into packed f32 operations
-// (v_pk_add/v_pk_mul round each half exactly like the scalar forms).
+// rad[b] += (target - rad[b]) * inv_n over the first nb bins (the plain step
+// loop; the speculative one defers it, see apply_pending). NBF (nb >= 12)
+// drops the per-bin guards. (A packed v_pk_fma pairing measured 5 % slower.)
 template <bool NBF>
 __device__ __forceinline__ void add_radiance(const MarchParams& P, float* rad, float inv_n,
                                              uint32_t bin, float l) {
-  if constexpr (NBF && !VPT_PK_RAD) {
+  if constexpr (NBF) {
 #pragma unroll
     for (int b = 0; b < kMaxBins; b++) {
       float tgt = ((uint32_t)b == bin) ? l : 0.0f;
       rad[b] = fmaf(tgt - rad[b], inv_n, rad[b]);
-    }
-  } else if constexpr (NBF) {
-    typedef float v2f __attribute__((ext_vector_type(2)));
-#pragma unroll
-    for (int b = 0; b < kMaxBins; b += 2) {
-      v2f r = {rad[b], rad[b + 1]};
-      v2f t = {((uint32_t)b == bin) ? l : 0.0f, ((uint32_t)b + 1u == bin) ? l : 0.0f};
-      v2f n = {inv_n, inv_n};
-      r = v2f{fmaf(t.x - r.x, n.x, r.x), fmaf(t.y - r.y, n.y, r.y)};
-      rad[b] = r.x;
-      rad[b + 1] = r.y;
     }
   } else {
 #pragma unroll
@@ -446,11 +417,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   f3 from{0.0f, 0.0f, 0.0f};
   bool fixed = near_fixed(P, sx, sy, from);
   WaveConst wc = wave_const(p.lambda, s_light);
-#if VPT_SLAB_HW
   const bool slab_hw = __builtin_amdgcn_ballot_w64(!slab_generic(fixed, from)) == 0ull;
-#else
-  const bool slab_hw = false;
-#endif
   // 1 - from, kept in VGPRs for the whole launch (the backend would otherwise
   // recompute it in every step's reset candidate)
   f3 omf{1.0f - from.x, 1.0f - from.y, 1.0f - from.z};
@@ -461,7 +428,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   // VALU issue arbitration over background waves, which have slack.
   bool hot = (P.sched == 0u) ? (T.flags_in[tile] != 0u) : true;
 #endif
-#if VPT_ROBUST
   // Robust-miss pixels (MarchParams::robust): once such a lane has been reset
   // with this launch's matrix its ray misses the cube by a margin, so every
   // later step of the launch is an exit whatever the distance drawn; a wave
@@ -471,7 +437,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   const bool rbpix = P.robust != 0u && fixed &&
                      (sx < P.rb_x0 || sx > P.rb_x1 || sy < P.rb_y0 || sy > P.rb_y1);
   bool rb = false, stale = false;
-#endif
   const uint32_t n_passes = PS.n;
   for (uint32_t pass = 0; pass < n_passes; pass++) {
 #if VPT_PRIO
@@ -486,7 +451,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     // add_radiance of a termination is deferred into the next step's gather
     // shadow (it only touches the radiance bins, applied in the same order).
     float pend_n = 0.0f, pend_l = 0.0f;
-#if VPT_OH_PEND
     // The pending bin as a byte one-hot: byte (bin & 3) of word bin >> 2 is 1,
     // so each bin's 0/1 factor is one v_cvt_f32_ubyteN (no per-bin compare
     // masks held in SGPRs). 0xffffffff (no bins) sets no byte.
@@ -499,16 +463,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       pend_oh[1] = wi == 1u ? one : 0u;
       pend_oh[2] = wi == 2u ? one : 0u;
     };
-#else
-    uint32_t pend_bin = 0u;
-    auto set_pending = [&](float n, float l, uint32_t bin) {
-      pend_n = n;
-      pend_l = l;
-      pend_bin = bin;
-    };
-#endif
     auto apply_pending = [&]() {
-#if VPT_OH_PEND
       // Branch-free with a zero weight for lanes without a pending sample:
       // fma(d, +0, r) == r for every finite r, and the radiance bins are
       // finite in every state the march produces (convex combinations of
@@ -526,28 +481,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       }
       pend_n = 0.0f;
       pend_oh[0] = pend_oh[1] = pend_oh[2] = 0u;
-#elif VPT_BF_PEND
-      // Branch-free: every lane runs the update and lanes without a pending
-      // sample keep their old bins through one shared select per bin (no
-      // exec-mask split, no phi copies). pend_n is a sample count >= 1, so
-      // the guard-free reciprocal is exact (rcp_in_range).
-      const bool on = pend_n != 0.0f;
-      const float inv = rcp_in_range(on ? pend_n : 1.0f);
-#pragma unroll
-      for (int b = 0; b < kMaxBins; b++) {
-        if (NBF || (uint32_t)b < P.nb) {
-          float tgt = ((uint32_t)b == pend_bin) ? pend_l : 0.0f;
-          float nv = fmaf(tgt - p.rad[b], inv, p.rad[b]);
-          p.rad[b] = on ? nv : p.rad[b];
-        }
-      }
-      pend_n = 0.0f;
-#else
-      if (pend_n != 0.0f) {
-        add_radiance<NBF>(P, p.rad, rcp(pend_n), pend_bin, pend_l);
-        pend_n = 0.0f;
-      }
-#endif
     };
     // exit or absorption: count the sample, defer its radiance, adopt the
     // reset candidate (drawn from h1..h5) and continue from state h5
@@ -559,15 +492,12 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       p.bounces = 0u;
       p.lambda = rc.lambda;
       p.bin = rc.bin;
-#if VPT_ROBUST
       rb = rbpix;
-#endif
     };
     for (uint32_t step = 0; step < P.steps; step++) {
 #if VPT_STAMP
       t_prev = (uint32_t)__builtin_amdgcn_s_memtime();
 #endif
-#if VPT_ROBUST
       if (__builtin_amdgcn_ballot_w64(!rb) == 0ull) {
         // Robust path: the exit of wgsl:142-150 and the reset, minus what a
         // certain exit does not need (the distance only moves the photon
@@ -589,7 +519,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         STAMP_AT(5);
         continue;
       }
-#endif
       // distance + wheel draws (exponential.wgsl, wgsl:124-125, :141)
       uint32_t s1 = pcg_hash(st);
       float dist = -spec_log_unit(s1) * P.rcp_extinction;
@@ -631,13 +560,11 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       STAMP_AT(0);
       const VolTap vt = vol_fetch<L>(P, vol, p.pos);  // gather in flight from here
       apply_pending();
-#if VPT_PIN_PEND
       // keep the update here, in the gather's shadow (the backend otherwise
       // sinks it past the decision, after the wait)
       asm volatile("" : "+v"(p.rad[0]), "+v"(p.rad[1]), "+v"(p.rad[2]), "+v"(p.rad[3]),
                    "+v"(p.rad[4]), "+v"(p.rad[5]), "+v"(p.rad[6]), "+v"(p.rad[7]),
                    "+v"(p.rad[8]), "+v"(p.rad[9]), "+v"(p.rad[10]), "+v"(p.rad[11]));
-#endif
 
       // Speculative candidates, all derived from the state after the wheel
       // draw and independent of the gather: the reset (draws h1..h5) and the
@@ -810,9 +737,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   }
   }  // pass
 
-#if VPT_ROBUST
   if (stale) p.pos = ray_start(from, p.dir);  // the last robust reset's start point
-#endif
   store_state(ph, S, i, p);  // uPhotons[globalIndex] = p (wgsl:165), once per launch
 #pragma unroll
   for (int b = 0; b < kMaxBins; b++)
