@@ -60,6 +60,10 @@ struct MarchParams {
   uint32_t steps;
   uint32_t nb;           // u32(spectrum[0] + 0.5)
   uint32_t bins_sorted;  // lam[1..nb-1] non-decreasing: branchless bin search valid
+  // sorted, every boundary and max - min finite: the count runs over 11
+  // boundaries unrolled, with lam_pad[i] = +inf for i >= nb (no trip loop)
+  uint32_t bins_padded;
+  float lam_pad[kMaxBins];
   uint32_t bins_uniform; // lam[i] == fma(f32(i), bin_w, lam[0]) exactly: arithmetic bin
   float bin_w, rcp_bin_w;
   float lam[13];         // spectrum[1 .. 13]: bin boundaries
@@ -180,7 +184,12 @@ __device__ __forceinline__ uint32_t bin_of(const MarchParams& P, float lambda) {
     const bool up = !(lambda < hi) & (k + 1 < (int)P.nb) & !dn;
     return (uint32_t)(k - (int)dn + (int)up);
   }
-  if (P.bins_sorted) {
+  if (P.bins_sorted && P.bins_padded) {
+    // every lambda is finite here, so !(lambda < +inf) adds nothing past nb - 1
+    bin = 0u;
+#pragma unroll
+    for (int i = 1; i < kMaxBins; i++) bin += !(lambda < P.lam_pad[i]) ? 1u : 0u;
+  } else if (P.bins_sorted) {
     // uniform trip count (nb - 1): no per-bin masks held live across the
     // march (they used to spill 22 SGPRs into VGPR lanes)
     bin = 0u;

@@ -228,6 +228,16 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
     if (!(s[1 + i] <= s[2 + i])) P.bins_sorted = 0u;  // lam[i] <= lam[i+1], NaN-safe
   P.min_lam = s[1];
   P.max_lam = s[nb + 1];
+  P.bins_padded = 0u;
+  if (P.bins_sorted && nb >= 1u && nb <= (uint32_t)kMaxBins) {
+    bool fin = std::isfinite(P.max_lam - P.min_lam);
+    for (uint32_t i = 0; i <= nb; i++) fin = fin && std::isfinite(s[1 + i]);
+    if (fin) {
+      P.bins_padded = 1u;
+      for (uint32_t i = 0; i < (uint32_t)kMaxBins; i++)
+        P.lam_pad[i] = (i >= 1u && i < nb) ? s[1 + i] : INFINITY;
+    }
+  }
   // Equal-width bins (the reference default, 12 x 25 nm from 400 nm) take the
   // arithmetic bin search of bin_of(); see its comment for the conditions.
   P.bins_uniform = 0u;
