@@ -14,7 +14,10 @@ const V = require(path.join(ROOT, 'vpt-spectral-volume-rendering_amd', 'js'));
   const out = process.argv[3];
   const cie = JSON.parse(fs.readFileSync(path.join(ROOT, 'tests', 'golden', 'cie1931.json')));
   let k = 0;
-  const random = () => c.seeds[k++];  // Math.random() stand-in: exact f32 values
+  const random = () => {  // Math.random() stand-in: exact f32 values
+    if (k >= c.seeds.length) throw new Error('seed stream exhausted');
+    return c.seeds[k++];
+  };
 
   const rgb = c.renderer === 'mcm-compute';
   const env = rgb && c.env ? { width: 1, height: 1, data: Uint8Array.from(c.env) } : null;
@@ -32,6 +35,20 @@ const V = require(path.join(ROOT, 'vpt-spectral-volume-rendering_amd', 'js'));
     renderer.setMaterialTransferFunction(new Uint8Array(fs.readFileSync(c.tf_path)), false);
   }
 
+  if (c.ui) {  // the headless UI models drive the renderer's inputs (js/ui.js)
+    const tf = new V.MaterialTransferFunctionModel();
+    for (const m of c.ui.materials) {
+      const mat = tf.addMaterial(m.albedo, m.alpha, m.anisotropy);
+      tf.paint(m.rows[0], m.rows[1], mat.id);
+    }
+    const sr = new V.SpectrumRepresentationModel(c.ui.n_bins, c.ui.k);
+    const le = new V.LightEditorModel();
+    if (c.ui.direction) le.direction = c.ui.direction;
+    V.connectUiModels(renderer, { lightEditor: le, spectrumRepresentation: sr,
+      materialTransferFunction: tf });  // each change resets, like the reference (js:116-125)
+    fs.writeFileSync(path.join(out, 'spectrum.bin'), Buffer.from(renderer.spectrumBuffer().buffer));
+    fs.writeFileSync(path.join(out, 'tf_used.bin'), Buffer.from(tf.value.buffer));
+  }
   const reader = c.bvp_path
     ? new (V.ReaderFactory('bvp'))(new V.FileLoader(c.bvp_path))   // bricked archive, many placements
     : new V.RAWReader(new V.FileLoader(c.volume_path), { width: c.W, height: c.H, depth: c.D });

@@ -34,6 +34,72 @@ test('spectrum buffers equal the reference compute_spectral_coefficients', () =>
     /12/);
 });
 
+test('UI models: material TF painting (MaterialTransferFunction.js semantics)', () => {
+  const m = new V.MaterialTransferFunctionModel();
+  assert.strictEqual(m.materials.length, 1);
+  assert.ok(m.materials[0].albedo.every(v => v === 127), 'default material is 127 everywhere');
+  assert.ok(m.value.every(v => v === 0), 'the TF starts empty');
+  let changes = 0;
+  m.addEventListener('change', () => changes++);
+  const col = Uint8Array.from({ length: 256 }, (_, c) => (60 + c * 0.7) | 0);
+  const a = m.addMaterial(180, 60, col);
+  m.paint(90, 20, a.id);  // reversed range, rows 20..90
+  assert.strictEqual(changes, 1);
+  const tx = (r, c) => Array.from(m.value.subarray((r * 256 + c) * 4, (r * 256 + c) * 4 + 4));
+  assert.deepStrictEqual(tx(20, 0), [180, 60, 60, 0]);
+  assert.deepStrictEqual(tx(90, 255), [180, 60, col[255], 0]);
+  assert.deepStrictEqual(tx(19, 7), [0, 0, 0, 0]);
+  assert.deepStrictEqual(tx(91, 7), [0, 0, 0, 0]);
+  m.paint(50, 60, a.id, true);  // erase
+  assert.deepStrictEqual(tx(55, 3), [0, 0, 0, 0]);
+  assert.deepStrictEqual(tx(49, 3), [180, 60, col[3], 0]);
+  m.paint(-5, 300, m.materials[0].id);  // clamped to the canvas
+  assert.deepStrictEqual(tx(0, 0), [127, 127, 127, 0]);
+  assert.deepStrictEqual(tx(255, 255), [127, 127, 127, 0]);
+  assert.strictEqual(m.removeMaterial(a.id), true);
+  assert.strictEqual(m.removeMaterial(m.materials[0].id), false, 'the last material stays');
+});
+
+test('UI models: spectrum markers (SpectrumRepresentation.js semantics)', () => {
+  const s = new V.SpectrumRepresentationModel();
+  // the default (12 bins, k = 0) is the renderer's default bin layout (js:79)
+  assert.deepStrictEqual(s.getBins(), gold('spectrum_buffers.json').layouts['12'].bins);
+  s.arrange(0, 6);
+  assert.deepStrictEqual(s.getBins(), gold('spectrum_buffers.json').layouts['6'].bins);
+  s.arrange(2, 8);  // exponential spacing: denser at the blue end, whole nm, sorted
+  const b = s.getBins();
+  assert.strictEqual(b.length, 9);
+  assert.strictEqual(b[0], 400);
+  assert.strictEqual(b[8], 700);
+  for (let i = 1; i < 9; i++) assert.ok(b[i] > b[i - 1]);
+  for (let i = 2; i < 9; i++) assert.ok(b[i] - b[i - 1] >= b[i - 1] - b[i - 2] - 1);
+  const x3 = (Math.exp(2 * 3 / 8) - 1) / (Math.exp(2) - 1);
+  assert.strictEqual(b[3], Math.round(400 + 300 * x3));
+  s.moveMarker(8, 1.7);  // clamped to the track
+  assert.strictEqual(s.getBins()[8], 700);
+  s.moveMarker(0, 0.5);  // crossing markers are re-sorted
+  const c = s.getBins();
+  assert.ok(c.every((v, i) => i === 0 || v >= c[i - 1]));
+});
+
+test('UI models drive a renderer like the element listeners', () => {
+  const calls = [];
+  const fake = {
+    setLight: (spd, dir) => calls.push(['light', spd[0], Array.from(dir)]),
+    setSpectrumRepresentation: bins => calls.push(['bins', bins.length]),
+    setMaterialTransferFunction: v => calls.push(['tf', v.length]),
+  };
+  const le = new V.LightEditorModel(), sr = new V.SpectrumRepresentationModel(),
+    tf = new V.MaterialTransferFunctionModel();
+  V.connectUiModels(fake, { lightEditor: le, spectrumRepresentation: sr, materialTransferFunction: tf });
+  assert.deepStrictEqual(calls, [['light', 100, [1, 0, 0]], ['bins', 13], ['tf', 262144]]);
+  le.setDirection([0, 1, 0]);
+  sr.arrange(0, 3);
+  tf.paint(0, 10);
+  assert.deepStrictEqual(calls.slice(3), [['light', 100, [0, 1, 0]], ['bins', 4], ['tf', 262144]]);
+  assert.throws(() => le.setSpectrum(new Uint8Array(10)), /256/);
+});
+
 test('property bag + change events', () => {
   const bag = new V.PropertyBag();
   bag.registerProperties([{ name: 'extinction', value: 1 }, { name: 'steps', value: 8 }]);

@@ -22,15 +22,15 @@ ROOT = Path(__file__).resolve().parents[1]
 
 
 def run_case(tmp_path, vol, tf, R=64, passes=3, ext=32.0, layout="corner8", stream=True,
-             change_event=False, tonemap=None, bvp=None):
+             change_event=False, tonemap=None, bvp=None, ui=None):
     D, H, W = vol.shape
     (tmp_path / "vol.raw").write_bytes(np.ascontiguousarray(vol).tobytes())
     (tmp_path / "tf.bin").write_bytes(np.ascontiguousarray(tf).tobytes())
-    seeds = [float(np.uint32(cf.seed_bits(k)).view(np.float32)) for k in range(passes + 2)]
+    seeds = [float(np.uint32(cf.seed_bits(k)).view(np.float32)) for k in range(passes + 6)]
     case = dict(R=R, passes=passes, extinction=ext, bounces=8, steps=8, layout=layout,
                 W=W, H=H, D=D, volume_path=str(tmp_path / "vol.raw"), tf_path=str(tmp_path / "tf.bin"),
                 seeds=seeds, stream_volume=stream, change_event=change_event, tonemap=tonemap,
-                bvp_path=None)
+                bvp_path=None, ui=ui)
     if bvp is not None:
         (tmp_path / "vol.bvp").write_bytes(bvp)
         case["bvp_path"] = str(tmp_path / "vol.bvp")
@@ -146,4 +146,39 @@ def test_js_rgb_renderer_bitexact(tmp_path):
     for k in range(3):
         _, want = o.render(mvp, bits(seeds[1 + k]))
     assert same(ph, o.photons)
+    assert np.array_equal(rgba, want)
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+def test_js_ui_models_drive_renderer_bitexact(tmp_path):
+    """The headless UI models (js/ui.js: MaterialTransferFunction, SpectrumRepresentation
+    with exponential markers, LightEditor) wired to the renderer: every model change resets
+    (js:116-125), the first render uploads their spectrum; the materials TF has few distinct
+    rows and 8 uneven bins, so the march runs its deduplicated-TF MODE 4. Bit-exact vs the
+    oracle replaying the same inputs."""
+    col = list(range(60, 60 + 256))
+    ui = {"materials": [{"albedo": 180, "alpha": 60, "anisotropy": 127, "rows": [20, 89]},
+                        {"albedo": 150, "alpha": 140, "anisotropy": 200, "rows": [90, 169]},
+                        {"albedo": 230, "alpha": 230, "anisotropy": [min(255, v) for v in col],
+                         "rows": [170, 255]}],
+          "n_bins": 8, "k": 1.5, "direction": [0.6, 0.8, 0.0]}
+    vol = cf.fbm_volume(64, 5, nthreads=8)
+    R, passes = 64, 3
+    ph, rgba, seeds, used = run_case(tmp_path, vol, cf.tf_zero(), R=R, passes=passes, ui=ui)
+    spec = np.frombuffer((tmp_path / "spectrum.bin").read_bytes(), np.float32)
+    tf = np.frombuffer((tmp_path / "tf_used.bin").read_bytes(), np.uint8).reshape(256, 256, 4)
+    assert int(spec[0] + 0.5) == 8
+    o = orc.Oracle(R)
+    o.volume, o.tf, o.light = vol, tf, np.full(256, 100, np.uint8)
+    o.light_dir = np.array(ui["direction"], np.float32)
+    o.params.update(extinction=32.0, bounces=8, steps=8)
+    mvp = cf.default_mvp_inverse()
+    bits = lambda s: int(np.float32(s).view(np.uint32))  # noqa: E731
+    n_resets = used - passes  # the three model connections and the volume load
+    assert n_resets == 4
+    o.reset(mvp, bits(seeds[n_resets - 1]))  # a full reset: only the last one is visible
+    o.set_spectrum(spec)                     # uploaded by the first render (js:311)
+    for k in range(passes):
+        _, want = o.render(mvp, bits(seeds[n_resets + k]))
+    assert same(ph[:, :34], o.photons[:, :34])
     assert np.array_equal(rgba, want)

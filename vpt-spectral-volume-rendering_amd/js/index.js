@@ -8,6 +8,7 @@ const { Camera, Transform, PerspectiveCamera, mvpInverse } = require('./Camera')
 const { PropertyBag } = require('./PropertyBag');
 const { BufferLoader, FileLoader, RAWReader, ZIPReader, BVPReader, ReaderFactory, Volume } = require('./readers');
 const spectrum = require('./spectrum');
+const ui = require('./ui');
 const mat4 = require('./mat4');
 
 // A HIP device descriptor in place of the reference's GPUDevice.
@@ -18,4 +19,7 @@ function createDevice(ordinal = 0, layout = 'corner8') {
 module.exports = {
   MCMSpectralComputeRenderer, MCMComputeRenderer, RendererFactory, ArtisticToneMapper, ToneMapperFactory, Camera, Transform, PerspectiveCamera, mvpInverse,
   PropertyBag, BufferLoader, FileLoader, RAWReader, ZIPReader, BVPReader, ReaderFactory, Volume, spectrum, mat4, createDevice, native,
+  ui, MaterialTransferFunctionModel: ui.MaterialTransferFunctionModel,
+  SpectrumRepresentationModel: ui.SpectrumRepresentationModel, LightEditorModel: ui.LightEditorModel,
+  connectUiModels: ui.connectUiModels,
 };
