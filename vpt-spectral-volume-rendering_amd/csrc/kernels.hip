@@ -1320,6 +1320,20 @@ __device__ __forceinline__ float cand_eval(int fn, float x, float* ref) {
       *ref = 1.0f / __builtin_sqrtf(x);
       return inv_len(x);
     }
+    case 18: {  // candidate: RN(sqrt x) from the rsq estimate alone (s0 = x*rsq, one correction)
+      *ref = __builtin_sqrtf(x);
+      float y = __builtin_amdgcn_rsqf(x);
+      float s0 = x * y;
+      float e = __builtin_fmaf(-s0, s0, x);
+      return __builtin_fmaf(e, 0.5f * y, s0);
+    }
+    case 19: {  // candidate: RN(1/RN(sqrt x)) = rcp_in_range(case 18)
+      *ref = 1.0f / __builtin_sqrtf(x);
+      float y = __builtin_amdgcn_rsqf(x);
+      float s0 = x * y;
+      float e = __builtin_fmaf(-s0, s0, x);
+      return rcp_in_range(__builtin_fmaf(e, 0.5f * y, s0));
+    }
     case 5: {  // v_sqrt_f32 + one Newton correction using the rsq estimate
       *ref = __builtin_sqrtf(x);
       float s0 = __builtin_amdgcn_sqrtf(x);

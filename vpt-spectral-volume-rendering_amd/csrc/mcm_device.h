@@ -92,13 +92,19 @@ __device__ __forceinline__ float rcp_small(float x) {
   return y;
 }
 
-// RN(sqrt x): v_sqrt_f32 + one Newton step (rsq estimate) is exact for
-// positive x with biased exponent 32..254.
-__device__ __forceinline__ float sqrt_cr(float x) {
-  float s = __builtin_amdgcn_sqrtf(x);
+// RN(sqrt x) from the rsq estimate alone: s0 = x * rsq(x), then one Newton
+// correction with the same estimate, s = fma(x - s0^2, rsq/2, s0) — exact for
+// positive x with biased exponent 32..254 (one transcendental instead of the
+// v_sqrt + v_rsq pair; proven like the pair, tests/test_gpu_fastmath.py).
+__device__ __forceinline__ float sqrt_rsq(float x) {
+  float y = __builtin_amdgcn_rsqf(x);
+  float s = x * y;
   float e = __builtin_fmaf(-s, s, x);
-  float h = 0.5f * __builtin_amdgcn_rsqf(x);
-  s = __builtin_fmaf(e, h, s);
+  return __builtin_fmaf(e, 0.5f * y, s);
+}
+
+__device__ __forceinline__ float sqrt_cr(float x) {
+  float s = sqrt_rsq(x);
   uint32_t ex = __float_as_uint(x) >> 23;  // sign bit included: negatives excluded
   VPT_FIXUP(ex - 32u > 222u, s, sqrt_slow(x));
   return s;
@@ -110,10 +116,7 @@ __device__ __forceinline__ float sqrt_cr(float x) {
 // for everything but +-0 (where the Newton step makes 0 * inf), which one
 // select returns as is.
 __device__ __forceinline__ float sqrt_z(float x) {
-  float s = __builtin_amdgcn_sqrtf(x);
-  float e = __builtin_fmaf(-s, s, x);
-  float h = 0.5f * __builtin_amdgcn_rsqf(x);
-  s = __builtin_fmaf(e, h, s);
+  float s = sqrt_rsq(x);
   return x == 0.0f ? x : s;
 }
 
@@ -217,11 +220,7 @@ __device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a
 // takes the IEEE pair. Equal to rcp_cr(sqrt_cr(x)) for all 2^32 x
 // (tests/test_gpu_fastmath.py, fn 17).
 __device__ __forceinline__ float inv_len(float x) {
-  float s = __builtin_amdgcn_sqrtf(x);
-  float e = __builtin_fmaf(-s, s, x);
-  float h = 0.5f * __builtin_amdgcn_rsqf(x);
-  s = __builtin_fmaf(e, h, s);
-  float y = rcp_in_range(s);
+  float y = rcp_in_range(sqrt_rsq(x));
   uint32_t ex = __float_as_uint(x) >> 23;
   VPT_FIXUP(ex - 32u > 222u, y, rcp_slow(sqrt_slow(x)));
   return y;
