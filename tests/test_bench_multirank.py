@@ -12,6 +12,8 @@ import socket
 import subprocess
 import sys
 import textwrap
+
+import pytest
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
@@ -74,13 +76,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_bench_two_ranks_driver_command_line(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_two_ranks_driver_command_line(tmp_path, world):
     port = _free_port()
-    argv = ["--gpus", "2", "--steps", "20", "--warmup", "5", "--volume", "16", "--resolution", "16",
-            "--cpu-seconds", "0"]
+    argv = ["--gpus", str(world), "--steps", "20", "--warmup", "5", "--volume", "16",
+            "--resolution", "16", "--cpu-seconds", "0"]
     procs = []
-    for rank in (0, 1):
-        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2",
+    for rank in range(world):
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BENCH_ARGV=json.dumps(argv),
                    BENCH_PATH=str(REPO / "bench.py"), LOG_OUT=str(tmp_path / f"log{rank}.json"),
                    TORCHELASTIC_RUN_ID=f"t{port}")
@@ -90,12 +93,12 @@ def test_bench_two_ranks_driver_command_line(tmp_path):
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, o + e
     line = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
-    assert len(line) == 1 and not [ln for ln in outs[1][0].splitlines() if ln.startswith("{")]
+    assert len(line) == 1 and not [ln for o in outs[1:] for ln in o[0].splitlines() if ln.startswith("{")]
     rec = json.loads(line[0])
-    assert rec["n_gpus"] == 2 and rec["steps"] == 20 and rec["warmup"] == 5
+    assert rec["n_gpus"] == world and rec["steps"] == 20 and rec["warmup"] == 5
     assert rec["value"] > 0 and rec["config"]["workload"].startswith("C4")
     assert rec["per_pass_allreduce"]["steps"] == 64 and rec["per_pass_allreduce"]["value"] > 0
-    logs = [json.loads((tmp_path / f"log{r}.json").read_text()) for r in (0, 1)]
+    logs = [json.loads((tmp_path / f"log{r}.json").read_text()) for r in range(world)]
     uids = {e[1] for lg in logs for e in lg if e[0] == "comm_init"}
     assert len(uids) == 1, "ranks must share rank 0's unique id"
     for r, lg in enumerate(logs):
@@ -114,4 +117,6 @@ def test_bench_two_ranks_driver_command_line(tmp_path):
         assert rk[:128] == ["passes", "allreduce"] * 64
         assert all(len(e[1]) == 1 for e in rest if e[0] == "passes")
     seeds = [[s for e in lg if e[0] == "passes" for s in e[1]] for lg in logs]
-    assert not set(seeds[0]) & set(seeds[1]), "ranks must use distinct seed streams"
+    for a in range(world):
+        for b in range(a + 1, world):
+            assert not set(seeds[a]) & set(seeds[b]), "ranks must use distinct seed streams"
