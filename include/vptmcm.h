@@ -144,6 +144,14 @@ int vptmcm_set_environment(vptmcm* h, const uint8_t* rgba, uint32_t width, uint3
  * anisotropy, MCMComputeRenderer.wgsl:140). */
 int vptmcm_set_params(vptmcm* h, const vptmcm_params* p);
 
+/* Image band (SURVEY 8e "Mode B"): restrict reset and render to the pixel rows
+ * [y0, y1) — photon y*R + x for those rows only, every other photon and image
+ * row left untouched. y0 and y1 are multiples of 8 (y1 may be R). A band
+ * renderer per GPU with the SAME seeds gives, row for row, the single-GPU
+ * result; vptmcm_comm_gather_bands composites them exactly. Setting a band
+ * zeroes the fp32 image outside it. Default: the whole frame. */
+int vptmcm_set_band(vptmcm* h, uint32_t y0, uint32_t y1);
+
 /* ---- the hot path -------------------------------------------------------- */
 
 /* _resetFrame (js:213-260) -> reset compute_main (wgsl:213-231): every photon
@@ -237,6 +245,11 @@ int vptmcm_comm_allreduce_radiance(vptmcm* h);
 /* Wait for the last all-reduce and return the composite rgb = sum(rgb*n)/sum(n)
  * (R*R*3 floats) and, if counts != NULL, the summed n per pixel. */
 int vptmcm_comm_read_composite(vptmcm* h, float* rgb, float* counts);
+
+/* Mode B composite: sum over ranks of the fp32 radiance_to_rgb image (each
+ * rank's rows outside its band are zero, so the sum IS the single-GPU image,
+ * bit for bit); rgb = R*R*3 floats. Synchronous. */
+int vptmcm_comm_gather_bands(vptmcm* h, float* rgb);
 
 /* Blocking host-side helpers over the communicator (barrier, max/sum of a
  * few doubles) for the benchmark's bracketing. op: 0 = sum, 1 = max. */

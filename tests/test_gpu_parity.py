@@ -297,6 +297,61 @@ def test_composite_single_rank():
     gpu.close()
 
 
+@pytest.mark.parametrize("tfname,bands", [("spectral", [(0, 32), (32, 64)]),
+                                          ("materials", [(0, 8), (8, 40), (40, 64)]),
+                                          ("spectral", [(0, 24), (24, 56), (56, 60)])])
+def test_mode_b_bands_bitexact(tfname, bands):
+    """SURVEY 8e Mode B on the HIP path: band renderers (one per GPU in a real run;
+    here several handles on one GPU) with the same seeds reproduce the full-frame
+    renderer row for row — photons, rgba16f rows, and the fp32 image whose band
+    sum (rows outside a band are zero) is the full image bit for bit. R = 60
+    exercises a last band ending at R."""
+    R = 60 if bands[-1][1] == 60 else 64
+    tf = cf.tf_spectral() if tfname == "spectral" else cf.tf_materials(True)
+    vol = cf.fbm_volume(48, 9, nthreads=8)
+    full, _ = make_pair(R, vol, tf, ext=24.0)
+    parts = []
+    for y0, y1 in bands:
+        g, _ = make_pair(R, vol, tf, ext=24.0)
+        g.set_band(y0, y1)
+        parts.append(g)
+    mvp = cf.golden_mvp("orbit")
+    seeds = cf.seed_stream(8, start=3)
+    for g in [full] + parts:
+        g.reset(mvp, seeds[0])
+        for s in seeds[1:4]:
+            g.render(mvp, s)
+        g.render_passes(mvp, seeds[4:])
+    want_ph, want_rgba, want_rgb = full.read_photons(), full.read_rgba16f(), full.read_rgb()
+    acc = np.zeros_like(want_rgb)
+    for (y0, y1), g in zip(bands, parts):
+        ph = g.read_photons().reshape(R, R, -1)
+        assert same_words(ph[y0:y1], want_ph.reshape(R, R, -1)[y0:y1]).all(), f"band {y0}:{y1} photons"
+        assert np.array_equal(g.read_rgba16f()[y0:y1], want_rgba[y0:y1]), f"band {y0}:{y1} image"
+        rgb = g.read_rgb()
+        assert not rgb[:y0].any() and not rgb[y1:].any(), "rows outside the band stay zero"
+        acc += rgb
+    assert same_words(acc.view(np.uint32), want_rgb.view(np.uint32)).all(), "band composite"
+    with pytest.raises(vptmcm.VptError):
+        parts[0].set_band(4, 16)  # not a multiple of 8
+    for g in [full] + parts:
+        g.close()
+
+
+def test_mode_b_gather_single_rank():
+    """vptmcm_comm_gather_bands over RCCL with one rank: the rank's own fp32 image."""
+    gpu, _ = make_pair(64, cf.sphere_in_cube(64), cf.tf_spectral())
+    gpu.comm_init(vptmcm.unique_id(), 1, 0)
+    gpu.set_band(16, 48)
+    mvp = cf.default_mvp_inverse()
+    gpu.reset(mvp, 5)
+    gpu.render_passes(mvp, cf.seed_stream(4))
+    img = gpu.read_rgb()
+    assert np.array_equal(gpu.gather_bands().view(np.uint32), img.view(np.uint32))
+    assert not img[:16].any() and not img[48:].any()
+    gpu.close()
+
+
 def test_kernel_timing_counts_launches():
     """render_passes fuses up to 32 passes per march launch."""
     gpu, _ = make_pair(64, cf.sphere_in_cube(64), cf.tf_spectral())

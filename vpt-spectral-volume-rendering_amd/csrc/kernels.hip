@@ -87,7 +87,7 @@ __device__ __forceinline__ bool near_fixed(const MarchParams& P, float sx, float
 __global__ __launch_bounds__(kBlock) void k_reset(const MarchParams P, float* __restrict__ ph) {
   uint32_t x, y;
   size_t i;
-  if (!tile_pixel(P, x, y, i)) return;
+  if (!tile_pixel(P, x, y, i) || y < P.band_y0 || y >= P.band_y1) return;
   const size_t S = P.npad;
   float sx, sy;
   screen_of(P, x, y, sx, sy);
@@ -371,7 +371,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   const uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
   const uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
   const size_t i = (size_t)tile * 64u + lane;
-  const bool live = tile != 0xffffffffu && x < P.R && y < P.R;
+  // tiles outside the band (whole tiles: band rows are multiples of 8) are idle
+  const bool live = tile != 0xffffffffu && x < P.R && y < P.R && y >= P.band_y0 && y < P.band_y1;
   const size_t S = P.npad;
   bool entered = false;  // wave-uniform: some lane of this wave was inside the volume
 #if VPT_STAMP
@@ -409,7 +410,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     if (DEDUP || (!FAST && P.tf_dedup)) s_rowmap[threadIdx.x] = (uint32_t)tf_rowmap[threadIdx.x] * 256u;
   }
   __syncthreads();
-  if (!live) return;
+  if (!live) {
+    if (tile < P.n_tiles && lane == 0u) T.flags_out[tile] = 0u;  // an idle out-of-band tile
+    return;
+  }
   const uint16_t* s_tf = reinterpret_cast<const uint16_t*>(s_tf4);
 
   float sx, sy;
@@ -783,7 +787,7 @@ __device__ __forceinline__ void rgb_reset_draws(const MarchParams& P, float sx, 
 __global__ __launch_bounds__(kBlock) void k_reset_rgb(const MarchParams P, float* __restrict__ ph) {
   uint32_t x, y;
   size_t i;
-  if (!tile_pixel(P, x, y, i)) return;
+  if (!tile_pixel(P, x, y, i) || y < P.band_y0 || y >= P.band_y1) return;
   const size_t S = P.npad;
   float sx, sy;
   screen_of(P, x, y, sx, sy);
@@ -839,7 +843,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
   const uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
   const uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
   const size_t i = (size_t)tile * 64u + lane;
-  const bool live = tile != 0xffffffffu && x < P.R && y < P.R;
+  const bool live = tile != 0xffffffffu && x < P.R && y < P.R && y >= P.band_y0 && y < P.band_y1;
   const size_t S = P.npad;
   f3 pos{0.0f, 0.0f, 0.0f}, dir{0.0f, 0.0f, 0.0f}, tr{0.0f, 0.0f, 0.0f}, rad{0.0f, 0.0f, 0.0f};
   uint32_t bounces = 0u, samples = 0u;
@@ -853,7 +857,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
   }
   for (uint32_t k = threadIdx.x; k < P.tf_w; k += kMarchBlock) s_tf[k] = tf[k];
   __syncthreads();
-  if (!live) return;
+  if (!live) {
+    if (tile < P.n_tiles && lane == 0u) T.flags_out[tile] = 0u;  // an idle out-of-band tile
+    return;
+  }
 
   float sx, sy;
   screen_of(P, x, y, sx, sy);

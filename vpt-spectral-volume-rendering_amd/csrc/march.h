@@ -83,6 +83,7 @@ struct MarchParams {
   uint32_t robust;
   float rb_x0, rb_x1, rb_y0, rb_y1;
   uint32_t R, tiles_x, n_tiles, npad;
+  uint32_t band_y0, band_y1;  // pixel rows [band_y0, band_y1) this renderer owns (Mode B)
   uint32_t W, H, D;
   // CORNER8 cell byte offsets fit 32 bits ((W+1)(H+1)(D+1) * 8 < 2^32 and
   // (D+1)(H+1) < 2^24): the gather address is u24 multiply-adds on a 32-bit

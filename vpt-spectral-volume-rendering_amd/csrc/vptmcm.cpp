@@ -38,6 +38,7 @@ struct vptmcm {
   uint32_t layout = kLayoutLinear;
   uint32_t kind = VPTMCM_RENDERER_SPECTRAL;
   uint32_t variant = 0;  // tuning knob (VPTMCM_MARCH_VARIANT), results identical
+  uint32_t band_y0 = 0, band_y1 = 0;  // vptmcm_set_band (band_y1 = R after create)
 
   float* photons = nullptr;    // kNumPlanes * npad words
   uint16_t* rgba = nullptr;    // R*R*4 halfs
@@ -292,6 +293,8 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
     P.rb_y1 = rb[3];
   }
   P.R = h->R;
+  P.band_y0 = h->band_y0;
+  P.band_y1 = h->band_y1;
   P.tiles_x = h->tiles_x;
   P.n_tiles = h->n_tiles;
   P.npad = h->npad;
@@ -446,6 +449,8 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   h->kind = cfg->renderer;
   if (const char* v = getenv("VPTMCM_MARCH_VARIANT")) h->variant = (uint32_t)strtoul(v, nullptr, 0);
   h->R = cfg->resolution;
+  h->band_y0 = 0;
+  h->band_y1 = h->R;
   h->tiles_x = (h->R + 7) / 8;
   h->n_tiles = h->tiles_x * h->tiles_x;
   h->npad = h->n_tiles * 64;
@@ -734,6 +739,21 @@ int vptmcm_set_environment(vptmcm* h, const uint8_t* rgba, uint32_t width, uint3
     FAIL(h, VPTMCM_EINVAL, "set_environment: only the 1x1 environment of the rendering context "
                            "(WebGPURenderingContext.js:97-108) is supported");
   for (int k = 0; k < 4; k++) h->env[k] = (float)rgba[k] * kInv255;
+  return VPTMCM_OK;
+}
+
+int vptmcm_set_band(vptmcm* h, uint32_t y0, uint32_t y1) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
+  if (!(y0 < y1 && y1 <= h->R && y0 % 8u == 0u && (y1 % 8u == 0u || y1 == h->R)))
+    FAIL(h, VPTMCM_EINVAL, "set_band: need y0 < y1 <= R, y0 and y1 multiples of 8 (y1 may be R)");
+  HIPCHK(h, hipSetDevice(h->device));
+  h->band_y0 = y0;
+  h->band_y1 = y1;
+  const size_t row = (size_t)h->R * 3 * sizeof(float);
+  if (y0 > 0) HIPCHK(h, hipMemsetAsync(h->rgb32, 0, y0 * row, h->stream));
+  if (y1 < h->R)
+    HIPCHK(h, hipMemsetAsync((char*)h->rgb32 + y1 * row, 0, (h->R - y1) * row, h->stream));
   return VPTMCM_OK;
 }
 
@@ -1047,6 +1067,24 @@ int vptmcm_comm_read_composite(vptmcm* h, float* rgb, float* counts) {
     for (int c = 0; c < 3; c++) rgb[i * 3 + c] = n > 0.0f ? buf[i * 4 + c] / n : 0.0f;
     if (counts) counts[i] = n;
   }
+  return VPTMCM_OK;
+}
+
+int vptmcm_comm_gather_bands(vptmcm* h, float* rgb) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
+  if (!h->comm) FAIL(h, VPTMCM_ECOMM, "comm_gather_bands: no communicator");
+  if (!rgb) FAIL(h, VPTMCM_EINVAL, "comm_gather_bands: null output");
+  HIPCHK(h, hipSetDevice(h->device));
+  const size_t n = (size_t)h->R * h->R * 3;
+  float* sum = reinterpret_cast<float*>(h->comp[h->comp_next]);  // R*R float4 >= R*R*3 floats
+  HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[h->comp_next], 0));
+  HIPCHK(h, hipMemcpyAsync(sum, h->rgb32, n * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  NCCLCHK(h, ncclAllReduce(sum, sum, n, ncclFloat32, ncclSum, h->comm, h->comm_stream));
+  HIPCHK(h, hipMemcpyAsync(rgb, sum, n * sizeof(float), hipMemcpyDeviceToHost, h->comm_stream));
+  HIPCHK(h, hipEventRecord(h->comp_done[h->comp_next], h->comm_stream));
+  HIPCHK(h, hipStreamSynchronize(h->comm_stream));
   return VPTMCM_OK;
 }
 

@@ -27,6 +27,7 @@ EXPORTS = [
     "vptmcm_create", "vptmcm_destroy", "vptmcm_last_error", "vptmcm_set_volume",
     "vptmcm_volume_begin", "vptmcm_volume_write_block", "vptmcm_volume_end",
     "vptmcm_set_material_tf", "vptmcm_set_light", "vptmcm_set_spectrum", "vptmcm_set_params",
+    "vptmcm_set_band", "vptmcm_comm_gather_bands",
     "vptmcm_reset", "vptmcm_render", "vptmcm_render_passes", "vptmcm_synchronize",
     "vptmcm_read_rgba16f", "vptmcm_read_rgb", "vptmcm_pack_radiance", "vptmcm_read_photons", "vptmcm_write_photons",
     "vptmcm_tonemap_artistic", "vptmcm_set_transfer_function", "vptmcm_set_environment",
@@ -90,6 +91,8 @@ def load() -> C.CDLL:
         "vptmcm_set_light": (C.c_int, [vp, vp, f32p]),
         "vptmcm_set_spectrum": (C.c_int, [vp, f32p]),
         "vptmcm_set_params": (C.c_int, [vp, C.POINTER(Params)]),
+        "vptmcm_set_band": (C.c_int, [vp, C.c_uint32, C.c_uint32]),
+        "vptmcm_comm_gather_bands": (C.c_int, [vp, f32p]),
         "vptmcm_reset": (C.c_int, [vp, f32p, C.c_uint32]),
         # the per-pass calls take raw addresses (c_void_p): no ctypes pointer objects
         "vptmcm_render": (C.c_int, [vp, vp, C.c_uint32]),
@@ -218,6 +221,10 @@ class Renderer:
         p = Params(extinction, anisotropy, bounces, steps, blur)
         self._ck(self.L.vptmcm_set_params(self.h, C.byref(p)))
 
+    def set_band(self, y0: int, y1: int) -> None:
+        """Mode B: reset/render only pixel rows [y0, y1) (multiples of 8)."""
+        self._ck(self.L.vptmcm_set_band(self.h, int(y0), int(y1)))
+
     # -- hot path
     def reset(self, mvp, seed_bits: int) -> None:
         m = mat_f32(mvp)
@@ -307,6 +314,12 @@ class Renderer:
         n = np.empty((self.R, self.R), np.float32)
         self._ck(self.L.vptmcm_comm_read_composite(self.h, _f32p(rgb), _f32p(n)))
         return rgb, n
+
+    def gather_bands(self) -> np.ndarray:
+        """Mode B composite over the communicator: the fp32 image, bit-exact."""
+        out = np.empty((self.R, self.R, 3), np.float32)
+        self._ck(self.L.vptmcm_comm_gather_bands(self.h, _f32p(out)))
+        return out
 
     def barrier(self) -> None:
         self._ck(self.L.vptmcm_comm_barrier(self.h))
