@@ -35,6 +35,7 @@ const V = require(path.join(ROOT, 'vpt-spectral-volume-rendering_amd', 'js'));
     renderer.setMaterialTransferFunction(new Uint8Array(fs.readFileSync(c.tf_path)), false);
   }
 
+  if (c.band) renderer.setBand(c.band[0], c.band[1]);  // Mode B row band
   if (c.ui) {  // the headless UI models drive the renderer's inputs (js/ui.js)
     const tf = new V.MaterialTransferFunctionModel();
     for (const m of c.ui.materials) {

@@ -134,7 +134,7 @@ test('addon loads; renderer construction fails loudly without a GPU', () => {
   for (const f of ['create', 'destroy', 'setVolume', 'volumeBegin', 'volumeWriteBlock', 'volumeEnd',
     'setMaterialTF', 'setLight', 'setSpectrum', 'setParams', 'reset', 'render', 'renderPasses',
     'synchronize', 'readRGBA16F', 'readPhotons', 'writePhotons', 'enableKernelTiming', 'kernelTime',
-    'commUniqueId', 'commInit', 'commAllreduceRadiance', 'commReadComposite', 'commBarrier', 'version',
+    'commUniqueId', 'commInit', 'commAllreduceRadiance', 'commReadComposite', 'commBarrier', 'setBand', 'commGatherBands', 'version',
     'tonemapArtistic']) {
     assert.strictEqual(typeof A[f], 'function', f);
   }

@@ -22,7 +22,7 @@ ROOT = Path(__file__).resolve().parents[1]
 
 
 def run_case(tmp_path, vol, tf, R=64, passes=3, ext=32.0, layout="corner8", stream=True,
-             change_event=False, tonemap=None, bvp=None, ui=None):
+             change_event=False, tonemap=None, bvp=None, ui=None, band=None):
     D, H, W = vol.shape
     (tmp_path / "vol.raw").write_bytes(np.ascontiguousarray(vol).tobytes())
     (tmp_path / "tf.bin").write_bytes(np.ascontiguousarray(tf).tobytes())
@@ -30,7 +30,7 @@ def run_case(tmp_path, vol, tf, R=64, passes=3, ext=32.0, layout="corner8", stre
     case = dict(R=R, passes=passes, extinction=ext, bounces=8, steps=8, layout=layout,
                 W=W, H=H, D=D, volume_path=str(tmp_path / "vol.raw"), tf_path=str(tmp_path / "tf.bin"),
                 seeds=seeds, stream_volume=stream, change_event=change_event, tonemap=tonemap,
-                bvp_path=None, ui=ui)
+                bvp_path=None, ui=ui, band=band)
     if bvp is not None:
         (tmp_path / "vol.bvp").write_bytes(bvp)
         case["bvp_path"] = str(tmp_path / "vol.bvp")
@@ -182,3 +182,23 @@ def test_js_ui_models_drive_renderer_bitexact(tmp_path):
         _, want = o.render(mvp, bits(seeds[n_resets + k]))
     assert same(ph[:, :34], o.photons[:, :34])
     assert np.array_equal(rgba, want)
+
+
+def test_js_mode_b_band_matches_full_frame(tmp_path):
+    """renderer.setBand (N-API setBand -> vptmcm_set_band): the band rows of photons,
+    rgba16float and fp32 image equal the full-frame JS render's; the fp32 image is zero
+    outside the band (what commGatherBands sums)."""
+    vol = cf.fbm_volume(64, 9, nthreads=8)
+    R, y0, y1 = 64, 16, 48
+    (tmp_path / "full").mkdir()
+    (tmp_path / "band").mkdir()
+    ph_f, rgba_f, _, _ = run_case(tmp_path / "full", vol, cf.tf_spectral(), R=R, passes=3)
+    rgb_f = run_case.rgb32
+    ph_b, rgba_b, _, _ = run_case(tmp_path / "band", vol, cf.tf_spectral(), R=R, passes=3,
+                                  band=[y0, y1])
+    rgb_b = run_case.rgb32
+    assert np.array_equal(rgba_b[y0:y1], rgba_f[y0:y1])
+    assert np.array_equal(rgb_b[y0:y1].view(np.uint32), rgb_f[y0:y1].view(np.uint32))
+    assert not rgb_b[:y0].any() and not rgb_b[y1:].any()
+    rows = ph_f.reshape(R, R, 36)[y0:y1]
+    assert np.array_equal(ph_b.reshape(R, R, 36)[y0:y1], rows)

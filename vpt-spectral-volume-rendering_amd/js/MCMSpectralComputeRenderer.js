@@ -226,6 +226,13 @@ class MCMSpectralComputeRenderer extends PropertyBag {
     for (let k = 0; k < n; k++) this._renderFrame();
   }
 
+  // Mode B (DESIGN.md): march only pixel rows [y0, y1) (multiples of 8; y1 may
+  // be the resolution); ranks holding disjoint bands composite with
+  // native().commGatherBands. A new resolution drops the band.
+  setBand(y0, y1) {
+    native().setBand(this._h, y0, y1);
+  }
+
   readPhotons() {
     const R = this._resolution;
     const out = new Uint8Array(R * R * 144);

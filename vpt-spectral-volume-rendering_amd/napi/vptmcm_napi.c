@@ -446,6 +446,27 @@ static napi_value js_comm_read_composite(napi_env env, napi_callback_info info) 
     return check(env, h, vptmcm_comm_read_composite(h, rgb, NULL));
 }
 
+/* setBand(h, y0, y1): Mode B row band (multiples of 8; y1 may be R) */
+static napi_value js_set_band(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (get_args(env, info, 3, argv)) return NULL;
+    vptmcm* h = get_handle(env, argv[0]);
+    if (!h) return NULL;
+    return check(env, h, vptmcm_set_band(h, get_u32(env, argv[1]), get_u32(env, argv[2])));
+}
+
+/* commGatherBands(h, Float32Array(R*R*3), R): every rank's band, composited */
+static napi_value js_comm_gather_bands(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (get_args(env, info, 3, argv)) return NULL;
+    vptmcm* h = get_handle(env, argv[0]);
+    if (!h) return NULL;
+    uint32_t R = get_u32(env, argv[2]);
+    float* rgb = get_typed(env, argv[1], 4, (size_t)R * R * 3, NULL);
+    if (!rgb) return NULL;
+    return check(env, h, vptmcm_comm_gather_bands(h, rgb));
+}
+
 static napi_value js_comm_barrier(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     if (get_args(env, info, 1, argv)) return NULL;
@@ -498,6 +519,8 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("commAllreduceRadiance", js_comm_allreduce_radiance);
     EXPORT("commReadComposite", js_comm_read_composite);
     EXPORT("commBarrier", js_comm_barrier);
+    EXPORT("setBand", js_set_band);
+    EXPORT("commGatherBands", js_comm_gather_bands);
     EXPORT("version", js_version);
     return exports;
 }
