@@ -47,7 +47,7 @@ def _stale(out: Path, deps: list[Path]) -> bool:
 def build_hip(force: bool = False) -> Path:
     out = LIB / "libvptmcm.so"
     srcs = [CSRC / "kernels.hip", CSRC / "vptmcm.cpp"]
-    deps = srcs + [CSRC / "kernels.h", CSRC / "march.h", CSRC / "mcm_device.h",
+    deps = srcs + [CSRC / "kernels.h", CSRC / "march.h", CSRC / "mcm_device.h", CSRC / "stamp.h",
                    REPO / "include" / "vptmcm.h"]
     if force or _stale(out, deps):
         hipcc = shutil.which("hipcc") or str(ROCM / "bin" / "hipcc")

@@ -15,25 +15,7 @@
 #ifndef VPT_PRIO
 #define VPT_PRIO 1  // s_setprio level of volume waves (0 = off); 11 % faster passes
 #endif
-// Measurement builds only (tools/stamp_profile.py, lib/libvptmcm_stamp.so): per
-// wave s_memtime sums of the volume step's segments, the launch's shader cycles
-// and 100 MHz real time, and the wave's hardware SIMD, written over the fp32
-// image (which these builds do not store). The product library has VPT_STAMP 0.
-#ifndef VPT_STAMP
-#define VPT_STAMP 0
-#endif
-#if VPT_STAMP
-#define STAMP_AT(k)                                                   \
-  do {                                                                \
-    const uint32_t _t = (uint32_t)__builtin_amdgcn_s_memtime();       \
-    prof[(k) >> 1] += (_t - t_prev) << (((k) & 1) * 16);              \
-    t_prev = _t;                                                      \
-  } while (0)
-#else
-#define STAMP_AT(k) \
-  do {              \
-  } while (0)
-#endif
+#include "stamp.h"  // measurement-build hooks (VPT_STAMP); empty in the product
 
 namespace vpt {
 
@@ -375,15 +357,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   const bool live = tile != 0xffffffffu && x < P.R && y < P.R && y >= P.band_y0 && y < P.band_y1;
   const size_t S = P.npad;
   bool entered = false;  // wave-uniform: some lane of this wave was inside the volume
-#if VPT_STAMP
-  // two 16-bit cycle sums per word (one-pass launches): [0] step head, [1] gather
-  // issue + shadow, [2] exposed gather wait, [3] filter + TF + decision, [4]
-  // decision branches, [5] robust/all-exit steps; word 3 = volume steps, word 4 = launch
-  uint32_t prof[5] = {0u, 0u, 0u, 0u, 0u};
-  uint32_t t_prev = (uint32_t)__builtin_amdgcn_s_memtime();
-  const uint32_t t_launch = t_prev;
-  const uint32_t rt_launch = (uint32_t)__builtin_amdgcn_s_memrealtime();
-#endif
+  STAMP_BEGIN();
   Photon p;
   if (live) load_photon(ph, S, i, p);  // issue the state loads before the LDS fill
 #if VPT_NB_ZERO
@@ -499,9 +473,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       rb = rbpix;
     };
     for (uint32_t step = 0; step < P.steps; step++) {
-#if VPT_STAMP
-      t_prev = (uint32_t)__builtin_amdgcn_s_memtime();
-#endif
+      STAMP_RESTART();
       if (__builtin_amdgcn_ballot_w64(!rb) == 0ull) {
         // Robust path: the exit of wgsl:142-150 and the reset, minus what a
         // certain exit does not need (the distance only moves the photon
@@ -588,11 +560,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       float ud = dot3(u, p.dir);
       f3 circle = norm3(f3{fmaf(-ud, p.dir.x, u.x), fmaf(-ud, p.dir.y, u.y), fmaf(-ud, p.dir.z, u.z)});
 
-#if VPT_STAMP
-      STAMP_AT(1);
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the gather's exposed latency
-      STAMP_AT(2);
-#endif
+      STAMP_GATHER_WAIT();
       // sample_volume_color (wgsl:75-80) -> probabilities (wgsl:132-139)
       float d = vol_filter(vt);  // in [0, 1]: a lerp of bytes times RN(1/255)
       float fr;
@@ -656,9 +624,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         st = sw;  // null collision
       }
       STAMP_AT(4);
-#if VPT_STAMP
-      prof[3]++;
-#endif
+      STAMP_COUNT_STEP();
     }
     apply_pending();
   } else {
@@ -748,19 +714,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     if (NBF || !VPT_NB_ZERO || (uint32_t)b < P.nb) ph[(kRad0 + b) * S + i] = p.rad[b];
 
   if (lane == 0u) T.flags_out[tile] = entered ? 1u : 0u;  // the next pass's schedule
-#if VPT_STAMP
-  prof[4] = (uint32_t)__builtin_amdgcn_s_memtime() - t_launch;
-  const uint32_t rt_total = (uint32_t)__builtin_amdgcn_s_memrealtime() - rt_launch;
-  if (lane == 0u) {  // vector stores (measurement builds only)
-    uint32_t* o = reinterpret_cast<uint32_t*>(rgb32) + (size_t)tile * 8u;
-#pragma unroll
-    for (int k = 0; k < 5; k++) o[k] = prof[k];
-    // HW_ID (hwreg 4: wave, SIMD, CU, SH, SE ids) and XCC_ID (hwreg 20)
-    o[5] = (entered ? 1u : 0u) | ((__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xffu) << 8);
-    o[6] = rt_total;  // 100 MHz ticks
-    o[7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-  }
-#endif
+  STAMP_END(rgb32, tile, entered);
 }
 
 
