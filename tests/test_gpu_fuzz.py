@@ -1,0 +1,201 @@
+"""Randomised GPU parity: seeded random configurations of every input the march
+reads — resolution (incl. R not a multiple of 8), ragged volume shapes, all
+three layouts, random / few-row / many-row TFs with constant or varying
+anisotropy, random bin layouts (uneven, duplicate and unsorted boundaries,
+random CMF coefficients), random light SPD and direction (incl. isotropic),
+extinction over three decades plus 0 and 1e4, bounces, steps, depth of field and random camera
+matrices (incl. a camera inside the volume) — against the oracle, bit for bit,
+through unfused and fused (queued) passes. Each case prints its draw, so a
+failure names the configuration that exposed it.
+"""
+import numpy as np
+import pytest
+
+import oracle as orc
+import vptmcm
+from vptmcm import configs as cf
+from test_gpu_parity import assert_photons_equal, assert_rgb32_equal, assert_rgba_equal
+
+pytestmark = pytest.mark.gpu
+
+N_CASES = 96
+
+
+def _perspective_inverse(rng, inside=False):
+    """invert(P * V * M) of a random look-at camera (float64, rounded to f32 once)."""
+    f = 1.0 / np.tan(rng.uniform(0.4, 1.2) / 2)
+    near, far = 0.1, 100.0
+    P = np.array([[f, 0, 0, 0], [0, f, 0, 0],
+                  [0, 0, (far + near) / (near - far), 2 * far * near / (near - far)],
+                  [0, 0, -1, 0]])
+    target = rng.uniform(0.3, 0.7, 3) if not inside else rng.uniform(0.45, 0.55, 3)
+    if inside:
+        eye = rng.uniform(0.3, 0.7, 3)
+    else:
+        d = rng.normal(size=3)
+        eye = 0.5 + d / np.linalg.norm(d) * rng.uniform(1.2, 3.0)
+    fwd = target - eye
+    fwd /= np.linalg.norm(fwd)
+    up = np.array([0.0, 1.0, 0.0]) if abs(fwd[1]) < 0.95 else np.array([1.0, 0.0, 0.0])
+    s = np.cross(fwd, up)
+    s /= np.linalg.norm(s)
+    u = np.cross(s, fwd)
+    V = np.eye(4)
+    V[0, :3], V[1, :3], V[2, :3] = s, u, -fwd
+    V[:3, 3] = -V[:3, :3] @ eye
+    # column-major f32[16], as the renderer uploads gl-matrix matrices
+    return np.linalg.inv(P @ V).T.reshape(16).astype(np.float32)
+
+
+def _spectrum(rng):
+    kind = rng.integers(0, 5)
+    if kind == 0:
+        return "12 equal", cf.spectrum_buffer("12")
+    nb = int(rng.integers(1, 13))
+    bins = np.sort(rng.integers(400, 701, nb + 1)).astype(np.float64)
+    what = f"{nb} random bins"
+    if kind == 1:  # duplicate boundaries: zero-width bins (UI markers may coincide)
+        bins[rng.integers(0, nb + 1)] = bins[rng.integers(0, nb + 1)]
+        bins = np.sort(bins)
+        what += " (duplicates)"
+    if kind == 2:  # unsorted markers (the generic bin search)
+        rng.shuffle(bins)
+        what += " (unsorted)"
+    buf = np.zeros(64, np.float32)
+    coeff = rng.uniform(0.0, 2.0, 3 * nb)
+    buf[: 1 + (nb + 1) + 3 * nb] = np.concatenate([[nb], bins, coeff])
+    return what, buf
+
+
+def _tf(rng):
+    kind = rng.integers(0, 5)
+    if kind == 0:
+        return "spectral", cf.tf_spectral()
+    if kind == 1:
+        return "materials varying b", cf.tf_materials(True)
+    if kind == 2:
+        return "materials constant b", cf.tf_materials(False)
+    if kind == 3:  # few distinct rows painted over random ranges (deduplicated TF)
+        t = np.zeros((256, 256, 4), np.uint8)
+        edges = np.sort(rng.integers(0, 256, 6))
+        for a, b in zip(edges[:-1], edges[1:]):
+            mat = rng.integers(0, 256, (256, 3), dtype=np.uint8)
+            if rng.random() < 0.5:
+                mat[:, 2] = mat[0, 2]
+            t[a:b, :, :3] = mat[None]
+        return "random few-row", t
+    t = rng.integers(0, 256, (256, 256, 4), dtype=np.uint8)  # every row distinct
+    return "random noise", t
+
+
+def _draw(k):
+    rng = np.random.default_rng(1000 + k)
+    R = int(rng.choice([8, 16, 24, 40, 48, 64, 72, 96, 128, 200, 256])) + (int(rng.integers(1, 8)) if rng.random() < 0.3 else 0)
+    shape = tuple(int(x) for x in rng.integers(1, 72, 3)) if rng.random() < 0.4 else (48, 48, 48)
+    layout = int(rng.choice([vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_LINEAR, vptmcm.LAYOUT_BRICK8]))
+    spec_what, spec = _spectrum(rng)
+    tf_what, tf = _tf(rng)
+    iso = rng.random() < 0.2
+    ld = np.zeros(3, np.float32) if iso else rng.normal(size=3).astype(np.float32)
+    spd = (np.full(256, 100, np.uint8) if rng.random() < 0.5
+           else rng.integers(0, 256, 256, dtype=np.uint8))
+    ext = float(np.float32(10 ** rng.uniform(-0.3, 2.5)))
+    ext = {0: 0.0, 1: 1e4}.get(int(rng.integers(0, 20)), ext)  # inf/NaN distances; huge majorant
+    params = dict(extinction=ext, bounces=int(rng.integers(0, 11)), steps=int(rng.integers(0, 41)),
+                  blur=float(np.float32(rng.uniform(0, 0.5))) if rng.random() < 0.25 else 0.0)
+    mvp = (cf.default_mvp_inverse() if rng.random() < 0.25
+           else _perspective_inverse(rng, inside=rng.random() < 0.2))
+    vol_seed = int(rng.integers(0, 1 << 16))
+    what = (f"case {k}: R={R} vol={shape} layout={layout} bins={spec_what} tf={tf_what} "
+            f"light={'isotropic' if iso else 'directional'} {params}")
+    return R, shape, layout, spec, tf, ld, spd, params, mvp, vol_seed, what
+
+
+def _volume(shape, seed):
+    if shape == (48, 48, 48):
+        return cf.fbm_volume(48, seed % 97, nthreads=8)
+    rng = np.random.default_rng(seed)
+    D, H, W = shape[2], shape[1], shape[0]
+    base = rng.integers(0, 256, (D, H, W)).astype(np.float64)
+    # a smooth blob plus noise: both empty and dense regions
+    z, y, x = np.meshgrid(*(np.linspace(-1, 1, n) for n in (D, H, W)), indexing="ij")
+    blob = np.clip(1.2 - np.sqrt(x * x + y * y + z * z), 0, 1) * 255
+    return np.clip(0.6 * blob + 0.4 * base * (blob > 0), 0, 255).astype(np.uint8)
+
+
+@pytest.mark.parametrize("k", range(N_CASES))
+def test_random_configuration_bitexact(k):
+    R, shape, layout, spec, tf, ld, spd, params, mvp, vol_seed, what = _draw(k)
+    print(what)
+    vol = _volume(shape, vol_seed)
+    with vptmcm.Renderer(R, device=0, layout=layout) as gpu:
+        cpu = orc.Oracle(R)
+        gpu.set_spectrum(spec)
+        cpu.set_spectrum(spec)
+        gpu.set_volume(vol)
+        gpu.set_material_tf(tf)
+        gpu.set_light(spd, ld)
+        gpu.set_params(**params)
+        cpu.volume, cpu.tf, cpu.light, cpu.light_dir = vol, tf, spd, ld
+        cpu.params.update(**params)
+        seeds = cf.seed_stream(6, start=10 * k)
+        gpu.reset(mvp, seeds[0])
+        cpu.reset(mvp, seeds[0], nthreads=16)
+        assert_photons_equal(gpu.read_photons(), cpu.photons, what + " reset")
+        for p in (1, 2):  # one launch per pass (read back between them)
+            gpu.render(mvp, seeds[p])
+            rgb, want = cpu.render(mvp, seeds[p], nthreads=16)
+            assert_photons_equal(gpu.read_photons(), cpu.photons, f"{what} pass {p}")
+            assert_rgba_equal(gpu.read_rgba16f(), want, f"{what} pass {p}")
+            assert_rgb32_equal(gpu.read_rgb(), rgb, f"{what} pass {p}")
+        for p in (3, 4, 5):  # queued: one fused launch of three passes
+            gpu.render(mvp, seeds[p])
+            rgb, want = cpu.render(mvp, seeds[p], nthreads=16)
+        assert_photons_equal(gpu.read_photons(), cpu.photons, f"{what} fused")
+        assert_rgba_equal(gpu.read_rgba16f(), want, f"{what} fused")
+        assert_rgb32_equal(gpu.read_rgb(), rgb, f"{what} fused")
+
+
+def _same_words(a, b):
+    fa, fb = a.view(np.float32), b.view(np.float32)
+    return (a == b) | (np.isnan(fa) & np.isnan(fb))
+
+
+@pytest.mark.parametrize("k", range(N_CASES // 2))
+def test_random_configuration_rgb_bitexact(k):
+    """The RGB sibling ('mcm-compute') under the same random draws, with a random
+    rgba8 TF image (random width/height; the kernel samples row 0), a random
+    environment colour and a random anisotropy."""
+    R, shape, layout, _, _, _, _, params, mvp, vol_seed, what = _draw(k)
+    rng = np.random.default_rng(5000 + k)
+    tf = rng.integers(0, 256, (int(rng.integers(1, 4)), int(rng.integers(2, 300)), 4), dtype=np.uint8)
+    env = tuple(int(x) for x in rng.integers(0, 256, 4))
+    aniso = float(np.float32(rng.uniform(-0.95, 0.95)))
+    params = dict(extinction=params["extinction"], anisotropy=aniso, bounces=params["bounces"],
+                  steps=params["steps"])
+    what = f"rgb {what} tf={tf.shape} env={env} anisotropy={aniso}"
+    print(what)
+    vol = _volume(shape, vol_seed)
+    with vptmcm.Renderer(R, device=0, layout=layout, renderer=vptmcm.RENDERER_RGB) as gpu:
+        cpu = orc.OracleRGB(R)
+        gpu.set_transfer_function(tf)
+        gpu.set_environment(env)
+        gpu.set_volume(vol)
+        gpu.set_params(**params)
+        cpu.volume, cpu.tf, cpu.env = vol, tf, np.array(env, np.uint8)
+        cpu.params.update(**params)
+        seeds = cf.seed_stream(6, start=10 * k + 3)
+        gpu.reset(mvp, seeds[0])
+        cpu.reset(mvp, seeds[0])
+        assert _same_words(gpu.read_photons(), cpu.photons).all(), what + " reset"
+        for p in (1, 2):
+            gpu.render(mvp, seeds[p])
+            _, want = cpu.render(mvp, seeds[p])
+            ok = _same_words(gpu.read_photons(), cpu.photons)
+            assert ok.all(), f"{what} pass {p}: {int((~ok).sum())} photon words differ"
+            assert np.array_equal(gpu.read_rgba16f(), want), f"{what} pass {p}: image differs"
+        gpu.render_passes(mvp, seeds[3:])  # one fused launch
+        for s in seeds[3:]:
+            _, want = cpu.render(mvp, s)
+        assert _same_words(gpu.read_photons(), cpu.photons).all(), what + " fused"
+        assert np.array_equal(gpu.read_rgba16f(), want), what + " fused image"
