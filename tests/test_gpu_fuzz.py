@@ -199,3 +199,61 @@ def test_random_configuration_rgb_bitexact(k):
             _, want = cpu.render(mvp, s)
         assert _same_words(gpu.read_photons(), cpu.photons).all(), what + " fused"
         assert np.array_equal(gpu.read_rgba16f(), want), what + " fused image"
+
+
+def _setup_spectral(gpu, cpu, draw):
+    R, shape, layout, spec, tf, ld, spd, params, mvp, vol_seed, what = draw
+    vol = _volume(shape, vol_seed)
+    for r in (gpu, cpu):
+        r.set_spectrum(spec)
+    gpu.set_volume(vol)
+    gpu.set_material_tf(tf)
+    gpu.set_light(spd, ld)
+    gpu.set_params(**params)
+    cpu.volume, cpu.tf, cpu.light, cpu.light_dir = vol, tf, spd, ld
+    cpu.params.update(**params)
+
+
+@pytest.mark.parametrize("k", range(N_CASES // 4))
+def test_random_bands_bitexact(k):
+    """Mode B under random draws: the frame cut into 1-4 random row bands (whole
+    8-row tiles; the last band ends at R, which need not be a multiple of 8), one
+    handle per band; every band's rows equal the oracle's full frame and the band
+    images sum to the oracle's fp32 image, bit for bit."""
+    draw = _draw(200 + k)
+    R, mvp, what = draw[0], draw[8], draw[10]
+    rng = np.random.default_rng(7000 + k)
+    tiles = (R + 7) // 8
+    cuts = sorted(set(int(c) * 8 for c in rng.integers(1, tiles, int(rng.integers(0, 4))))) if tiles > 1 else []
+    edges = [0] + cuts + [R]
+    bands = list(zip(edges[:-1], edges[1:]))
+    print(what, "bands", bands)
+    cpu = orc.Oracle(R)
+    gpus = [vptmcm.Renderer(R, device=0, layout=draw[2]) for _ in bands]
+    try:
+        _setup_spectral(gpus[0], cpu, draw)
+        for g, (y0, y1) in zip(gpus[1:], bands[1:]):
+            _setup_spectral(g, orc.Oracle(R), draw)
+        for g, (y0, y1) in zip(gpus, bands):
+            g.set_band(y0, y1)
+        seeds = cf.seed_stream(5, start=10 * k + 7)
+        cpu.reset(mvp, seeds[0], nthreads=16)
+        for s in seeds[1:]:
+            rgb, want = cpu.render(mvp, s, nthreads=16)
+        acc = np.zeros((R, R, 3), np.float32)
+        for g, (y0, y1) in zip(gpus, bands):
+            g.reset(mvp, seeds[0])
+            g.render(mvp, seeds[1])
+            g.read_rgb()  # a read between passes: an unfused launch, then a fused one
+            g.render_passes(mvp, seeds[2:])
+            ph = g.read_photons().reshape(R, R, -1)[y0:y1].reshape(-1, 36)
+            assert_photons_equal(ph, cpu.photons.reshape(R, R, -1)[y0:y1].reshape(-1, 36),
+                                 f"{what} band {y0}:{y1}")
+            assert_rgba_equal(g.read_rgba16f()[y0:y1], want[y0:y1], f"{what} band {y0}:{y1}")
+            img = g.read_rgb()
+            assert not img[:y0].any() and not img[y1:].any()
+            acc += img
+        assert_rgb32_equal(acc, rgb, f"{what} band sum")
+    finally:
+        for g in gpus:
+            g.close()
