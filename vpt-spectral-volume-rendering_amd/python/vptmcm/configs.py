@@ -187,6 +187,8 @@ def algorithmic_bytes_per_pass(R: int, steps: int, nb: int = 12) -> int:
 def algorithmic_bytes_per_launch(R: int, steps: int, passes: int, nb: int = 12) -> int:
     """SURVEY 8(d), counting only what a launch materialises: a launch running
     `passes` passes back to back reads and writes the observable photon state
-    once, and stores one rgba16f image and gathers S 2x2x2 cells per photon per
-    pass: R^2 * (2*(40 + 4 nb) + passes*(8 + 8 S)). passes=1 is the per-pass formula."""
-    return R * R * (2 * (40 + 4 * nb) + passes * (8 + 8 * steps))
+    once, gathers S 2x2x2 cells per photon per pass, and stores one rgba16f
+    image (its last pass's: the passes of a launch are queued render() calls
+    with no read between them): R^2 * (2*(40 + 4 nb) + 8 + passes*8 S).
+    passes=1 is the per-pass formula."""
+    return R * R * (2 * (40 + 4 * nb) + 8 + passes * 8 * steps)
