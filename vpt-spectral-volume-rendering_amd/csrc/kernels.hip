@@ -415,6 +415,54 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   const bool rbpix = P.robust != 0u && fixed &&
                      (sx < P.rb_x0 || sx > P.rb_x1 || sy < P.rb_y0 || sy > P.rb_y1);
   bool rb = false, stale = false;
+  // add_radiance of a termination is deferred into the next step's gather
+  // shadow (it only touches the radiance bins, applied in the same order),
+  // across pass boundaries too: only the launch's last pass applies it at its
+  // end (for radiance_to_rgb and the state store).
+  float pend_n = 0.0f, pend_l = 0.0f;
+  // The pending bin as a byte one-hot: byte (bin & 3) of word bin >> 2 is 1,
+  // so each bin's 0/1 factor is one v_cvt_f32_ubyteN (no per-bin compare
+  // masks held in SGPRs). 0xffffffff (no bins) sets no byte.
+  uint32_t pend_oh[3] = {0u, 0u, 0u};
+  auto set_pending = [&](float n, float l, uint32_t bin) {
+    pend_n = n;
+    pend_l = l;
+    const uint32_t one = 1u << ((bin & 3u) << 3), wi = bin >> 2;
+    pend_oh[0] = wi == 0u ? one : 0u;
+    pend_oh[1] = wi == 1u ? one : 0u;
+    pend_oh[2] = wi == 2u ? one : 0u;
+  };
+  auto apply_pending = [&]() {
+    // Branch-free with a zero weight for lanes without a pending sample:
+    // fma(d, +0, r) == r for every finite r, and the radiance bins are
+    // finite in every state the march produces (convex combinations of
+    // finite light samples), so no per-bin select is needed. The target
+    // difference fma(oh, l, -r) is RN(l - r) for the pending bin and -r
+    // (exact) elsewhere: the same values as (tgt - r).
+    const bool on = pend_n != 0.0f;
+    const float inv = on ? rcp_in_range(on ? pend_n : 1.0f) : 0.0f;
+#pragma unroll
+    for (int b = 0; b < kMaxBins; b++) {
+      if (NBF || VPT_NB_ZERO || (uint32_t)b < P.nb) {
+        const float oh = (float)((pend_oh[b >> 2] >> ((b & 3) * 8)) & 0xffu);
+        p.rad[b] = fmaf(fmaf(oh, pend_l, -p.rad[b]), inv, p.rad[b]);
+      }
+    }
+    pend_n = 0.0f;
+    pend_oh[0] = pend_oh[1] = pend_oh[2] = 0u;
+  };
+  // exit or absorption: count the sample, defer its radiance, adopt the
+  // reset candidate (drawn from h1..h5) and continue from state h5
+  auto terminate = [&](float rad, const Photon& rc) {
+    p.samples++;
+    set_pending((float)p.samples, rad, p.bin);
+    p.pos = rc.pos;
+    p.dir = rc.dir;
+    p.bounces = 0u;
+    p.lambda = rc.lambda;
+    p.bin = rc.bin;
+    rb = rbpix;
+  };
   const uint32_t n_passes = PS.n;
   for (uint32_t pass = 0; pass < n_passes; pass++) {
 #if VPT_PRIO
@@ -426,52 +474,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   uint32_t st = hash3(x, y, pass_seed(pass));  // wgsl:122 (state is not carried across passes)
 
   if constexpr (SPEC) {
-    // add_radiance of a termination is deferred into the next step's gather
-    // shadow (it only touches the radiance bins, applied in the same order).
-    float pend_n = 0.0f, pend_l = 0.0f;
-    // The pending bin as a byte one-hot: byte (bin & 3) of word bin >> 2 is 1,
-    // so each bin's 0/1 factor is one v_cvt_f32_ubyteN (no per-bin compare
-    // masks held in SGPRs). 0xffffffff (no bins) sets no byte.
-    uint32_t pend_oh[3] = {0u, 0u, 0u};
-    auto set_pending = [&](float n, float l, uint32_t bin) {
-      pend_n = n;
-      pend_l = l;
-      const uint32_t one = 1u << ((bin & 3u) << 3), wi = bin >> 2;
-      pend_oh[0] = wi == 0u ? one : 0u;
-      pend_oh[1] = wi == 1u ? one : 0u;
-      pend_oh[2] = wi == 2u ? one : 0u;
-    };
-    auto apply_pending = [&]() {
-      // Branch-free with a zero weight for lanes without a pending sample:
-      // fma(d, +0, r) == r for every finite r, and the radiance bins are
-      // finite in every state the march produces (convex combinations of
-      // finite light samples), so no per-bin select is needed. The target
-      // difference fma(oh, l, -r) is RN(l - r) for the pending bin and -r
-      // (exact) elsewhere: the same values as (tgt - r).
-      const bool on = pend_n != 0.0f;
-      const float inv = on ? rcp_in_range(on ? pend_n : 1.0f) : 0.0f;
-#pragma unroll
-      for (int b = 0; b < kMaxBins; b++) {
-        if (NBF || VPT_NB_ZERO || (uint32_t)b < P.nb) {
-          const float oh = (float)((pend_oh[b >> 2] >> ((b & 3) * 8)) & 0xffu);
-          p.rad[b] = fmaf(fmaf(oh, pend_l, -p.rad[b]), inv, p.rad[b]);
-        }
-      }
-      pend_n = 0.0f;
-      pend_oh[0] = pend_oh[1] = pend_oh[2] = 0u;
-    };
-    // exit or absorption: count the sample, defer its radiance, adopt the
-    // reset candidate (drawn from h1..h5) and continue from state h5
-    auto terminate = [&](float rad, const Photon& rc) {
-      p.samples++;
-      set_pending((float)p.samples, rad, p.bin);
-      p.pos = rc.pos;
-      p.dir = rc.dir;
-      p.bounces = 0u;
-      p.lambda = rc.lambda;
-      p.bin = rc.bin;
-      rb = rbpix;
-    };
     for (uint32_t step = 0; step < P.steps; step++) {
       STAMP_RESTART();
       if (__builtin_amdgcn_ballot_w64(!rb) == 0ull) {
@@ -626,7 +628,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       STAMP_AT(4);
       STAMP_COUNT_STEP();
     }
-    apply_pending();
+    if (pass + 1u == n_passes) apply_pending();
   } else {
     for (uint32_t step = 0; step < P.steps; step++) {
       float dist = -spec_log(rnd_uniform(st)) * P.rcp_extinction;  // exponential.wgsl
