@@ -4,7 +4,7 @@ host enqueue of one 20-pass launch, the launch's GPU time (HIP events), and the
 synchronize, over repeated regions after clock settling. Analysis only.
 
     python tools/launch_latency.py [--passes 20] [--regions 30]
-(env VPTMCM_SYNC_SPIN=1: spin-waiting host synchronisation)
+(env VPTMCM_SYNC_SPIN=1: spin-waiting host synchronisation; --no-timing: no HIP events)
 """
 import argparse
 import json
@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--passes", type=int, default=20)
     ap.add_argument("--regions", type=int, default=30)
+    ap.add_argument("--no-timing", action="store_true", help="no HIP events in the region")
     a = ap.parse_args()
     r = vptmcm.Renderer(512, device=0)
     r.set_volume(cf.fbm_volume(512, 512))
@@ -44,20 +45,20 @@ def main():
     enq, syn, wall, kern = [], [], [], []
     for _ in range(a.regions):
         r.synchronize()
-        r.enable_kernel_timing(True)
+        r.enable_kernel_timing(not a.no_timing)
         t0 = time.perf_counter()
         r.render_passes(mvp, sd)
         t1 = time.perf_counter()
         r.synchronize()
         t2 = time.perf_counter()
-        k_ms, _ = r.kernel_time()
+        k_ms = r.kernel_time()[0] if not a.no_timing else float("nan")
         enq.append((t1 - t0) * 1e6)
         syn.append((t2 - t1) * 1e6)
         wall.append((t2 - t0) * 1e6)
         kern.append(k_ms * 1e3)
     r.close()
     med = lambda v: round(float(np.median(v)), 2)  # noqa: E731
-    print(json.dumps({"passes": a.passes, "enqueue_us": med(enq), "sync_us": med(syn),
+    print(json.dumps({"passes": a.passes, "timing": not a.no_timing, "enqueue_us": med(enq), "sync_us": med(syn),
                       "wall_us": med(wall), "kernel_region_us": med(kern),
                       "overhead_us": round(med(wall) - med(kern), 2)}))
 

@@ -69,11 +69,14 @@ struct vptmcm {
 
   // timing
   // Region timing: the first march launch after enable stamps `region.beg`
-  // from its own dispatch packet; synchronize / kernel_time enqueue
-  // `region.end` behind the last launch. Per-launch event pairs were measured
-  // to cost 1.6 us per fused pass (the markers' cache maintenance between
-  // back-to-back launches), so only the region is bracketed.
+  // from its own dispatch packet and every timed launch stamps `region.end`
+  // at its completion, so the last one closes the region (an end marker
+  // enqueued behind it cost 9-11 us of wall time per region). Per-launch
+  // event pairs were measured to cost 1.6 us per fused pass (the markers'
+  // cache maintenance between back-to-back launches), so only the region is
+  // bracketed.
   bool timing = false;
+  bool time_stop = true;  // the last launch stamps region.end itself (VPTMCM_TIME_STOP=0: a marker)
   bool region_closed = false;
   EventPair region;
   uint64_t launches = 0;
@@ -336,6 +339,10 @@ int time_slot(vptmcm* h, hipEvent_t* beg) {
 // Enqueue the region's end event behind the last timed launch (once).
 int time_close(vptmcm* h) {
   if (!h->timing || h->launches == 0 || h->region_closed) return VPTMCM_OK;
+  if (h->time_stop) {
+    h->region_closed = true;
+    return VPTMCM_OK;
+  }
   HIPCHK(h, hipEventRecord(h->region.end, h->stream));
   h->region_closed = true;
   return VPTMCM_OK;
@@ -352,6 +359,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   hipEvent_t eb = nullptr, ee = nullptr;
   int rc = time_slot(h, &eb);
   if (rc) return rc;
+  if (h->timing && h->time_stop) ee = h->region.end;
   const uint8_t* vol = h->layout != kLayoutLinear ? (const uint8_t*)h->vol_c8 : h->vol_lin;
   const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
   TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf};
@@ -445,6 +453,7 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   } else {
     (void)hipGetDevice(&h->device);
   }
+  if (const char* v = getenv("VPTMCM_TIME_STOP")) h->time_stop = v[0] != '0';
   h->layout = cfg->volume_layout;
   h->kind = cfg->renderer;
   if (const char* v = getenv("VPTMCM_MARCH_VARIANT")) h->variant = (uint32_t)strtoul(v, nullptr, 0);
