@@ -138,7 +138,8 @@ def _tf_many_rows_varying_b():
 def test_tf_modes_bitexact(variant, spec, tfname, monkeypatch):
     """The march specialisations chosen per launch — MODE 2 (FAST: row-invariant
     anisotropy), 3 (row-deduplicated LDS TF, 12 equal bins), 4 (deduplicated TF,
-    any bins), 1/0 (generic; variant bits 4/5 force them) — against the oracle,
+    any bins), 5 (more distinct rows than the deduplicated TF holds, any bins),
+    1/0 (generic; variant bits 4/5 force them) — against the oracle,
     bit for bit, over TFs with few distinct rows (the UI's materials, with
     constant and wavelength-varying anisotropy) and many rows with varying
     anisotropy (tf_b4 gather), for equal, uneven, few and wide bin layouts."""

@@ -313,6 +313,9 @@ __device__ __forceinline__ const __attribute__((address_space(4))) float* cmf_ta
 // branches vanish. 3: MODE 2's geometry, light and bins with a general TF
 // held row-deduplicated in LDS (wavelength-varying anisotropy: the UI's
 // materials, MaterialTransferFunction.js:56-75). 4: MODE 3 with any bin layout.
+// 5: MODE 2's geometry and light with any bin layout and a TF of more than
+// kTfRowsMax distinct rows (u16 LDS TF; anisotropy from the row table or the
+// tf_b4 gather).
 template <uint32_t L, bool SPEC, uint32_t MODE>
 __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const MarchParams P,
                                                        const TileSched T, float* __restrict__ ph,
@@ -325,10 +328,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
                                                        float* __restrict__ rgb32,
                                                        const uint8_t* __restrict__ tf_rowmap) {
   constexpr bool NBF = MODE >= 1u && MODE <= 3u;
-  constexpr bool GEO = MODE >= 2u;    // FAST geometry and light (MODE 2, 3, 4)
+  constexpr bool GEO = MODE >= 2u;    // FAST geometry and light (MODE 2 to 5)
   constexpr bool UNIB = MODE == 2u || MODE == 3u;  // ... and 12 equal-width bins
   constexpr bool FAST = MODE == 2u;   // ... and a row-invariant anisotropy channel
-  constexpr bool DEDUP = MODE >= 3u;  // ... or a row-deduplicated LDS TF (P.tf_dedup)
+  constexpr bool DEDUP = MODE == 3u || MODE == 4u;  // ... or a row-deduplicated LDS TF (P.tf_dedup)
   // (albedo, alpha) of the whole TF in LDS: every step's 4 TF taps become
   // ds_read_u16 instead of divergent L2 gathers. When the anisotropy channel
   // does not vary with wavelength (P.b_rows), its 256 row values sit in LDS
@@ -1106,6 +1109,8 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
       VPT_LAUNCH(LAY, SP, SP ? 3u : 1u); \
     else if (SP && geom && Q.tf_dedup) \
       VPT_LAUNCH(LAY, SP, SP ? 4u : 1u); \
+    else if (SP && geom)              \
+      VPT_LAUNCH(LAY, SP, SP ? 5u : 1u); \
     else if (nbf)                     \
       VPT_LAUNCH(LAY, SP, 1u);        \
     else                              \
