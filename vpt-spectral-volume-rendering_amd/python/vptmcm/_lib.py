@@ -158,6 +158,14 @@ class Renderer:
             raise VptError(rc, self.L.vptmcm_last_error(None).decode())
         self.h = h
         self.R = resolution
+        # Staging for the per-call hot-path arguments: numpy's .ctypes.data
+        # costs ~2 us per array, so the matrix and the seeds are copied into
+        # buffers whose addresses are taken once (the library copies both
+        # during the call).
+        self._m = np.zeros(16, np.float32)
+        self._m_p = self._m.ctypes.data
+        self._s = np.zeros(4096, np.uint32)
+        self._s_p = self._s.ctypes.data
 
     # -- lifetime
     def close(self) -> None:
@@ -230,14 +238,29 @@ class Renderer:
         m = mat_f32(mvp)
         self._ck(self.L.vptmcm_reset(self.h, _f32p(m), int(seed_bits) & 0xFFFFFFFF))
 
+    def _stage_matrix(self, mvp) -> int:
+        try:
+            self._m[:] = mvp  # 16 values (np.reshape alone costs ~1.7 us)
+        except ValueError:
+            self._m[:] = np.asarray(mvp, np.float32).ravel()  # e.g. a 4 x 4 matrix
+        return self._m_p
+
     def render(self, mvp, seed_bits: int) -> None:
-        m = mat_f32(mvp)
-        self._ck(self.L.vptmcm_render(self.h, m.ctypes.data, int(seed_bits) & 0xFFFFFFFF))
+        rc = self.L.vptmcm_render(self.h, self._stage_matrix(mvp), int(seed_bits) & 0xFFFFFFFF)
+        if rc != OK:
+            self._ck(rc)
 
     def render_passes(self, mvp, seeds) -> None:
-        m = mat_f32(mvp)
-        s = np.ascontiguousarray(seeds, dtype=np.uint32)
-        self._ck(self.L.vptmcm_render_passes(self.h, m.ctypes.data, s.ctypes.data, s.size))
+        n = len(seeds)
+        if n <= self._s.size:
+            self._s[:n] = seeds
+            sp = self._s_p
+        else:
+            s = np.ascontiguousarray(seeds, dtype=np.uint32)
+            sp = s.ctypes.data
+        rc = self.L.vptmcm_render_passes(self.h, self._stage_matrix(mvp), sp, n)
+        if rc != OK:
+            self._ck(rc)
 
     def synchronize(self) -> None:
         self._ck(self.L.vptmcm_synchronize(self.h))
