@@ -362,7 +362,12 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   bool entered = false;  // wave-uniform: some lane of this wave was inside the volume
   STAMP_BEGIN();
   Photon p;
-  if (live) load_photon(ph, S, i, p);  // issue the state loads before the LDS fill
+  // Photon state: the waves whose tile entered the volume last launch (the
+  // long ones) issue their loads before the LDS TF fill, the background waves
+  // after it, so the hot waves' state is not queued behind theirs (~1 % per
+  // launch).
+  const bool hot0 = P.sched != 0u || (tile != 0xffffffffu && T.flags_in[tile] != 0u);
+  if (live && hot0) load_photon(ph, S, i, p);
 #if VPT_NB_ZERO
   // Bins past nb (nb < 12) are never read or written by the reference
   // (wgsl:296, :310): their registers start at 0 and are left out of the final
@@ -387,6 +392,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     if (DEDUP || (!FAST && P.tf_dedup)) s_rowmap[threadIdx.x] = (uint32_t)tf_rowmap[threadIdx.x] * 256u;
   }
   __syncthreads();
+  if (live && !hot0) load_photon(ph, S, i, p);
   if (!live) {
     if (tile < P.n_tiles && lane == 0u) T.flags_out[tile] = 0u;  // an idle out-of-band tile
     return;
@@ -407,7 +413,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 #if VPT_PRIO
   // Waves whose tile entered the volume last pass are the long ones; they win
   // VALU issue arbitration over background waves, which have slack.
-  bool hot = (P.sched == 0u) ? (T.flags_in[tile] != 0u) : true;
+  bool hot = hot0;
 #endif
   // Robust-miss pixels (MarchParams::robust): once such a lane has been reset
   // with this launch's matrix its ray misses the cube by a margin, so every
