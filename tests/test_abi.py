@@ -46,3 +46,19 @@ def test_no_silent_cpu_fallback(monkeypatch, tmp_path):
     monkeypatch.setattr(vptmcm._lib, "LIB_DIR", tmp_path)
     with pytest.raises(RuntimeError, match="not built"):
         vptmcm._lib.load()
+
+
+def test_hot_path_argument_staging():
+    """Renderer stages the matrix and the seeds in buffers whose addresses are
+    taken once; every accepted matrix form lands as the same 16 floats
+    (row-major flattening of a 4 x 4, as np.reshape would give)."""
+    import numpy as np
+    from vptmcm import configs as cf
+
+    r = vptmcm.Renderer.__new__(vptmcm.Renderer)  # no device: staging only
+    r._m = np.zeros(16, np.float32)
+    r._m_p = r._m.ctypes.data
+    m = cf.default_mvp_inverse()
+    for form in (m, m.reshape(4, 4), [float(v) for v in m], m.astype(np.float64)):
+        assert r._stage_matrix(form) == r._m_p
+        assert np.array_equal(r._m.view(np.uint32), m.view(np.uint32))
