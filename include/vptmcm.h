@@ -164,8 +164,9 @@ int vptmcm_reset(vptmcm* h, const float* mvp_inverse /* 16 */, uint32_t seed_bit
  * render() calls with the same matrix are queued (up to 32) and launched as
  * one multi-pass march (photon state stays in registers between the passes)
  * as soon as any other entry point is called, so every observable result is
- * that of the passes run one by one. The no-volume error is still reported
- * here, synchronously. */
+ * that of the passes run one by one (a fused launch writes the render target
+ * once, for its last pass: the intermediate images could not be read). The
+ * no-volume error is still reported here, synchronously. */
 int vptmcm_render(vptmcm* h, const float* mvp_inverse /* 16 */, uint32_t seed_bits);
 
 /* n back-to-back passes with seeds[0..n) (one enqueue; for progressive
