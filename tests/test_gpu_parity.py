@@ -132,14 +132,15 @@ def _tf_many_rows_varying_b():
     return t
 
 
-@pytest.mark.parametrize("variant", ["0", "16", "32"])
+@pytest.mark.parametrize("variant", ["0", "16", "32", "64"])
 @pytest.mark.parametrize("spec", ["12", "8_uneven", "3", "12_wide"])
 @pytest.mark.parametrize("tfname", ["materials", "materials_const_b", "many_rows_b"])
 def test_tf_modes_bitexact(variant, spec, tfname, monkeypatch):
     """The march specialisations chosen per launch — MODE 2 (FAST: row-invariant
     anisotropy), 3 (row-deduplicated LDS TF, 12 equal bins), 4 (deduplicated TF,
     any bins), 5 (more distinct rows than the deduplicated TF holds, any bins),
-    1/0 (generic; variant bits 4/5 force them) — against the oracle,
+    6/7 (4/5 with the wavelength-bin table; variant bit 6 keeps 4/5), 1/0
+    (generic; variant bits 4/5 force them) — against the oracle,
     bit for bit, over TFs with few distinct rows (the UI's materials, with
     constant and wavelength-varying anisotropy) and many rows with varying
     anisotropy (tf_b4 gather), for equal, uneven, few and wide bin layouts."""

@@ -59,7 +59,8 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
                         const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba, float* rgb32,
                         hipStream_t s, hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr,
-                        const uint32_t* tf_rows = nullptr, const uint8_t* tf_rowmap = nullptr);
+                        const uint32_t* tf_rows = nullptr, const uint8_t* tf_rowmap = nullptr,
+                        const uint32_t* bin_lut = nullptr);
 // Artistic tone mapper uniforms, derived on the host from (low, mid, high,
 // saturation, gamma) (WebGPUArtisticToneMapper.js:81-88, ArtisticToneMapper.wgsl:40-46).
 struct ToneParams {

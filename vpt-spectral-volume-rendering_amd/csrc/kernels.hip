@@ -326,12 +326,14 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
                                                        const uint8_t* __restrict__ light,
                                                        uint16_t* __restrict__ rgba,
                                                        float* __restrict__ rgb32,
-                                                       const uint8_t* __restrict__ tf_rowmap) {
+                                                       const uint8_t* __restrict__ tf_rowmap,
+                                                       const uint32_t* __restrict__ bin_lut) {
   constexpr bool NBF = MODE >= 1u && MODE <= 3u;
   constexpr bool GEO = MODE >= 2u;    // FAST geometry and light (MODE 2 to 5)
   constexpr bool UNIB = MODE == 2u || MODE == 3u;  // ... and 12 equal-width bins
   constexpr bool FAST = MODE == 2u;   // ... and a row-invariant anisotropy channel
-  constexpr bool DEDUP = MODE == 3u || MODE == 4u;  // ... or a row-deduplicated LDS TF (P.tf_dedup)
+  constexpr bool DEDUP = MODE == 3u || MODE == 4u || MODE == 6u;  // ... or a row-deduplicated LDS TF
+  constexpr bool LUTB = MODE >= 6u;   // MODE 4 / 5 with the wavelength-bin table (P.bins_lut)
   // (albedo, alpha) of the whole TF in LDS: every step's 4 TF taps become
   // ds_read_u16 instead of divergent L2 gathers. When the anisotropy channel
   // does not vary with wavelength (P.b_rows), its 256 row values sit in LDS
@@ -341,6 +343,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __shared__ float s_light[256];
   __shared__ float s_brow[256];
   __shared__ uint32_t s_rowmap[256];  // P.tf_dedup: density row -> first texel of its distinct row
+  __shared__ uint32_t s_binlut[LUTB ? kBinLutCells + kBinLutCells / 4 : 1];  // MODE 6 / 7
 
   __shared__ uint32_t s_red[17];
   __shared__ uint32_t s_tile[16];
@@ -390,6 +393,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     s_light[threadIdx.x] = (float)light[threadIdx.x];
     s_brow[threadIdx.x] = (float)tf_brow[threadIdx.x];
     if (DEDUP || (!FAST && P.tf_dedup)) s_rowmap[threadIdx.x] = (uint32_t)tf_rowmap[threadIdx.x] * 256u;
+  }
+  if constexpr (LUTB) {
+    for (uint32_t k = threadIdx.x; k < kBinLutCells + kBinLutCells / 4; k += kMarchBlock)
+      s_binlut[k] = bin_lut[k];
   }
   __syncthreads();
   if (live && !hot0) load_photon(ph, S, i, p);
@@ -499,7 +506,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         p.dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
         p.bounces = 0u;
         p.lambda = lambda_of(P, h5);
-        p.bin = bin_of<UNIB>(P, p.lambda);
+        p.bin = bin_of_draw<UNIB, LUTB>(P, p.lambda, h5, s_binlut);
         wc = wave_const(p.lambda, s_light);
         st = h5;
         stale = true;
@@ -535,7 +542,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         float dx = 0.0f, dy = 0.0f;
         if (!fixed) disk_of(h1, h2, dx, dy);
         Photon rc;
-        reset_from_draws<GEO, UNIB>(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
+        reset_from_draws<GEO, UNIB, LUTB>(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf,
+                                          s_binlut);
         terminate(exit_radiance<GEO>(P, p.dir, wc), rc);
         wc = wave_const(rc.lambda, s_light);
         st = h5;
@@ -562,7 +570,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       disk_of(h1, h2, dx, dy);
       Photon rc;
       WaveConst wcr = wc;
-      reset_from_draws<GEO, UNIB>(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf);
+      reset_from_draws<GEO, UNIB, LUTB>(P, rc, sx, sy, fixed, from, dx, dy, h3, h4, h5, slab_hw, omf,
+                                          s_binlut);
       wcr = wave_const(rc.lambda, s_light);
       float nrm = fmaf(dy, dy, dx * dx);  // sphere.wgsl
       float srad = 2.0f * sqrt_z(1.0f - nrm);
@@ -1085,7 +1094,7 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
                         const TileSched& T, float* ph, const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba, float* rgb32,
                         hipStream_t s, hipEvent_t ev_beg, hipEvent_t ev_end,
-                        const uint32_t* tf_rows, const uint8_t* tf_rowmap) {
+                        const uint32_t* tf_rows, const uint8_t* tf_rowmap, const uint32_t* bin_lut) {
   dim3 grid(tile_blocks(P, kMarchBlock));
   // variant bits (analysis; results identical; bits 1-3 are the host's):
   // 0 plain (non-speculative) step, 4 none of the GEO specialisations (MODE 1
@@ -1100,27 +1109,33 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   // (P.tf_dedup on entry: the host found <= kTfRowsMax distinct rows)
   MarchParams Q = P;
   Q.tf_dedup = (P.tf_dedup && tf_rows && tf_rowmap && spec && !fast) ? 1u : 0u;
+  // MODE 4 / 5 -> 6 / 7 with the wavelength-bin table (variant bit 6: without)
+  const bool lut = P.bins_lut && bin_lut && (variant & 64u) == 0u;
   const uint16_t* tf_lds = Q.tf_dedup ? reinterpret_cast<const uint16_t*>(tf_rows) : tf_rg;
   const uint8_t* rowmap = tf_rowmap ? tf_rowmap : tf_brow;
   // hipExtLaunchKernelGGL stamps the events from the dispatch packet itself
   // (no extra barrier/marker packets between back-to-back launches)
 #define VPT_LAUNCH(LAY, SP, MO)                                                                \
   hipExtLaunchKernelGGL((k_march<LAY, SP, MO>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
-                        PS, Q, T, ph, vol, tf_lds, tf_b4, tf_brow, light, rgba, rgb32, rowmap)
-#define VPT_LAUNCH_NB(LAY, SP)        \
-  do {                                \
-    if (SP && fast)                   \
-      VPT_LAUNCH(LAY, SP, SP ? 2u : 1u); \
-    else if (SP && geo && Q.tf_dedup) \
-      VPT_LAUNCH(LAY, SP, SP ? 3u : 1u); \
-    else if (SP && geom && Q.tf_dedup) \
-      VPT_LAUNCH(LAY, SP, SP ? 4u : 1u); \
-    else if (SP && geom)              \
-      VPT_LAUNCH(LAY, SP, SP ? 5u : 1u); \
-    else if (nbf)                     \
-      VPT_LAUNCH(LAY, SP, 1u);        \
-    else                              \
-      VPT_LAUNCH(LAY, SP, 0u);        \
+                        PS, Q, T, ph, vol, tf_lds, tf_b4, tf_brow, light, rgba, rgb32, rowmap, bin_lut)
+#define VPT_LAUNCH_NB(LAY, SP)                 \
+  do {                                         \
+    if (SP && fast)                            \
+      VPT_LAUNCH(LAY, SP, SP ? 2u : 1u);       \
+    else if (SP && geo && Q.tf_dedup)          \
+      VPT_LAUNCH(LAY, SP, SP ? 3u : 1u);       \
+    else if (SP && geom && Q.tf_dedup && lut)  \
+      VPT_LAUNCH(LAY, SP, SP ? 6u : 1u);       \
+    else if (SP && geom && Q.tf_dedup)         \
+      VPT_LAUNCH(LAY, SP, SP ? 4u : 1u);       \
+    else if (SP && geom && lut)                \
+      VPT_LAUNCH(LAY, SP, SP ? 7u : 1u);       \
+    else if (SP && geom)                       \
+      VPT_LAUNCH(LAY, SP, SP ? 5u : 1u);       \
+    else if (nbf)                              \
+      VPT_LAUNCH(LAY, SP, 1u);                 \
+    else                                       \
+      VPT_LAUNCH(LAY, SP, 0u);                 \
   } while (0)
   if (layout == kLayoutBrick8 && P.vol32) {
     if (spec) VPT_LAUNCH_NB(kTplBrick8, true); else VPT_LAUNCH_NB(kTplBrick8, false);

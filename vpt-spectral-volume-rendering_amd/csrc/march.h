@@ -98,7 +98,15 @@ struct MarchParams {
   // anisotropy << 16) and s_rowmap maps a density row to its distinct row, so
   // the anisotropy taps come from LDS with albedo and alpha (no tf_b4 gather).
   uint32_t tf_dedup;
+  // The bin as a function of the wavelength draw h5 (lambda_of is monotone in
+  // h5 and the bin in lambda, so bin(h5) is a step function): per cell of
+  // 2^22 draws the bin at the cell start and the one threshold inside it,
+  // host-built and exact (kBinLutCells u32 thresholds, then as many bytes of
+  // base | count << 4). Set when no cell holds two distinct thresholds.
+  uint32_t bins_lut;
 };
+constexpr uint32_t kBinLutCells = 1024u;
+constexpr uint32_t kBinLutShift = 22u;
 
 // ---------------------------------------------------------------- RNG draws
 // disk.wgsl from its two hash draws
@@ -316,13 +324,29 @@ __device__ __forceinline__ float lambda_of(const MarchParams& P, uint32_t h5) {
   return fmaf((float)h5 * 2.3283064365386963e-10f, P.max_lam - P.min_lam, P.min_lam);
 }
 
+// bin_of(lambda_of(h5)); LUTB: from the LDS copy of MarchParams::bins_lut's
+// table (lut: kBinLutCells thresholds, then the base | count << 4 bytes).
+template <bool UNIB = false, bool LUTB = false>
+__device__ __forceinline__ uint32_t bin_of_draw(const MarchParams& P, float lambda, uint32_t h5,
+                                                const uint32_t* lut) {
+  if constexpr (LUTB) {
+    const uint32_t c = h5 >> kBinLutShift;
+    const uint32_t t = lut[c];
+    const uint32_t bk = reinterpret_cast<const uint8_t*>(lut + kBinLutCells)[c];
+    return (bk & 15u) + (h5 >= t ? (bk >> 4) : 0u);
+  } else {
+    return bin_of<UNIB>(P, lambda);
+  }
+}
+
 // UNI: blur 0, even R and a host-bounded |w| (fixed near points, one-compare
 // reciprocal guard); UNIB: equal-width bins (bin_of's arithmetic path).
-template <bool UNI = false, bool UNIB = UNI>
+template <bool UNI = false, bool UNIB = UNI, bool LUTB = false>
 __device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p, float sx, float sy,
                                                  bool fixed_from, f3 from, float dx, float dy,
                                                  uint32_t h3, uint32_t h4, uint32_t h5,
-                                                 bool slab_hw = false, f3 omf = f3{0.0f, 0.0f, 0.0f}) {
+                                                 bool slab_hw = false, f3 omf = f3{0.0f, 0.0f, 0.0f},
+                                                 const uint32_t* lut = nullptr) {
   // UNI launches have blur == 0 and an even R, so every near point is fixed
   // (screen coordinates of pixel centres are never 0 then)
   if constexpr (!UNI) {
@@ -334,7 +358,7 @@ __device__ __forceinline__ void reset_from_draws(const MarchParams& P, Photon& p
   else
     p.pos = ray_start(from, p.dir);
   p.lambda = lambda_of(P, h5);
-  p.bin = bin_of<UNIB>(P, p.lambda);
+  p.bin = bin_of_draw<UNIB, LUTB>(P, p.lambda, h5, lut);
 }
 
 __device__ __forceinline__ void screen_of(const MarchParams& P, uint32_t x, uint32_t y, float& sx,

@@ -53,6 +53,9 @@ struct vptmcm {
   uint8_t* tf_brow = nullptr;  // 256 anisotropy rows (valid when b_rows)
   uint32_t* tf_rows = nullptr;   // kTfRowsMax distinct TF rows, u32 texels (valid when tf_dedup)
   uint8_t* tf_rowmap = nullptr;  // density row -> distinct row
+  uint32_t* bin_lut = nullptr;   // MarchParams::bins_lut table (device)
+  bool bin_lut_ok = false;
+  uint32_t bin_lut_host[kBinLutCells + kBinLutCells / 4] = {};
   uint32_t tf_dedup = 0;
   uint32_t b_rows = 1;         // zero TF: column-invariant
   uint8_t* light = nullptr;    // 256 bytes
@@ -275,6 +278,7 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
   }
   P.b_rows = h->b_rows;
   P.tf_dedup = h->tf_dedup;
+  P.bins_lut = h->bin_lut_ok ? 1u : 0u;
   {  // |w| bound for unproject<true>: |a|, |b| <= 1 + max(2/R, |blur|) + 1 (slop)
     const double A = 2.0 + std::max(2.0 / h->R, std::fabs((double)P.blur));
     bool fin = true;
@@ -321,6 +325,80 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
 }
 
 int check_handle(vptmcm* h) { return h ? VPTMCM_OK : VPTMCM_EINVAL; }
+
+// MarchParams::bins_lut (march MODE 6 / 7): the wavelength bin as a step
+// function of the draw h5. lambda_of(h5) = fma(f32(h5) * 2^-32, max - min,
+// min) is monotone in h5 when max >= min (every operation rounds
+// monotonically) and bin_of counts the padded boundaries b_i with
+// !(lambda < b_i), so bin(h5) = #{i : h5 >= T_i}, T_i the first h5 whose
+// lambda reaches b_i, found by bisection on the f32 expression the kernel
+// evaluates. Per cell of 2^22 draws the table holds the bin at the cell start
+// and the one threshold inside the cell; boundaries closer than about
+// (max - min) / 1024 (two distinct thresholds in one cell) keep the
+// comparison search. The table is checked against bin_of's rule at every
+// threshold and its neighbours and on a 2^16-point grid before it is enabled.
+int build_bin_lut(vptmcm* h) {
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));  // no launch still reads the table
+  h->bin_lut_ok = false;
+  const float ident[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+  const MarchParams Q = make_params(h, ident, 0u);
+  if (!Q.bins_sorted || !Q.bins_padded || !(Q.max_lam >= Q.min_lam)) return VPTMCM_OK;
+  const float d = Q.max_lam - Q.min_lam, mn = Q.min_lam;
+  auto lam = [&](uint64_t v) { return std::fmaf((float)(uint32_t)v * 2.3283064365386963e-10f, d, mn); };
+  auto bin_rule = [&](uint64_t v) {  // bin_of's padded search
+    const float l = lam(v);
+    uint32_t b = 0u;
+    for (int i = 1; i < kMaxBins; i++) b += !(l < Q.lam_pad[i]) ? 1u : 0u;
+    return b;
+  };
+  uint64_t T[kMaxBins];
+  int nt = 0;
+  for (int i = 1; i < kMaxBins; i++) {
+    const float b = Q.lam_pad[i];
+    if (!std::isfinite(b)) continue;  // the +inf padding never counts
+    uint64_t lo = 0, hi = 1ull << 32;  // first v in [0, 2^32) with !(lam(v) < b), else 2^32
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) / 2;
+      if (!(lam(mid) < b)) hi = mid; else lo = mid + 1;
+    }
+    T[nt++] = lo;
+  }
+  uint32_t* thr = h->bin_lut_host;
+  uint8_t* bk = reinterpret_cast<uint8_t*>(h->bin_lut_host + kBinLutCells);
+  for (uint32_t c = 0; c < kBinLutCells; c++) {
+    const uint64_t c0 = (uint64_t)c << kBinLutShift, c1 = c0 + (1ull << kBinLutShift);
+    uint32_t base = 0u, k = 0u;
+    uint64_t t = 0;
+    for (int j = 0; j < nt; j++) {
+      if (T[j] <= c0) {
+        base++;
+      } else if (T[j] < c1) {
+        if (k && T[j] != t) return VPTMCM_OK;  // two distinct thresholds in one cell
+        t = T[j];
+        k++;
+      }
+    }
+    thr[c] = k ? (uint32_t)t : 0u;
+    bk[c] = (uint8_t)(base | (k << 4));
+  }
+  auto lut_bin = [&](uint64_t v) {
+    const uint32_t c = (uint32_t)(v >> kBinLutShift);
+    return (bk[c] & 15u) + ((uint32_t)v >= thr[c] ? (bk[c] >> 4) : 0u);
+  };
+  for (int j = 0; j < nt; j++)
+    for (int64_t e = -2; e <= 2; e++) {
+      const int64_t v = (int64_t)T[j] + e;
+      if (v >= 0 && v < (1ll << 32) && lut_bin((uint64_t)v) != bin_rule((uint64_t)v)) return VPTMCM_OK;
+    }
+  for (uint64_t v = 0; v < (1ull << 32); v += 0x10001ull)
+    if (lut_bin(v) != bin_rule(v)) return VPTMCM_OK;
+  HIPCHK(h, hipMemcpyAsync(h->bin_lut, h->bin_lut_host, sizeof h->bin_lut_host,
+                           hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->bin_lut_ok = true;
+  return VPTMCM_OK;
+}
 
 // The start event of the next march launch: the region's begin event for the
 // first timed launch (stamped by the dispatch packet itself), else none.
@@ -370,7 +448,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   else
     HIPCHK(h, launch_march(h->layout, h->variant, P, PS, T, h->photons, vol, h->tf_rg, h->tf_b4,
                            h->tf_brow, h->light, h->rgba, h->rgb32, h->stream, eb, ee, h->tf_rows,
-                           h->tf_rowmap));
+                           h->tf_rowmap, h->bin_lut));
   h->sched_cur = c ^ 1u;
   return VPTMCM_OK;
 }
@@ -487,6 +565,8 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   CK(hipMemsetAsync(h->tf_brow, 0, 256, h->stream));
   CK(hipMalloc(&h->tf_rows, kTfRowsMax * 256 * sizeof(uint32_t)));
   CK(hipMemsetAsync(h->tf_rows, 0, kTfRowsMax * 256 * sizeof(uint32_t), h->stream));
+  CK(hipMalloc(&h->bin_lut, sizeof h->bin_lut_host));
+  CK(hipMemsetAsync(h->bin_lut, 0, sizeof h->bin_lut_host, h->stream));
   CK(hipMalloc(&h->tf_rowmap, 256));
   CK(hipMemsetAsync(h->tf_rowmap, 0, 256, h->stream));
   CK(hipMalloc(&h->light, 256));
@@ -528,6 +608,7 @@ void vptmcm_destroy(vptmcm* h) {
   if (h->tf_brow) (void)hipFree(h->tf_brow);
   if (h->tf_rows) (void)hipFree(h->tf_rows);
   if (h->tf_rowmap) (void)hipFree(h->tf_rowmap);
+  if (h->bin_lut) (void)hipFree(h->bin_lut);
   if (h->light) (void)hipFree(h->light);
   if (h->sched) (void)hipFree(h->sched);
   if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
@@ -715,7 +796,7 @@ int vptmcm_set_spectrum(vptmcm* h, const float* buf) {
   if (!(nbf >= 0.0f) || nbf >= (float)(VPTMCM_MAX_BINS + 1))
     FAIL(h, VPTMCM_EINVAL, "set_spectrum: n_bins = %g exceeds MAX_N_BINS (12)", (double)buf[0]);
   memcpy(h->spectrum, buf, sizeof h->spectrum);
-  return VPTMCM_OK;
+  return build_bin_lut(h);
 }
 
 int vptmcm_set_transfer_function(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height) {
