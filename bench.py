@@ -360,8 +360,8 @@ def main():
             traffic, issue = None, None
 
     # The march on a UI-like configuration of the same volume: 8 uneven bins and
-    # a materials TF with wavelength-varying anisotropy (MODE 4: FAST geometry,
-    # the TF's distinct rows in LDS, the general bin search)
+    # a materials TF with wavelength-varying anisotropy (MODE 6: FAST geometry,
+    # the TF's distinct rows and the exact wavelength-bin table in LDS)
     general = None
     if a.general_steps > 0 and not multi:
         r.synchronize()
@@ -384,7 +384,8 @@ def main():
                                           if not a.no_timing else None),
                    "workload": "same volume/camera, tf_materials(varying anisotropy), "
                                "8_uneven bins: a UI-like TF (row-deduplicated in LDS) and "
-                               "uneven bins, march MODE 4 (MODE 2 is the headline's)"}
+                               "uneven bins (exact bin table in LDS), march MODE 6 (MODE 2 is the "
+                               "headline's)"}
 
     # The RGB sibling ('mcm-compute') on the same volume and camera:
     # a 256 x 1 sRGB TF ramp, HG anisotropy 0.7, white 1x1 environment

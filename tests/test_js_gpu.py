@@ -154,7 +154,7 @@ def test_js_ui_models_drive_renderer_bitexact(tmp_path):
     """The headless UI models (js/ui.js: MaterialTransferFunction, SpectrumRepresentation
     with exponential markers, LightEditor) wired to the renderer: every model change resets
     (js:116-125), the first render uploads their spectrum; the materials TF has few distinct
-    rows and 8 uneven bins, so the march runs its deduplicated-TF MODE 4. Bit-exact vs the
+    rows and 8 uneven bins, so the march runs its deduplicated-TF, bin-table MODE 6. Bit-exact vs the
     oracle replaying the same inputs."""
     col = list(range(60, 60 + 256))
     ui = {"materials": [{"albedo": 180, "alpha": 60, "anisotropy": 127, "rows": [20, 89]},
