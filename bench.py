@@ -81,6 +81,10 @@ def parse():
                     help="passes of a third timed region through the drop-in render() entry "
                          "point, one call per pass (lazily fused by the library; reported as "
                          "'render_api'; 0 = skip; N = 1 only)")
+    ap.add_argument("--js-steps", type=int, default=256,
+                    help="passes of a timed region driven from Node through the drop-in JS "
+                         "renderer (MCMSpectralComputeRenderer.render() per pass over N-API; "
+                         "reported as 'js_api'; 0 = skip; N = 1 only)")
     ap.add_argument("--no-timing", action="store_true",
                     help="diagnostics: no per-launch kernel timestamps (wall clock only; the "
                          "roofline fields are then null)")
@@ -108,10 +112,15 @@ def cpu_baseline(vol, tf, spec, spd, ldir, mvp, R, S, ext, budget_s):
     import js_march  # test-infrastructure restatement, timed here as the CPU baseline
     import oracle as orc  # test-infrastructure checker, timed as the secondary baseline
 
-    # the GPU box's per-GPU CPU share is 16 cores (OMP_NUM_THREADS there); the
-    # machine reports many more, which belong to the other GPUs' jobs
+    # threads = the CPUs in this process's affinity mask, capped by
+    # OMP_NUM_THREADS when set; the machine may report many more CPUs
     threads = cf.host_threads()
-    share = f"{threads} of {os.cpu_count()} host CPUs (the per-GPU CPU share)"
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count()
+    share = (f"{threads} threads: affinity mask {aff} CPUs, OMP_NUM_THREADS="
+             f"{os.environ.get('OMP_NUM_THREADS', 'unset')}, os.cpu_count() {os.cpu_count()}")
     out = None
     if js_march.node():
         j = js_march.run_bench(R, vol, tf, spd, ldir, spec, mvp, cf.seed_stream(64, start=0),
@@ -145,6 +154,38 @@ def cpu_baseline(vol, tf, spec, spd, ldir, mvp, R, S, ext, budget_s):
     else:
         out["c_port"] = c_port
     return out
+
+
+def js_api_line(vol, tf, spec, R, S, ext, passes, settle_ms):
+    """The north_star host: Node drives MCMSpectralComputeRenderer (js/) with one
+    render() per pass, as the reference's rendering loop does, over the N-API
+    shim into the same library (tools/js_render_bench.js). Runs in its own
+    process on the same GPU after this process's regions have drained."""
+    import shutil
+    import subprocess
+    import tempfile
+    if shutil.which("node") is None:
+        return None
+    with tempfile.TemporaryDirectory(prefix="vptmcm-js-") as d:
+        d = Path(d)
+        np.ascontiguousarray(vol).tofile(d / "vol.raw")
+        np.ascontiguousarray(tf, np.uint8).tofile(d / "tf.bin")
+        np.ascontiguousarray(spec, np.float32).tofile(d / "spec.bin")
+        D, H, W = vol.shape
+        case = dict(R=R, W=W, H=H, D=D, volume_path=str(d / "vol.raw"), tf_path=str(d / "tf.bin"),
+                    spectrum_path=str(d / "spec.bin"), extinction=ext, steps=S,
+                    settle_ms=settle_ms, warmup=64, passes=passes)
+        (d / "case.json").write_text(json.dumps(case))
+        p = subprocess.run(["node", str(REPO / "tools" / "js_render_bench.js"), str(d / "case.json")],
+                           capture_output=True, text=True, timeout=300)
+    if p.returncode != 0:
+        raise RuntimeError(f"js_render_bench.js failed ({p.returncode}): {p.stderr[-2000:]}")
+    j = json.loads(p.stdout.strip().splitlines()[-1])
+    return {"value": round(j["value"], 3), "ms_per_step": round(j["ms_per_step"], 5),
+            "steps": j["steps"], "launches": j["launches"],
+            "note": f"node {j['node']}: MCMSpectralComputeRenderer.render() once per pass (each "
+                    "re-sending the unchanged uniforms, as the reference does) over N-API; the "
+                    "library fuses the queued passes into 32-pass launches"}
 
 
 def main():
@@ -424,6 +465,11 @@ def main():
                            "camera: 256x1 sRGB TF ramp, anisotropy 0.7, white environment"}
         q.close()
 
+    r.synchronize()
+    js_api = None
+    if a.js_steps > 0 and not multi and a.tf == "spectral" and a.camera == "default":
+        js_api = js_api_line(vol, tf, spec, R, S, a.extinction, a.js_steps, a.settle_ms)
+
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mphoton-steps/s",
@@ -458,6 +504,7 @@ def main():
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "unfused": unfused,
             "render_api": render_api,
+            "js_api": js_api,
             "general": general,
             "rgb": rgb,
             "per_pass_allreduce": per_pass,

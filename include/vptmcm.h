@@ -141,7 +141,9 @@ int vptmcm_set_transfer_function(vptmcm* h, const uint8_t* rgba, uint32_t width,
 int vptmcm_set_environment(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height);
 
 /* The scalar render uniforms, js:296-306 (the RGB renderer also reads
- * anisotropy, MCMComputeRenderer.wgsl:140). */
+ * anisotropy, MCMComputeRenderer.wgsl:140). The reference rewrites them before
+ * every pass; values identical (bit for bit) to the current ones are a no-op
+ * and do not end the queue of fused render() passes. */
 int vptmcm_set_params(vptmcm* h, const vptmcm_params* p);
 
 /* Image band (SURVEY 8e "Mode B"): restrict reset and render to the pixel rows
@@ -234,7 +236,13 @@ int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches);
 /* ncclGetUniqueId on rank 0; the caller ships the 128 bytes to other ranks. */
 int vptmcm_comm_unique_id(uint8_t* out /* 128 */);
 
-/* ncclCommInitRank on the handle's device. */
+/* Non-blocking ncclCommInitRankConfig on the handle's device. Every wait on
+ * the communicator (this init, an RCCL enqueue in progress, synchronize and
+ * the composite reads while RCCL work is queued) polls ncclCommGetAsyncError
+ * and is bounded by VPTMCM_COMM_TIMEOUT_MS (environment, read here; default
+ * 120000): on an asynchronous error or the timeout the communicator is
+ * aborted (ncclCommAbort) and the call returns VPTMCM_ECOMM, so a dead or
+ * hung peer ends every rank instead of hanging it. */
 int vptmcm_comm_init(vptmcm* h, const uint8_t* unique_id, int nranks, int rank);
 
 /* Enqueue the cross-rank radiance composite of the current pass:
@@ -249,7 +257,10 @@ int vptmcm_comm_read_composite(vptmcm* h, float* rgb, float* counts);
 
 /* Mode B composite: sum over ranks of the fp32 radiance_to_rgb image (each
  * rank's rows outside its band are zero, so the sum IS the single-GPU image,
- * bit for bit); rgb = R*R*3 floats. Synchronous. */
+ * bit for bit up to the sign of a -0.0 pixel, which comes back +0.0);
+ * rgb = R*R*3 floats. The ranks' bands are all-reduced first and must tile
+ * the frame (every 8-row tile in exactly one band), else VPTMCM_ECOMM.
+ * Synchronous. */
 int vptmcm_comm_gather_bands(vptmcm* h, float* rgb);
 
 /* Blocking host-side helpers over the communicator (barrier, max/sum of a
@@ -274,6 +285,15 @@ int vptmcm_debug_eval(vptmcm* h, int fn, const uint32_t* in, uint32_t* out, uint
  * selected for the current spectrum. */
 int vptmcm_debug_verify(vptmcm* h, int fn, uint32_t lo, uint64_t count, uint64_t* mismatches,
                         uint32_t* first_bad, uint32_t nfirst);
+
+/* What the last march launch ran (after launching any queued render() passes):
+ * info[0] the march specialisation (MODE 0-7 of the spectral kernel, see
+ * DESIGN.md; RGB renderer: 1 with the fast geometry, else 0), info[1] the
+ * volume layout template (0 linear, 1 corner8, 2 corner8 with 64-bit offsets,
+ * 3 brick8, 4 brick8 with 64-bit offsets), info[2] 1 for the speculative step
+ * loop, info[3] the passes fused into it; *launches (may be NULL) counts every
+ * march launch since create. */
+int vptmcm_debug_last_launch(vptmcm* h, uint32_t info[4], uint64_t* launches);
 
 /* Library version string. */
 const char* vptmcm_version(void);

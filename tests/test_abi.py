@@ -62,3 +62,8 @@ def test_hot_path_argument_staging():
     for form in (m, m.reshape(4, 4), [float(v) for v in m], m.astype(np.float64)):
         assert r._stage_matrix(form) == r._m_p
         assert np.array_equal(r._m.view(np.uint32), m.view(np.uint32))
+    # a scalar or a short array must not broadcast into all 16 entries
+    for bad in (1.0, np.ones(1, np.float32), np.ones(4, np.float32), np.ones((4, 1), np.float32),
+                [1.0] * 15):
+        with pytest.raises(ValueError, match="16 values"):
+            r._stage_matrix(bad)

@@ -2,9 +2,10 @@
 
 Each rank renders its own replica of the frame with its rank seed stream
 (configs.seed_bits(k, rank); rank 0 == the 1-GPU stream) using the CPU oracle,
-packs (rgb*n, n) per pixel exactly as k_pack does (rgb decoded from the
-rgba16f target, n = photon sample count), all-reduces over gloo and checks
-the composite against the single-process sum of both replicas.
+packs (rgb*n, n) per pixel exactly as k_pack does (rgb = the last pass's fp32
+radiance_to_rgb image, read_rgb; n = photon sample count; f32 products),
+all-reduces over gloo and checks the composite against the single-process sum
+of both replicas.
 """
 import os
 
@@ -27,10 +28,10 @@ def _replica(rank):
     mvp = cf.default_mvp_inverse()
     o.reset(mvp, cf.seed_bits(0, rank), nthreads=1)
     for k in range(1, 4):
-        _, rgba = o.render(mvp, cf.seed_bits(k, rank), nthreads=1)
+        rgb, _ = o.render(mvp, cf.seed_bits(k, rank), nthreads=1)
     n = o.photons[:, 7].astype(np.float32).reshape(R, R)
-    rgb = rgba[..., :3].view(np.float16).astype(np.float32)
-    return np.concatenate([rgb * n[..., None], n[..., None]], axis=-1)
+    rgb = np.asarray(rgb, np.float32).reshape(R, R, 3)
+    return np.concatenate([rgb * n[..., None], n[..., None]], axis=-1).astype(np.float32)
 
 
 def _run(rank, world, port, out):

@@ -19,6 +19,9 @@ from test_gpu_parity import assert_photons_equal, assert_rgb32_equal, assert_rgb
 pytestmark = pytest.mark.gpu
 
 N_CASES = 96
+# (MODE, layout template) pairs the random cases' fused launches ran
+# (vptmcm_debug_last_launch); test_mode_template_coverage forces the rest
+HIT = set()
 
 
 def _perspective_inverse(rng, inside=False):
@@ -154,6 +157,9 @@ def test_random_configuration_bitexact(k):
         assert_photons_equal(gpu.read_photons(), cpu.photons, f"{what} fused")
         assert_rgba_equal(gpu.read_rgba16f(), want, f"{what} fused")
         assert_rgb32_equal(gpu.read_rgb(), rgb, f"{what} fused")
+        info = gpu.last_launch()
+        assert info["passes"] == 3 and info["spec"], info
+        HIT.add((info["mode"], info["tpl"]))
 
 
 def _same_words(a, b):
@@ -257,3 +263,84 @@ def test_random_bands_bitexact(k):
     finally:
         for g in gpus:
             g.close()
+
+
+def _close_bins():
+    """3 bins whose inner boundaries (500.1, 500.15 nm) put two distinct
+    thresholds in one cell of the wavelength-bin table: the table is refused and
+    the comparison search runs (MODE 4 / 5 instead of 6 / 7)."""
+    buf = np.zeros(64, np.float32)
+    buf[:1 + 4 + 9] = [3, 450.0, 500.1, 500.15, 650.0, 0.3, 1.1, 0.7, 0.2, 0.9, 1.4, 1.6, 0.1, 0.4]
+    return buf
+
+
+# the inputs that make launch_march select each MODE (see its dispatcher and
+# DESIGN.md section 5): TF, bin layout, light direction
+_MODE_INPUTS = {
+    2: ("spectral", "12", False),
+    3: ("materials", "12", False),
+    6: ("materials", "8_uneven", False),
+    4: ("materials", "close", False),
+    7: ("noise", "8_uneven", False),
+    5: ("noise", "close", False),
+    1: ("spectral", "12", True),
+    0: ("spectral", "8_uneven", True),
+}
+# layout template -> (layout, force 64-bit offsets: VPTMCM_MARCH_VARIANT=8)
+_TEMPLATES = {0: (vptmcm.LAYOUT_LINEAR, False), 1: (vptmcm.LAYOUT_CORNER8, False),
+              2: (vptmcm.LAYOUT_CORNER8, True), 3: (vptmcm.LAYOUT_BRICK8, False),
+              4: (vptmcm.LAYOUT_BRICK8, True)}
+
+
+def test_mode_template_coverage(monkeypatch):
+    """Every (MODE, layout template) pair the dispatcher can select has run bit
+    for bit against the oracle: the pairs the random cases did not reach are
+    forced here (and asserted to be the pair that launched)."""
+    rng = np.random.default_rng(77)
+    noise = rng.integers(0, 256, (256, 256, 4), dtype=np.uint8)
+    tfs = {"spectral": cf.tf_spectral(), "materials": cf.tf_materials(True), "noise": noise}
+    specs = {"12": cf.spectrum_buffer("12"), "8_uneven": cf.spectrum_buffer("8_uneven"),
+             "close": _close_bins()}
+    vol = cf.sphere_in_cube(24)
+    mvp = cf.default_mvp_inverse()
+    spd, ldir = cf.light_default()
+    R = 32
+    forced = []
+    for mode, (tfk, bk, iso) in _MODE_INPUTS.items():
+        for tpl, (layout, wide) in _TEMPLATES.items():
+            if (mode, tpl) in HIT:
+                continue
+            forced.append((mode, tpl))
+            what = f"MODE {mode} template {tpl}: tf={tfk} bins={bk} isotropic={iso}"
+            ld = np.zeros(3, np.float32) if iso else ldir
+            if wide:
+                monkeypatch.setenv("VPTMCM_MARCH_VARIANT", "8")
+            else:
+                monkeypatch.delenv("VPTMCM_MARCH_VARIANT", raising=False)
+            with vptmcm.Renderer(R, device=0, layout=layout) as gpu:
+                cpu = orc.Oracle(R)
+                for r in (gpu, cpu):
+                    r.set_spectrum(specs[bk])
+                gpu.set_volume(vol)
+                gpu.set_material_tf(tfs[tfk])
+                gpu.set_light(spd, ld)
+                gpu.set_params(extinction=24.0, bounces=8, steps=8)
+                cpu.volume, cpu.tf, cpu.light, cpu.light_dir = vol, tfs[tfk], spd, ld
+                cpu.params.update(extinction=24.0, bounces=8, steps=8)
+                seeds = cf.seed_stream(5, start=mode * 10 + tpl)
+                gpu.reset(mvp, seeds[0])
+                cpu.reset(mvp, seeds[0], nthreads=8)
+                gpu.render(mvp, seeds[1])
+                cpu.render(mvp, seeds[1], nthreads=8)
+                assert_photons_equal(gpu.read_photons(), cpu.photons, what + " pass 1")
+                gpu.render_passes(mvp, seeds[2:])
+                for sd in seeds[2:]:
+                    rgb, want = cpu.render(mvp, sd, nthreads=8)
+                info = gpu.last_launch()
+                assert (info["mode"], info["tpl"], info["passes"]) == (mode, tpl, 3), (what, info)
+                assert_photons_equal(gpu.read_photons(), cpu.photons, what + " fused")
+                assert_rgba_equal(gpu.read_rgba16f(), want, what + " fused")
+                assert_rgb32_equal(gpu.read_rgb(), rgb, what + " fused")
+            HIT.add((mode, tpl))
+    print(f"forced {len(forced)} of 40 pairs: {forced}")
+    assert len(HIT) == 40

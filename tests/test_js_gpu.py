@@ -22,7 +22,7 @@ ROOT = Path(__file__).resolve().parents[1]
 
 
 def run_case(tmp_path, vol, tf, R=64, passes=3, ext=32.0, layout="corner8", stream=True,
-             change_event=False, tonemap=None, bvp=None, ui=None, band=None):
+             change_event=False, tonemap=None, bvp=None, ui=None, band=None, render_passes=False):
     D, H, W = vol.shape
     (tmp_path / "vol.raw").write_bytes(np.ascontiguousarray(vol).tobytes())
     (tmp_path / "tf.bin").write_bytes(np.ascontiguousarray(tf).tobytes())
@@ -30,7 +30,7 @@ def run_case(tmp_path, vol, tf, R=64, passes=3, ext=32.0, layout="corner8", stre
     case = dict(R=R, passes=passes, extinction=ext, bounces=8, steps=8, layout=layout,
                 W=W, H=H, D=D, volume_path=str(tmp_path / "vol.raw"), tf_path=str(tmp_path / "tf.bin"),
                 seeds=seeds, stream_volume=stream, change_event=change_event, tonemap=tonemap,
-                bvp_path=None, ui=ui, band=band)
+                bvp_path=None, ui=ui, band=band, render_passes=render_passes)
     if bvp is not None:
         (tmp_path / "vol.bvp").write_bytes(bvp)
         case["bvp_path"] = str(tmp_path / "vol.bvp")
@@ -41,8 +41,9 @@ def run_case(tmp_path, vol, tf, R=64, passes=3, ext=32.0, layout="corner8", stre
     ph = np.frombuffer((tmp_path / "photons.bin").read_bytes(), np.uint32).reshape(R * R, 36)
     rgba = np.frombuffer((tmp_path / "rgba.bin").read_bytes(), np.uint16).reshape(R, R, 4)
     rgb32 = np.frombuffer((tmp_path / "rgb32.bin").read_bytes(), np.float32).reshape(R, R, 3)
-    used = json.loads((tmp_path / "meta.json").read_text())["seeds_used"]
-    run_case.rgb32 = rgb32
+    meta = json.loads((tmp_path / "meta.json").read_text())
+    used = meta["seeds_used"]
+    run_case.rgb32, run_case.meta = rgb32, meta
     return ph, rgba, seeds, used
 
 
@@ -65,6 +66,24 @@ def oracle_replay(vol, tf, R, seeds, passes, ext, change_event=False):
 def same(a, b):
     fa, fb = a.view(np.float32), b.view(np.float32)
     return ((a == b) | (np.isnan(fa) & np.isnan(fb))).all()
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+@pytest.mark.parametrize("render_passes", [False, True])
+def test_js_render_calls_fuse(tmp_path, render_passes):
+    """40 JS render() calls (each re-sending the unchanged uniforms, as the
+    reference does every pass) reach the fused march: 2 launches (32 + 8
+    passes), bit-exact; renderPasses(40) takes one N-API call to the same."""
+    vol, tf = cf.sphere_in_cube(64), cf.tf_spectral()
+    ph, rgba, seeds, used = run_case(tmp_path, vol, tf, passes=40, render_passes=render_passes)
+    assert used == 41
+    meta = run_case.meta
+    assert meta["march_launches"] == 2, meta
+    assert meta["last_launch"]["passes"] == 8 and meta["last_launch"]["mode"] == 2, meta
+    want_ph, want_rgba = oracle_replay(vol, tf, 64, seeds, 40, 32.0)
+    assert same(ph[:, :34], want_ph[:, :34])
+    assert np.array_equal(rgba, want_rgba)
+    assert same(run_case.rgb32.view(np.uint32), oracle_replay.rgb32.view(np.uint32))
 
 
 @pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")

@@ -33,6 +33,12 @@ for s in $STEPS; do
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$GRAFT_REPO_ROOT/$OUT/calib_pmc_$mib" -o run --output-format csv -- "$GRAFT_REPO_ROOT/tools/gather_calib" $mib > /dev/null 2> "$GRAFT_REPO_ROOT/$OUT/calib_pmc_$mib.err")
       rc=$?; echo "calib pmc $mib rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
     done ;;
+  latency)  # first-region and median wall overhead of the driver's 20-pass region
+    timeout -k 10 300 python tools/launch_latency.py --passes 20 --regions 40 > $OUT/latency.json 2> $OUT/latency.err
+    rc=$?; echo "latency rc=$rc" | tee -a $OUT/status.txt; cat $OUT/latency.json; fault $rc && exit $rc ;;
+  cost)  # floor of a one-pass launch (tools/launch_cost.hip)
+    timeout -k 10 120 tools/launch_cost > $OUT/launch_cost.json 2>&1
+    rc=$?; echo "cost rc=$rc" | tee -a $OUT/status.txt; cat $OUT/launch_cost.json; fault $rc && exit $rc ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)

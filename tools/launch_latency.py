@@ -60,7 +60,11 @@ def main():
     med = lambda v: round(float(np.median(v)), 2)  # noqa: E731
     print(json.dumps({"passes": a.passes, "timing": not a.no_timing, "enqueue_us": med(enq), "sync_us": med(syn),
                       "wall_us": med(wall), "kernel_region_us": med(kern),
-                      "overhead_us": round(med(wall) - med(kern), 2)}))
+                      "overhead_us": round(med(wall) - med(kern), 2),
+                      # the first region is the one a single-region bench (the driver's) times
+                      "first": {"enqueue_us": round(enq[0], 2), "sync_us": round(syn[0], 2),
+                                "wall_us": round(wall[0], 2), "kernel_region_us": round(kern[0], 2)},
+                      "wall_us_max": round(max(wall), 2), "wall_us_min": round(min(wall), 2)}))
 
 
 if __name__ == "__main__":

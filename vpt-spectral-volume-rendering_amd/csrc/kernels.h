@@ -53,6 +53,12 @@ inline uint32_t sched_flag_bytes(uint32_t n_tiles) {
 }
 
 hipError_t launch_reset(const MarchParams& P, float* ph, hipStream_t s);
+// What one march launch ran (vptmcm_debug_last_launch): the MODE
+// specialisation, the layout template (kTpl*), the step loop (1 speculative,
+// 0 plain) and the number of fused passes.
+struct MarchLaunchInfo {
+  uint32_t mode, tpl, spec, passes;
+};
 // variant: tuning bits (bit 0 = plain step loop instead of the speculative one)
 hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P, const PassSeeds& PS,
                         const TileSched& T, float* ph,
@@ -60,7 +66,7 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba, float* rgb32,
                         hipStream_t s, hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr,
                         const uint32_t* tf_rows = nullptr, const uint8_t* tf_rowmap = nullptr,
-                        const uint32_t* bin_lut = nullptr);
+                        const uint32_t* bin_lut = nullptr, MarchLaunchInfo* info = nullptr);
 // Artistic tone mapper uniforms, derived on the host from (low, mid, high,
 // saturation, gamma) (WebGPUArtisticToneMapper.js:81-88, ArtisticToneMapper.wgsl:40-46).
 struct ToneParams {
@@ -73,7 +79,8 @@ hipError_t launch_reset_rgb(const MarchParams& P, float* ph, hipStream_t s);
 hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSeeds& PS,
                             const TileSched& T, float* ph, const uint8_t* vol, const float4* tf,
                             uint16_t* rgba, float* rgb32, hipStream_t s,
-                            hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr);
+                            hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr,
+                            MarchLaunchInfo* info = nullptr);
 hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, uint32_t BW,
                           uint32_t BH, void* out, hipStream_t s);
 hipError_t launch_pack(const MarchParams& P, const float* ph, const float* rgb32, float4* out,

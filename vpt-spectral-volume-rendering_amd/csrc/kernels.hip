@@ -1094,7 +1094,8 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
                         const TileSched& T, float* ph, const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba, float* rgb32,
                         hipStream_t s, hipEvent_t ev_beg, hipEvent_t ev_end,
-                        const uint32_t* tf_rows, const uint8_t* tf_rowmap, const uint32_t* bin_lut) {
+                        const uint32_t* tf_rows, const uint8_t* tf_rowmap, const uint32_t* bin_lut,
+                        MarchLaunchInfo* info) {
   dim3 grid(tile_blocks(P, kMarchBlock));
   // variant bits (analysis; results identical; bits 1-3 are the host's):
   // 0 plain (non-speculative) step, 4 none of the GEO specialisations (MODE 1
@@ -1113,40 +1114,46 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   const bool lut = P.bins_lut && bin_lut && (variant & 64u) == 0u;
   const uint16_t* tf_lds = Q.tf_dedup ? reinterpret_cast<const uint16_t*>(tf_rows) : tf_rg;
   const uint8_t* rowmap = tf_rowmap ? tf_rowmap : tf_brow;
+  uint32_t mode;
+  if (spec && fast) mode = 2u;
+  else if (spec && geo && Q.tf_dedup) mode = 3u;
+  else if (spec && geom && Q.tf_dedup && lut) mode = 6u;
+  else if (spec && geom && Q.tf_dedup) mode = 4u;
+  else if (spec && geom && lut) mode = 7u;
+  else if (spec && geom) mode = 5u;
+  else if (nbf) mode = 1u;
+  else mode = 0u;
+  uint32_t tpl;
+  if (layout == kLayoutBrick8) tpl = P.vol32 ? kTplBrick8 : kTplBrick8Wide;
+  else if (layout == kLayoutCorner8) tpl = P.vol32 ? kTplCorner8 : kTplCorner8Wide;
+  else tpl = kTplLinear;
+  if (info) *info = MarchLaunchInfo{mode, tpl, spec ? 1u : 0u, PS.n};
   // hipExtLaunchKernelGGL stamps the events from the dispatch packet itself
   // (no extra barrier/marker packets between back-to-back launches)
 #define VPT_LAUNCH(LAY, SP, MO)                                                                \
   hipExtLaunchKernelGGL((k_march<LAY, SP, MO>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
                         PS, Q, T, ph, vol, tf_lds, tf_b4, tf_brow, light, rgba, rgb32, rowmap, bin_lut)
-#define VPT_LAUNCH_NB(LAY, SP)                 \
-  do {                                         \
-    if (SP && fast)                            \
-      VPT_LAUNCH(LAY, SP, SP ? 2u : 1u);       \
-    else if (SP && geo && Q.tf_dedup)          \
-      VPT_LAUNCH(LAY, SP, SP ? 3u : 1u);       \
-    else if (SP && geom && Q.tf_dedup && lut)  \
-      VPT_LAUNCH(LAY, SP, SP ? 6u : 1u);       \
-    else if (SP && geom && Q.tf_dedup)         \
-      VPT_LAUNCH(LAY, SP, SP ? 4u : 1u);       \
-    else if (SP && geom && lut)                \
-      VPT_LAUNCH(LAY, SP, SP ? 7u : 1u);       \
-    else if (SP && geom)                       \
-      VPT_LAUNCH(LAY, SP, SP ? 5u : 1u);       \
-    else if (nbf)                              \
-      VPT_LAUNCH(LAY, SP, 1u);                 \
-    else                                       \
-      VPT_LAUNCH(LAY, SP, 0u);                 \
+#define VPT_LAUNCH_NB(LAY)                 \
+  do {                                     \
+    switch (spec ? mode : 8u + mode) {     \
+      case 2u: VPT_LAUNCH(LAY, true, 2u); break; \
+      case 3u: VPT_LAUNCH(LAY, true, 3u); break; \
+      case 4u: VPT_LAUNCH(LAY, true, 4u); break; \
+      case 5u: VPT_LAUNCH(LAY, true, 5u); break; \
+      case 6u: VPT_LAUNCH(LAY, true, 6u); break; \
+      case 7u: VPT_LAUNCH(LAY, true, 7u); break; \
+      case 1u: VPT_LAUNCH(LAY, true, 1u); break; \
+      case 0u: VPT_LAUNCH(LAY, true, 0u); break; \
+      case 9u: VPT_LAUNCH(LAY, false, 1u); break; \
+      default: VPT_LAUNCH(LAY, false, 0u); break; \
+    }                                      \
   } while (0)
-  if (layout == kLayoutBrick8 && P.vol32) {
-    if (spec) VPT_LAUNCH_NB(kTplBrick8, true); else VPT_LAUNCH_NB(kTplBrick8, false);
-  } else if (layout == kLayoutBrick8) {
-    if (spec) VPT_LAUNCH_NB(kTplBrick8Wide, true); else VPT_LAUNCH_NB(kTplBrick8Wide, false);
-  } else if (layout == kLayoutCorner8 && P.vol32) {
-    if (spec) VPT_LAUNCH_NB(kTplCorner8, true); else VPT_LAUNCH_NB(kTplCorner8, false);
-  } else if (layout == kLayoutCorner8) {
-    if (spec) VPT_LAUNCH_NB(kTplCorner8Wide, true); else VPT_LAUNCH_NB(kTplCorner8Wide, false);
-  } else {
-    if (spec) VPT_LAUNCH_NB(kTplLinear, true); else VPT_LAUNCH_NB(kTplLinear, false);
+  switch (tpl) {
+    case kTplBrick8: VPT_LAUNCH_NB(kTplBrick8); break;
+    case kTplBrick8Wide: VPT_LAUNCH_NB(kTplBrick8Wide); break;
+    case kTplCorner8: VPT_LAUNCH_NB(kTplCorner8); break;
+    case kTplCorner8Wide: VPT_LAUNCH_NB(kTplCorner8Wide); break;
+    default: VPT_LAUNCH_NB(kTplLinear); break;
   }
 #undef VPT_LAUNCH_NB
 #undef VPT_LAUNCH
@@ -1161,9 +1168,15 @@ hipError_t launch_reset_rgb(const MarchParams& P, float* ph, hipStream_t s) {
 hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSeeds& PS,
                             const TileSched& T, float* ph, const uint8_t* vol, const float4* tf,
                             uint16_t* rgba, float* rgb32, hipStream_t s, hipEvent_t ev_beg,
-                            hipEvent_t ev_end) {
+                            hipEvent_t ev_end, MarchLaunchInfo* info) {
   dim3 grid(tile_blocks(P, kMarchBlock));
   const bool geo = P.w_bounded && P.blur == 0.0f && (P.R & 1u) == 0u;
+  if (info) {  // mode: 1 with the FAST geometry (k_march_rgb<L, true>), else 0
+    const uint32_t tpl = layout == kLayoutBrick8 ? (P.vol32 ? kTplBrick8 : kTplBrick8Wide)
+                       : layout == kLayoutCorner8 ? (P.vol32 ? kTplCorner8 : kTplCorner8Wide)
+                       : kTplLinear;
+    *info = MarchLaunchInfo{geo ? 1u : 0u, tpl, 1u, PS.n};
+  }
 #define VPT_LAUNCH_RGB(LAY)                                                                       \
   do {                                                                                            \
     if (geo)                                                                                      \

@@ -8,11 +8,14 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -83,10 +86,19 @@ struct vptmcm {
   bool region_closed = false;
   EventPair region;
   uint64_t launches = 0;
+  uint64_t march_launches = 0;  // every march launch since create (vptmcm_debug_last_launch)
+  MarchLaunchInfo last_launch{};
 
   // multi-GPU
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  // Bound on any wait for the communicator (init, an enqueue still in progress,
+  // a stream holding RCCL work): VPTMCM_COMM_TIMEOUT_MS, default 120 s. On
+  // expiry or an asynchronous RCCL error the communicator is aborted and the
+  // call returns VPTMCM_ECOMM, so a dead or hung peer ends the job instead of
+  // hanging every rank.
+  int64_t comm_timeout_ms = 120000;
+  uint32_t* band_cover = nullptr;  // Mode B: one counter per 8-row tile, all-reduced
   hipStream_t comm_stream = nullptr;
   float4* comp[2] = {nullptr, nullptr};
   hipEvent_t comp_ready[2] = {nullptr, nullptr};
@@ -117,13 +129,6 @@ struct vptmcm {
     if (_e != hipSuccess)                                                      \
       FAIL(h, VPTMCM_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(_e),     \
            __FILE__, __LINE__);                                                \
-  } while (0)
-
-#define NCCLCHK(h, expr)                                                      \
-  do {                                                                        \
-    ncclResult_t _r = (expr);                                                 \
-    if (_r != ncclSuccess)                                                    \
-      FAIL(h, VPTMCM_ECOMM, "%s: %s", #expr, ncclGetErrorString(_r));         \
   } while (0)
 
 namespace {
@@ -338,9 +343,9 @@ int check_handle(vptmcm* h) { return h ? VPTMCM_OK : VPTMCM_EINVAL; }
 // comparison search. The table is checked against bin_of's rule at every
 // threshold and its neighbours and on a 2^16-point grid before it is enabled.
 int build_bin_lut(vptmcm* h) {
+  h->bin_lut_ok = false;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));  // no launch still reads the table
-  h->bin_lut_ok = false;
   const float ident[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
   const MarchParams Q = make_params(h, ident, 0u);
   if (!Q.bins_sorted || !Q.bins_padded || !(Q.max_lam >= Q.min_lam)) return VPTMCM_OK;
@@ -444,11 +449,12 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : 0u;
   if (h->kind == VPTMCM_RENDERER_RGB)
     HIPCHK(h, launch_march_rgb(h->layout, P, PS, T, h->photons, vol, h->tf_rgb, h->rgba, h->rgb32,
-                               h->stream, eb, ee));
+                               h->stream, eb, ee, &h->last_launch));
   else
     HIPCHK(h, launch_march(h->layout, h->variant, P, PS, T, h->photons, vol, h->tf_rg, h->tf_b4,
                            h->tf_brow, h->light, h->rgba, h->rgb32, h->stream, eb, ee, h->tf_rows,
-                           h->tf_rowmap, h->bin_lut));
+                           h->tf_rowmap, h->bin_lut, &h->last_launch));
+  h->march_launches++;
   h->sched_cur = c ^ 1u;
   return VPTMCM_OK;
 }
@@ -460,6 +466,86 @@ int flush_renders(vptmcm* h) {
   h->pend_n = 0;
   HIPCHK(h, hipSetDevice(h->device));
   return do_march(h, h->pend_mvp, h->pend_seeds, n);
+}
+
+// ---- communicator waits (see vptmcm::comm_timeout_ms)
+
+int64_t now_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Abort the communicator after an error or a timeout: RCCL kernels still
+// waiting for a peer observe the abort flag and exit, so the handle's streams
+// drain. Every later communicator call returns VPTMCM_ECOMM.
+int comm_fail(vptmcm* h, const char* what, const char* why) {
+  if (h->comm) (void)ncclCommAbort(h->comm);
+  h->comm = nullptr;
+  FAIL(h, VPTMCM_ECOMM, "%s: %s (communicator aborted; rank %d of %d)", what, why, h->rank,
+       h->nranks);
+}
+
+// The communicator's asynchronous state: OK, 1 (still in progress) or the
+// VPTMCM_ECOMM of comm_fail.
+int comm_state(vptmcm* h, const char* what) {
+  ncclResult_t st = ncclSuccess;
+  const ncclResult_t r = ncclCommGetAsyncError(h->comm, &st);
+  if (r != ncclSuccess) st = r;
+  if (st == ncclSuccess) return VPTMCM_OK;
+  if (st == ncclInProgress) return 1;
+  return comm_fail(h, what, ncclGetErrorString(st));
+}
+
+// Wait until a non-blocking communicator call (init, or an enqueue that
+// returned ncclInProgress) has completed.
+int comm_settle(vptmcm* h, const char* what) {
+  const int64_t t0 = now_ms();
+  for (uint32_t spin = 0;; spin++) {
+    const int rc = comm_state(h, what);
+    if (rc <= 0) return rc;
+    if (now_ms() - t0 > h->comm_timeout_ms) {
+      char b[96];
+      snprintf(b, sizeof b, "no progress after %lld ms (a peer rank died or hangs?)",
+               (long long)h->comm_timeout_ms);
+      return comm_fail(h, what, b);
+    }
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
+
+// Check the result of an RCCL call on a non-blocking communicator.
+int comm_call(vptmcm* h, ncclResult_t r, const char* what) {
+  if (r == ncclInProgress) return comm_settle(h, what);
+  if (r != ncclSuccess) return comm_fail(h, what, ncclGetErrorString(r));
+  return VPTMCM_OK;
+}
+
+// Block until stream s has drained. With a communicator the stream may hold
+// RCCL work (or wait on it), so the wait polls the stream and the
+// communicator's asynchronous error, spinning first (a composite is a few
+// hundred microseconds), and gives up after the communicator timeout.
+int wait_stream(vptmcm* h, hipStream_t s, const char* what) {
+  if (!h->comm) {
+    HIPCHK(h, hipStreamSynchronize(s));
+    return VPTMCM_OK;
+  }
+  const int64_t t0 = now_ms();
+  for (uint32_t spin = 0;; spin++) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return VPTMCM_OK;
+    if (e != hipErrorNotReady) FAIL(h, VPTMCM_EHIP, "%s: %s", what, hipGetErrorString(e));
+    if ((spin & 255u) == 0u) {
+      const int rc = comm_state(h, what);
+      if (rc < 0) return rc;
+      if (now_ms() - t0 > h->comm_timeout_ms) {
+        char b[96];
+        snprintf(b, sizeof b, "stream not drained after %lld ms (a peer rank died or hangs?)",
+                 (long long)h->comm_timeout_ms);
+        return comm_fail(h, what, b);
+      }
+    }
+    if (now_ms() - t0 > 20) std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
 }
 
 void free_volume(vptmcm* h) {
@@ -586,9 +672,12 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
 
 void vptmcm_destroy(vptmcm* h) {
   if (!h) return;
-  if (h->stream) (void)hipStreamSynchronize(h->stream);
-  if (h->comm_stream) (void)hipStreamSynchronize(h->comm_stream);
-  if (h->comm) ncclCommDestroy(h->comm);
+  // bounded waits while a communicator exists (a failed one is aborted)
+  if (h->comm_stream) (void)wait_stream(h, h->comm_stream, "destroy");
+  if (h->stream) (void)wait_stream(h, h->stream, "destroy");
+  if (h->comm && comm_call(h, ncclCommFinalize(h->comm), "destroy: ncclCommFinalize") == VPTMCM_OK)
+    (void)ncclCommDestroy(h->comm);
+  if (h->band_cover) (void)hipFree(h->band_cover);
   for (int k = 0; k < 2; k++) {
     if (h->comp[k]) (void)hipFree(h->comp[k]);
     if (h->comp_ready[k]) (void)hipEventDestroy(h->comp_ready[k]);
@@ -795,6 +884,7 @@ int vptmcm_set_spectrum(vptmcm* h, const float* buf) {
   float nbf = buf[0] + 0.5f;
   if (!(nbf >= 0.0f) || nbf >= (float)(VPTMCM_MAX_BINS + 1))
     FAIL(h, VPTMCM_EINVAL, "set_spectrum: n_bins = %g exceeds MAX_N_BINS (12)", (double)buf[0]);
+  h->bin_lut_ok = false;  // every error path below leaves the bin table disabled
   memcpy(h->spectrum, buf, sizeof h->spectrum);
   return build_bin_lut(h);
 }
@@ -849,8 +939,12 @@ int vptmcm_set_band(vptmcm* h, uint32_t y0, uint32_t y1) {
 
 int vptmcm_set_params(vptmcm* h, const vptmcm_params* p) {
   if (check_handle(h)) return VPTMCM_EINVAL;
-  if (int rc_ = flush_renders(h)) return rc_;
   if (!p) FAIL(h, VPTMCM_EINVAL, "set_params: null params");
+  // The reference rewrites the same uniform values before every pass
+  // (js:295-309); only a change of bits ends the queue of fused passes.
+  static_assert(sizeof(vptmcm_params) == 20, "vptmcm_params has no padding");
+  if (memcmp(&h->params, p, sizeof *p) == 0) return VPTMCM_OK;
+  if (int rc_ = flush_renders(h)) return rc_;
   h->params = *p;
   return VPTMCM_OK;
 }
@@ -904,8 +998,8 @@ int vptmcm_synchronize(vptmcm* h) {
   HIPCHK(h, hipSetDevice(h->device));
   int rc = time_close(h);
   if (rc) return rc;
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  if (h->comm_stream) HIPCHK(h, hipStreamSynchronize(h->comm_stream));
+  if ((rc = wait_stream(h, h->stream, "synchronize"))) return rc;
+  if (h->comm_stream && (rc = wait_stream(h, h->comm_stream, "synchronize"))) return rc;
   return VPTMCM_OK;
 }
 
@@ -1064,6 +1158,10 @@ int vptmcm_enable_kernel_timing(vptmcm* h, int enable) {
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->timing = enable != 0;
+  if (h->timing && !h->region.beg) {  // created here, outside the region they time
+    HIPCHK(h, hipEventCreateWithFlags(&h->region.beg, hipEventDisableSystemFence));
+    HIPCHK(h, hipEventCreateWithFlags(&h->region.end, hipEventDisableSystemFence));
+  }
   h->launches = 0;
   h->region_closed = false;
   return VPTMCM_OK;
@@ -1105,11 +1203,24 @@ int vptmcm_comm_init(vptmcm* h, const uint8_t* uid, int nranks, int rank) {
     FAIL(h, VPTMCM_EINVAL, "comm_init: bad arguments (nranks=%d rank=%d)", nranks, rank);
   if (h->comm) FAIL(h, VPTMCM_ESTATE, "comm_init: communicator already initialised");
   HIPCHK(h, hipSetDevice(h->device));
+  if (const char* v = getenv("VPTMCM_COMM_TIMEOUT_MS")) {
+    const long long t = strtoll(v, nullptr, 10);
+    if (t > 0) h->comm_timeout_ms = t;
+  }
   ncclUniqueId id;
   memcpy(&id, uid, sizeof id);
-  NCCLCHK(h, ncclCommInitRank(&h->comm, nranks, id, rank));
+  // non-blocking: a peer that never joins ends in VPTMCM_ECOMM after the timeout
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
   h->nranks = nranks;
   h->rank = rank;
+  const ncclResult_t r = ncclCommInitRankConfig(&h->comm, nranks, id, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (h->comm) (void)ncclCommAbort(h->comm);
+    h->comm = nullptr;
+    FAIL(h, VPTMCM_ECOMM, "ncclCommInitRankConfig: %s", ncclGetErrorString(r));
+  }
+  if (int rc = comm_settle(h, "comm_init")) return rc;
   HIPCHK(h, hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking));
   size_t bytes = (size_t)h->R * h->R * sizeof(float4);
   for (int k = 0; k < 2; k++) {
@@ -1134,8 +1245,10 @@ int vptmcm_comm_allreduce_radiance(vptmcm* h) {
   HIPCHK(h, launch_pack(P, h->photons, h->rgb32, h->comp[k], h->stream));
   HIPCHK(h, hipEventRecord(h->comp_ready[k], h->stream));
   HIPCHK(h, hipStreamWaitEvent(h->comm_stream, h->comp_ready[k], 0));
-  NCCLCHK(h, ncclAllReduce(h->comp[k], h->comp[k], (size_t)h->R * h->R * 4, ncclFloat32, ncclSum,
-                           h->comm, h->comm_stream));
+  if (int rc = comm_call(h, ncclAllReduce(h->comp[k], h->comp[k], (size_t)h->R * h->R * 4,
+                                          ncclFloat32, ncclSum, h->comm, h->comm_stream),
+                         "comm_allreduce_radiance"))
+    return rc;
   HIPCHK(h, hipEventRecord(h->comp_done[k], h->comm_stream));
   h->comp_last = k;
   h->comp_next = k ^ 1;
@@ -1148,7 +1261,7 @@ int vptmcm_comm_read_composite(vptmcm* h, float* rgb, float* counts) {
   if (!h->comm || h->comp_last < 0) FAIL(h, VPTMCM_ESTATE, "read_composite: no all-reduce issued");
   if (!rgb) FAIL(h, VPTMCM_EINVAL, "read_composite: null output");
   HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipStreamSynchronize(h->comm_stream));
+  if (int rc = wait_stream(h, h->comm_stream, "comm_read_composite")) return rc;
   size_t npx = (size_t)h->R * h->R;
   std::vector<float> buf(npx * 4);
   HIPCHK(h, hipMemcpy(buf.data(), h->comp[h->comp_last], npx * 16, hipMemcpyDeviceToHost));
@@ -1166,16 +1279,38 @@ int vptmcm_comm_gather_bands(vptmcm* h, float* rgb) {
   if (!h->comm) FAIL(h, VPTMCM_ECOMM, "comm_gather_bands: no communicator");
   if (!rgb) FAIL(h, VPTMCM_EINVAL, "comm_gather_bands: null output");
   HIPCHK(h, hipSetDevice(h->device));
+  int rc = 0;
+  // The bands must tile the frame: every 8-row tile covered by exactly one rank.
+  const uint32_t ty = (h->R + 7) / 8;
+  if (!h->band_cover) HIPCHK(h, hipMalloc(&h->band_cover, ty * sizeof(uint32_t)));
+  std::vector<uint32_t> cover(ty, 0u);
+  for (uint32_t t = h->band_y0 / 8; t < (h->band_y1 + 7) / 8; t++) cover[t] = 1u;
+  HIPCHK(h, hipMemcpyAsync(h->band_cover, cover.data(), ty * sizeof(uint32_t), hipMemcpyHostToDevice,
+                           h->comm_stream));
+  if ((rc = comm_call(h, ncclAllReduce(h->band_cover, h->band_cover, ty, ncclUint32, ncclSum, h->comm,
+                                       h->comm_stream), "comm_gather_bands")))
+    return rc;
+  HIPCHK(h, hipMemcpyAsync(cover.data(), h->band_cover, ty * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           h->comm_stream));
+  if ((rc = wait_stream(h, h->comm_stream, "comm_gather_bands"))) return rc;
+  for (uint32_t t = 0; t < ty; t++)
+    if (cover[t] != 1u)
+      FAIL(h, VPTMCM_ECOMM, "comm_gather_bands: rows [%u, %u) are covered by %u ranks' bands (need "
+           "exactly 1: the bands must tile the frame)", t * 8, std::min(t * 8 + 8, h->R), cover[t]);
+  // Sum of the fp32 images (zero outside each band): exact, up to the sign of
+  // a -0.0 pixel (-0 + +0 = +0).
   const size_t n = (size_t)h->R * h->R * 3;
   float* sum = reinterpret_cast<float*>(h->comp[h->comp_next]);  // R*R float4 >= R*R*3 floats
   HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[h->comp_next], 0));
   HIPCHK(h, hipMemcpyAsync(sum, h->rgb32, n * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  NCCLCHK(h, ncclAllReduce(sum, sum, n, ncclFloat32, ncclSum, h->comm, h->comm_stream));
+  HIPCHK(h, hipEventRecord(h->comp_ready[h->comp_next], h->stream));
+  HIPCHK(h, hipStreamWaitEvent(h->comm_stream, h->comp_ready[h->comp_next], 0));
+  if ((rc = comm_call(h, ncclAllReduce(sum, sum, n, ncclFloat32, ncclSum, h->comm, h->comm_stream),
+                      "comm_gather_bands")))
+    return rc;
   HIPCHK(h, hipMemcpyAsync(rgb, sum, n * sizeof(float), hipMemcpyDeviceToHost, h->comm_stream));
   HIPCHK(h, hipEventRecord(h->comp_done[h->comp_next], h->comm_stream));
-  HIPCHK(h, hipStreamSynchronize(h->comm_stream));
-  return VPTMCM_OK;
+  return wait_stream(h, h->comm_stream, "comm_gather_bands");
 }
 
 int vptmcm_comm_barrier(vptmcm* h) {
@@ -1190,14 +1325,28 @@ int vptmcm_comm_allreduce_host(vptmcm* h, double* vals, int n, int op) {
   if (!vals || n < 1 || n > 64 || op < 0 || op > 1)
     FAIL(h, VPTMCM_EINVAL, "comm_allreduce_host: bad arguments");
   HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  int rc = wait_stream(h, h->stream, "comm_allreduce_host");
+  if (rc) return rc;
   HIPCHK(h, hipMemcpyAsync(h->host_scratch, vals, n * sizeof(double), hipMemcpyHostToDevice,
                            h->comm_stream));
-  NCCLCHK(h, ncclAllReduce(h->host_scratch, h->host_scratch, (size_t)n, ncclFloat64,
-                           op ? ncclMax : ncclSum, h->comm, h->comm_stream));
+  if ((rc = comm_call(h, ncclAllReduce(h->host_scratch, h->host_scratch, (size_t)n, ncclFloat64,
+                                       op ? ncclMax : ncclSum, h->comm, h->comm_stream),
+                      "comm_allreduce_host")))
+    return rc;
   HIPCHK(h, hipMemcpyAsync(vals, h->host_scratch, n * sizeof(double), hipMemcpyDeviceToHost,
                            h->comm_stream));
-  HIPCHK(h, hipStreamSynchronize(h->comm_stream));
+  return wait_stream(h, h->comm_stream, "comm_allreduce_host");
+}
+
+int vptmcm_debug_last_launch(vptmcm* h, uint32_t info[4], uint64_t* launches) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
+  if (!info) FAIL(h, VPTMCM_EINVAL, "debug_last_launch: null output");
+  info[0] = h->last_launch.mode;
+  info[1] = h->last_launch.tpl;
+  info[2] = h->last_launch.spec;
+  info[3] = h->last_launch.passes;
+  if (launches) *launches = h->march_launches;
   return VPTMCM_OK;
 }
 

@@ -222,8 +222,21 @@ class MCMSpectralComputeRenderer extends PropertyBag {
   }
 
   // ---- extensions beyond the reference surface ----
+  // n render() calls in one enqueue: the same uploads, then n passes with n
+  // fresh seeds (launched as fused multi-pass marches, 32 passes per launch)
   renderPasses(n) {
-    for (let k = 0; k < n; k++) this._renderFrame();
+    if (!this._volumeReady) throw new Error('render: no volume loaded (setVolume first)');
+    const m = this._matrix();
+    this._uploadTables();
+    const seeds = new Uint32Array(n);
+    for (let k = 0; k < n; k++) seeds[k] = this._seedBits();
+    native().renderPasses(this._h, m, seeds);
+  }
+
+  // What the last march launch ran: { mode, tpl, spec, passes, launches }
+  // (vptmcm_debug_last_launch; launches counts every march launch so far)
+  lastLaunch() {
+    return native().lastLaunch(this._h);
   }
 
   // Mode B (DESIGN.md): march only pixel rows [y0, y1) (multiples of 8; y1 may
@@ -273,6 +286,8 @@ class MCMSpectralComputeRenderer extends PropertyBag {
       A.setMaterialTF(this._h, this.material_transfer_function);
       this._dirty.tf = false;
     }
+    // rewritten every pass like the reference's UBO (js:295-309); the library
+    // ignores unchanged values, so queued render() passes stay fused
     A.setParams(this._h, this.extinction, this.anisotropy, this.bounces, this.steps, 0);  // blur 0, js:299
     if (this._dirty.spectrum) {
       A.setSpectrum(this._h, this.spectrumBuffer());  // only in _renderFrame (js:311-312)

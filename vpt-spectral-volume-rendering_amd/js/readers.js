@@ -79,73 +79,69 @@ class RAWReader {
   }
 }
 
-// ZIP archive reader (ZIPReader.js): end-of-central-directory record, central
-// directory entries, local header -> file data. The reference returns the
-// stored bytes as they are (BVP archives are written uncompressed, method 0);
-// deflated entries (method 8) are inflated here with Node's zlib.
+// ZIP archive reader, the ZIPReader.js surface (getFiles / readFile). The
+// archive's directory is parsed once into a name -> record map: the trailer
+// (signature 0x06054b50, the last 22 bytes: no archive comment) gives the
+// directory's extent and record count; each directory record (0x02014b50, 46
+// fixed bytes + name + extra + comment) gives a member's compression method,
+// stored size and local-record offset; a member's bytes follow its local
+// record (0x04034b50, 30 fixed bytes + name + extra). Stored members (method 0,
+// how BVP archives are written) are returned as they lie; deflated ones
+// (method 8) are inflated with Node's zlib, which the reference does not do.
+const ZIP_TRAILER = 0x06054b50, ZIP_DIRREC = 0x02014b50, ZIP_LOCAL = 0x04034b50;
+
 class ZIPReader {
   constructor(loader) {
     this._loader = loader;
-    this._eocd = null;
-    this._cd = null;
+    this._members = null;  // Map: member name -> { method, stored, local }
   }
 
   async getFiles() {
-    if (!this._cd) await this._readCD();
-    return this._cd.map(e => e.name);
+    return Array.from((await this._directory()).keys());
   }
 
   async readFile(fileName) {
-    if (!this._cd) await this._readCD();
-    const entry = this._cd.find(e => e.name === fileName);
-    if (!entry) throw new Error(`ZIPReader: file ${fileName} not in CD`);
-    const headerStart = entry.headerOffset;
-    const headerEnd = headerStart + 30;
-    const header = view(await this._loader.readData(headerStart, headerEnd));
-    if (header.getUint32(0, true) !== 0x04034b50) throw new Error(`ZIPReader: bad local header for ${fileName}`);
-    const dataStart = headerEnd + header.getUint16(26, true) + header.getUint16(28, true);
-    const data = await this._loader.readData(dataStart, dataStart + entry.compressedSize);
-    if (entry.method === 0) return data;
-    if (entry.method === 8) return new Uint8Array(zlib.inflateRawSync(Buffer.from(data)));
-    throw new Error(`ZIPReader: unsupported compression method ${entry.method} for ${fileName}`);
+    const m = (await this._directory()).get(fileName);
+    if (!m) throw new Error(`ZIPReader: the archive has no member named '${fileName}'`);
+    const local = bytesView(await this._loader.readData(m.local, m.local + 30));
+    if (local.getUint32(0, true) !== ZIP_LOCAL) {
+      throw new Error(`ZIPReader: member '${fileName}' has no local record at byte ${m.local}`);
+    }
+    const first = m.local + 30 + local.getUint16(26, true) + local.getUint16(28, true);
+    const raw = await this._loader.readData(first, first + m.stored);
+    switch (m.method) {
+      case 0: return raw;
+      case 8: return new Uint8Array(zlib.inflateRawSync(Buffer.from(raw)));
+      default: throw new Error(`ZIPReader: member '${fileName}' uses compression method ${m.method}`);
+    }
   }
 
-  async _readEOCD() {
-    const MIN_EOCD_SIZE = 22;
-    const length = await this._loader.readLength();
-    const offset = Math.max(length - MIN_EOCD_SIZE, 0);
-    const v = view(await this._loader.readData(offset, offset + Math.min(length, MIN_EOCD_SIZE)));
-    if (v.byteLength < MIN_EOCD_SIZE || v.getUint32(0, true) !== 0x06054b50) {
-      throw new Error('ZIPReader: no end-of-central-directory record (archive comments are not supported)');
+  async _directory() {
+    if (this._members) return this._members;
+    const total = await this._loader.readLength();
+    const at = Math.max(total - 22, 0);
+    const tail = bytesView(await this._loader.readData(at, total));
+    if (tail.byteLength < 22 || tail.getUint32(0, true) !== ZIP_TRAILER) {
+      throw new Error('ZIPReader: the last 22 bytes are not a zip trailer (archives with a comment are not read)');
     }
-    this._eocd = { entries: v.getUint16(10, true), size: v.getUint32(12, true), offset: v.getUint32(16, true) };
-  }
-
-  async _readCD() {
-    if (!this._eocd) await this._readEOCD();
-    const { offset: cdStart, size, entries: n } = this._eocd;
-    const bytes = await this._loader.readData(cdStart, cdStart + size);
-    const v = view(bytes);
-    const entries = [];
-    let o = 0;
-    for (let i = 0; i < n; i++) {
-      if (v.getUint32(o, true) !== 0x02014b50) throw new Error('ZIPReader: corrupt central directory');
-      const nameLength = v.getUint16(o + 28, true);
-      entries.push({
-        gpflag: v.getUint16(o + 8, true),
-        method: v.getUint16(o + 10, true),
-        compressedSize: v.getUint32(o + 20, true),
-        uncompressedSize: v.getUint32(o + 24, true),
-        name: Buffer.from(bytes.buffer, bytes.byteOffset + o + 46, nameLength).toString('utf8'),
-        headerOffset: v.getUint32(o + 42, true),
-      });
-      o += 46 + nameLength + v.getUint16(o + 30, true) + v.getUint16(o + 32, true);
+    const count = tail.getUint16(10, true), dirBytes = tail.getUint32(12, true), dirAt = tail.getUint32(16, true);
+    const dir = await this._loader.readData(dirAt, dirAt + dirBytes);
+    const v = bytesView(dir);
+    const members = new Map();
+    for (let k = 0, pos = 0; k < count; k++) {
+      if (v.getUint32(pos, true) !== ZIP_DIRREC) throw new Error(`ZIPReader: directory record ${k} is damaged`);
+      const nameLen = v.getUint16(pos + 28, true);
+      const name = Buffer.from(dir.buffer, dir.byteOffset + pos + 46, nameLen).toString('utf8');
+      members.set(name, { method: v.getUint16(pos + 10, true), stored: v.getUint32(pos + 20, true),
+        local: v.getUint32(pos + 42, true) });
+      pos += 46 + nameLen + v.getUint16(pos + 30, true) + v.getUint16(pos + 32, true);
     }
-    this._cd = entries;
+    this._members = members;
+    return members;
   }
 }
 
-function view(u8) {
+function bytesView(u8) {
   return new DataView(u8.buffer, u8.byteOffset, u8.byteLength);
 }
 

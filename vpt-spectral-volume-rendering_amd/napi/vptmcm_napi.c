@@ -21,6 +21,7 @@
 typedef struct {
     vptmcm* h;
     uint32_t photon_bytes; /* 144 spectral, 64 RGB */
+    uint32_t R;            /* the handle's resolution: every output array is sized from it */
 } handle_box;
 
 #define NAPI_OK(env, call)                                                   \
@@ -68,13 +69,18 @@ static int get_args(napi_env env, napi_callback_info info, size_t want, napi_val
     return 0;
 }
 
-static vptmcm* get_handle(napi_env env, napi_value v) {
+static handle_box* get_box(napi_env env, napi_value v) {
     handle_box* box = NULL;
     if (napi_get_value_external(env, v, (void**)&box) != napi_ok || !box || !box->h) {
         napi_throw_error(env, "VPTMCM_HANDLE", "invalid or destroyed renderer handle");
         return NULL;
     }
-    return box->h;
+    return box;
+}
+
+static vptmcm* get_handle(napi_env env, napi_value v) {
+    handle_box* box = get_box(env, v);
+    return box ? box->h : NULL;
 }
 
 /* typed array -> pointer + element count (+ element size check) */
@@ -112,6 +118,23 @@ static void* get_typed(napi_env env, napi_value v, size_t elem, size_t min_count
     }
     if (count) *count = length;
     return data;
+}
+
+static uint32_t get_u32(napi_env env, napi_value v);
+
+/* An output array of per_pixel elements per pixel of the handle's R x R
+ * frame. The caller's R must be the handle's: the library writes R*R*per_pixel
+ * elements whatever the caller believes. */
+static void* get_frame_out(napi_env env, handle_box* box, napi_value arr, napi_value r,
+                           size_t elem, size_t per_pixel) {
+    if (get_u32(env, r) != box->R) {
+        char msg[96];
+        snprintf(msg, sizeof msg, "resolution %u does not match the renderer's %u", get_u32(env, r),
+                 box->R);
+        napi_throw_range_error(env, NULL, msg);
+        return NULL;
+    }
+    return get_typed(env, arr, elem, (size_t)box->R * box->R * per_pixel, NULL);
 }
 
 static uint32_t get_u32(napi_env env, napi_value v) {
@@ -158,6 +181,7 @@ static napi_value js_create(napi_env env, napi_callback_info info) {
     if (rc) return throw_code(env, rc, vptmcm_last_error(NULL));
     handle_box* box = (handle_box*)malloc(sizeof *box);
     box->h = h;
+    box->R = cfg.resolution;
     box->photon_bytes = cfg.renderer == VPTMCM_RENDERER_RGB ? VPTMCM_PHOTON_RGB_BYTES : VPTMCM_PHOTON_BYTES;
     napi_value ext;
     NAPI_OK(env, napi_create_external(env, box, finalize_box, NULL, &ext));
@@ -307,12 +331,11 @@ static napi_value js_synchronize(napi_env env, napi_callback_info info) {
 static napi_value js_read_rgba16f(napi_env env, napi_callback_info info) {
     napi_value argv[3];
     if (get_args(env, info, 3, argv)) return NULL;
-    vptmcm* h = get_handle(env, argv[0]);
-    if (!h) return NULL;
-    uint32_t R = get_u32(env, argv[2]);
-    uint16_t* p = get_typed(env, argv[1], 2, (size_t)R * R * 4, NULL);
+    handle_box* box = get_box(env, argv[0]);
+    if (!box) return NULL;
+    uint16_t* p = get_frame_out(env, box, argv[1], argv[2], 2, 4);
     if (!p) return NULL;
-    return check(env, h, vptmcm_read_rgba16f(h, p));
+    return check(env, box->h, vptmcm_read_rgba16f(box->h, p));
 }
 
 /* readRGB(h, Float32Array(R*R*3), R): the last pass's fp32 radiance_to_rgb
@@ -320,12 +343,11 @@ static napi_value js_read_rgba16f(napi_env env, napi_callback_info info) {
 static napi_value js_read_rgb(napi_env env, napi_callback_info info) {
     napi_value argv[3];
     if (get_args(env, info, 3, argv)) return NULL;
-    vptmcm* h = get_handle(env, argv[0]);
-    if (!h) return NULL;
-    uint32_t R = get_u32(env, argv[2]);
-    float* p = get_typed(env, argv[1], 4, (size_t)R * R * 3, NULL);
+    handle_box* box = get_box(env, argv[0]);
+    if (!box) return NULL;
+    float* p = get_frame_out(env, box, argv[1], argv[2], 4, 3);
     if (!p) return NULL;
-    return check(env, h, vptmcm_read_rgb(h, p));
+    return check(env, box->h, vptmcm_read_rgb(box->h, p));
 }
 
 /* setTransferFunction(h, Uint8Array(w*h*4), w, h) / setEnvironment(h, Uint8Array(4), 1, 1) */
@@ -347,14 +369,13 @@ static napi_value js_set_environment(napi_env env, napi_callback_info info) { re
 static napi_value js_tonemap_artistic(napi_env env, napi_callback_info info) {
     napi_value argv[4];
     if (get_args(env, info, 4, argv)) return NULL;
-    vptmcm* h = get_handle(env, argv[0]);
-    if (!h) return NULL;
+    handle_box* box = get_box(env, argv[0]);
+    if (!box) return NULL;
     const float* params = get_typed(env, argv[1], 4, 5, NULL);
     if (!params) return NULL;
-    uint32_t R = get_u32(env, argv[3]);
-    uint8_t* out = get_typed(env, argv[2], 1, (size_t)R * R * 4, NULL);
+    uint8_t* out = get_frame_out(env, box, argv[2], argv[3], 1, 4);
     if (!out) return NULL;
-    return check(env, h, vptmcm_tonemap_artistic(h, params, out));
+    return check(env, box->h, vptmcm_tonemap_artistic(box->h, params, out));
 }
 
 /* readPhotons(h, Uint8Array(R*R*stride), R) / writePhotons(h, Uint8Array, R);
@@ -362,14 +383,11 @@ static napi_value js_tonemap_artistic(napi_env env, napi_callback_info info) {
 static napi_value photons_call(napi_env env, napi_callback_info info, int write) {
     napi_value argv[3];
     if (get_args(env, info, 3, argv)) return NULL;
-    vptmcm* h = get_handle(env, argv[0]);
-    if (!h) return NULL;
-    handle_box* box = NULL;
-    napi_get_value_external(env, argv[0], (void**)&box);
-    uint32_t R = get_u32(env, argv[2]);
-    uint8_t* p = get_typed(env, argv[1], 1, (size_t)R * R * box->photon_bytes, NULL);
+    handle_box* box = get_box(env, argv[0]);
+    if (!box) return NULL;
+    uint8_t* p = get_frame_out(env, box, argv[1], argv[2], 1, box->photon_bytes);
     if (!p) return NULL;
-    return check(env, h, write ? vptmcm_write_photons(h, p) : vptmcm_read_photons(h, p));
+    return check(env, box->h, write ? vptmcm_write_photons(box->h, p) : vptmcm_read_photons(box->h, p));
 }
 static napi_value js_read_photons(napi_env env, napi_callback_info info) { return photons_call(env, info, 0); }
 static napi_value js_write_photons(napi_env env, napi_callback_info info) { return photons_call(env, info, 1); }
@@ -438,12 +456,11 @@ static napi_value js_comm_allreduce_radiance(napi_env env, napi_callback_info in
 static napi_value js_comm_read_composite(napi_env env, napi_callback_info info) {
     napi_value argv[3];
     if (get_args(env, info, 3, argv)) return NULL;
-    vptmcm* h = get_handle(env, argv[0]);
-    if (!h) return NULL;
-    uint32_t R = get_u32(env, argv[2]);
-    float* rgb = get_typed(env, argv[1], 4, (size_t)R * R * 3, NULL);
+    handle_box* box = get_box(env, argv[0]);
+    if (!box) return NULL;
+    float* rgb = get_frame_out(env, box, argv[1], argv[2], 4, 3);
     if (!rgb) return NULL;
-    return check(env, h, vptmcm_comm_read_composite(h, rgb, NULL));
+    return check(env, box->h, vptmcm_comm_read_composite(box->h, rgb, NULL));
 }
 
 /* setBand(h, y0, y1): Mode B row band (multiples of 8; y1 may be R) */
@@ -459,12 +476,11 @@ static napi_value js_set_band(napi_env env, napi_callback_info info) {
 static napi_value js_comm_gather_bands(napi_env env, napi_callback_info info) {
     napi_value argv[3];
     if (get_args(env, info, 3, argv)) return NULL;
-    vptmcm* h = get_handle(env, argv[0]);
-    if (!h) return NULL;
-    uint32_t R = get_u32(env, argv[2]);
-    float* rgb = get_typed(env, argv[1], 4, (size_t)R * R * 3, NULL);
+    handle_box* box = get_box(env, argv[0]);
+    if (!box) return NULL;
+    float* rgb = get_frame_out(env, box, argv[1], argv[2], 4, 3);
     if (!rgb) return NULL;
-    return check(env, h, vptmcm_comm_gather_bands(h, rgb));
+    return check(env, box->h, vptmcm_comm_gather_bands(box->h, rgb));
 }
 
 static napi_value js_comm_barrier(napi_env env, napi_callback_info info) {
@@ -473,6 +489,28 @@ static napi_value js_comm_barrier(napi_env env, napi_callback_info info) {
     vptmcm* h = get_handle(env, argv[0]);
     if (!h) return NULL;
     return check(env, h, vptmcm_comm_barrier(h));
+}
+
+/* lastLaunch(h) -> { mode, tpl, spec, passes, launches } (vptmcm_debug_last_launch) */
+static napi_value js_last_launch(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (get_args(env, info, 1, argv)) return NULL;
+    vptmcm* h = get_handle(env, argv[0]);
+    if (!h) return NULL;
+    uint32_t v[4];
+    uint64_t n = 0;
+    int rc = vptmcm_debug_last_launch(h, v, &n);
+    if (rc) return throw_code(env, rc, vptmcm_last_error(h));
+    static const char* names[4] = {"mode", "tpl", "spec", "passes"};
+    napi_value o, x;
+    napi_create_object(env, &o);
+    for (int k = 0; k < 4; k++) {
+        napi_create_uint32(env, v[k], &x);
+        napi_set_named_property(env, o, names[k], x);
+    }
+    napi_create_double(env, (double)n, &x);
+    napi_set_named_property(env, o, "launches", x);
+    return o;
 }
 
 static napi_value js_version(napi_env env, napi_callback_info info) {
@@ -521,6 +559,7 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("commBarrier", js_comm_barrier);
     EXPORT("setBand", js_set_band);
     EXPORT("commGatherBands", js_comm_gather_bands);
+    EXPORT("lastLaunch", js_last_launch);
     EXPORT("version", js_version);
     return exports;
 }

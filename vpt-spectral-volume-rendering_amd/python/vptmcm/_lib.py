@@ -34,7 +34,7 @@ EXPORTS = [
     "vptmcm_enable_kernel_timing", "vptmcm_kernel_time", "vptmcm_comm_unique_id",
     "vptmcm_comm_init", "vptmcm_comm_allreduce_radiance", "vptmcm_comm_read_composite",
     "vptmcm_comm_barrier", "vptmcm_comm_allreduce_host", "vptmcm_debug_eval",
-    "vptmcm_debug_verify", "vptmcm_version",
+    "vptmcm_debug_verify", "vptmcm_debug_last_launch", "vptmcm_version",
 ]
 
 
@@ -117,6 +117,7 @@ def load() -> C.CDLL:
         "vptmcm_debug_eval": (C.c_int, [vp, C.c_int, u32p, u32p, C.c_uint32]),
         "vptmcm_debug_verify": (C.c_int, [vp, C.c_int, C.c_uint32, C.c_uint64,
                                           C.POINTER(C.c_uint64), u32p, C.c_uint32]),
+        "vptmcm_debug_last_launch": (C.c_int, [vp, u32p, C.POINTER(C.c_uint64)]),
         "vptmcm_version": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
@@ -239,6 +240,9 @@ class Renderer:
         self._ck(self.L.vptmcm_reset(self.h, _f32p(m), int(seed_bits) & 0xFFFFFFFF))
 
     def _stage_matrix(self, mvp) -> int:
+        # a scalar or a short array would broadcast below (len() is the cheap test)
+        if (len(mvp) if hasattr(mvp, "__len__") else 0) != 16 and np.size(mvp) != 16:
+            raise ValueError(f"matrix needs 16 values, got {np.size(mvp)}")
         try:
             self._m[:] = mvp  # 16 values (np.reshape alone costs ~1.7 us)
         except ValueError:
@@ -360,6 +364,14 @@ class Renderer:
         self._ck(self.L.vptmcm_debug_eval(self.h, fn, _u32p(i), _u32p(o), i.size))
         return o
 
+
+    def last_launch(self) -> dict:
+        """What the last march launch ran (vptmcm_debug_last_launch)."""
+        info = np.zeros(4, np.uint32)
+        n = C.c_uint64()
+        self._ck(self.L.vptmcm_debug_last_launch(self.h, _u32p(info), C.byref(n)))
+        return {"mode": int(info[0]), "tpl": int(info[1]), "spec": bool(info[2]),
+                "passes": int(info[3]), "launches": n.value}
 
     def uniform_bins(self) -> bool:
         """True when the current spectrum takes the arithmetic bin search."""

@@ -107,8 +107,16 @@ def _synth_lib():
 
 
 def host_threads() -> int:
-    n = os.cpu_count() or 1
-    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
+    """CPU threads the CPU baselines use: the CPUs this process may run on
+    (its affinity mask), capped by OMP_NUM_THREADS when the job sets it."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def fbm_volume(n: int, seed: int, octaves: int = 4, base_freq: float = 4.0,
