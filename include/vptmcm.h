@@ -109,7 +109,11 @@ int vptmcm_set_volume(vptmcm* h, const uint8_t* voxels, uint32_t width,
 
 /* Block-wise volume ingest, mirroring WebGPUVolume.readModality's per-placement
  * writeTexture(origin=[x,y,z]) (WebGPUVolume.js:67-93): begin allocates the
- * volume, each block lands at its origin, end re-lays it out. */
+ * volume (all zero, like a fresh texture), each block lands at its origin and
+ * the cells / bricks it touches are re-laid out at once (they are resident in
+ * HBM as soon as the placement arrives), end releases the staging copy. The
+ * volume is renderable from begin on: blocks not yet written read as zero
+ * density (the reference's renderers instead wait for Volume.ready). */
 int vptmcm_volume_begin(vptmcm* h, uint32_t width, uint32_t height, uint32_t depth);
 int vptmcm_volume_write_block(vptmcm* h, const uint8_t* data, uint32_t x, uint32_t y,
                               uint32_t z, uint32_t bw, uint32_t bh, uint32_t bd);

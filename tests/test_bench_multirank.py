@@ -40,7 +40,8 @@ DRIVER = textwrap.dedent('''
         def set_params(self, **kw): pass
         def comm_init(self, uid, world, rank):
             LOG.append(["comm_init", bytes(uid).hex()[:16], world, rank])
-            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.init_process_group("gloo", rank=rank, world_size=world,
+                                    timeout=__import__("datetime").timedelta(seconds=60))
         def barrier(self): dist.barrier()
         def reset(self, mvp, seed): LOG.append(["reset", int(seed)])
         def render_passes(self, mvp, seeds):
@@ -52,7 +53,10 @@ DRIVER = textwrap.dedent('''
             LOG.append(["timing"])
         def kernel_time(self):
             return (time.perf_counter() - self.t0) * 1e3 + 1e-3, self.launches
-        def allreduce_radiance(self): LOG.append(["allreduce"])
+        def allreduce_radiance(self):
+            LOG.append(["allreduce"])
+            if os.environ.get("FAKE_DIE_RANK") == os.environ["RANK"]:
+                os._exit(3)  # this rank dies before its first composite
         def read_composite(self):
             LOG.append(["composite"])
             return np.zeros((4, 4, 3), np.float32), np.zeros((4, 4), np.float32)
@@ -120,3 +124,30 @@ def test_bench_two_ranks_driver_command_line(tmp_path, world):
     for a in range(world):
         for b in range(a + 1, world):
             assert not set(seeds[a]) & set(seeds[b]), "ranks must use distinct seed streams"
+
+
+def test_bench_rank_death_ends_the_job(tmp_path):
+    """A rank that dies before the first radiance all-reduce must not leave the
+    others hanging: rank 0's next collective fails and bench.py exits non-zero
+    within the timeout, printing no result line. (On the GPU the library's RCCL
+    watchdog does the same: vptmcm_comm_* poll ncclCommGetAsyncError and abort
+    after VPTMCM_COMM_TIMEOUT_MS, test_comm_init_peer_never_joins.)"""
+    import time
+    port = _free_port()
+    argv = ["--gpus", "2", "--steps", "20", "--warmup", "5", "--volume", "16",
+            "--resolution", "16", "--cpu-seconds", "0"]
+    procs = []
+    t0 = time.monotonic()
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BENCH_ARGV=json.dumps(argv),
+                   BENCH_PATH=str(REPO / "bench.py"), LOG_OUT=str(tmp_path / f"log{rank}.json"),
+                   TORCHELASTIC_RUN_ID=f"d{port}", FAKE_DIE_RANK="1")
+        procs.append(subprocess.Popen([sys.executable, "-c", DRIVER], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True, cwd=str(tmp_path)))
+    outs = [p.communicate(timeout=240) for p in procs]
+    took = time.monotonic() - t0
+    assert procs[1].returncode == 3
+    assert procs[0].returncode != 0, outs[0]
+    assert not [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
+    assert took < 200, took

@@ -224,6 +224,58 @@ def test_photon_roundtrip_and_resume():
     gpu.close()
 
 
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_streamed_volume_renders_while_blocks_arrive(layout):
+    """Streaming ingest (SURVEY 8f f1, C5's brick streaming): every placement's
+    cells / bricks are re-laid out as it arrives, and the volume renders
+    throughout: before any block (a zero volume), between blocks (the blocks
+    not yet written read zero) and after volume_end, bit for bit against the
+    oracle on the same partially written volume. Ragged extents, 3-D blocks
+    of uneven sizes in shuffled order (block edges cut through bricks)."""
+    full = cf.fbm_volume(48, 31, nthreads=8)[:41, :45, :37].copy()  # [D, H, W]
+    D, H, W = full.shape
+    rng = np.random.default_rng(5)
+    zs, ys, xs = [0, 7, 20, 41], [0, 13, 30, 45], [0, 5, 22, 37]
+    blocks = [((x0, y0, z0), (x1, y1, z1)) for z0, z1 in zip(zs[:-1], zs[1:])
+              for y0, y1 in zip(ys[:-1], ys[1:]) for x0, x1 in zip(xs[:-1], xs[1:])]
+    order = rng.permutation(len(blocks))
+    R = 48
+    gpu, cpu = make_pair(R, np.zeros((2, 2, 2), np.uint8), cf.tf_spectral(), ext=24.0, layout=layout)
+    gpu.volume_begin(full.shape)
+    part = np.zeros_like(full)
+    cpu.volume = part.copy()
+    mvp = cf.golden_mvp("orbit")
+    seeds = cf.seed_stream(16, start=40)
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0])
+    k = 1
+
+    def step(what):
+        nonlocal k
+        gpu.render(mvp, seeds[k])
+        rgb, want = cpu.render(mvp, seeds[k])
+        k += 1
+        assert_photons_equal(gpu.read_photons(), cpu.photons, what)
+        assert_rgba_equal(gpu.read_rgba16f(), want, what)
+        assert_rgb32_equal(gpu.read_rgb(), rgb, what)
+
+    step("no block yet")
+    for j, bi in enumerate(order):
+        (x0, y0, z0), (x1, y1, z1) = blocks[bi]
+        gpu.volume_write_block((x0, y0, z0), full[z0:z1, y0:y1, x0:x1])
+        part[z0:z1, y0:y1, x0:x1] = full[z0:z1, y0:y1, x0:x1]
+        cpu.volume = part.copy()
+        if j % 6 == 5:
+            step(f"after {j + 1} of {len(blocks)} blocks")
+    gpu.volume_end()
+    assert np.array_equal(part, full)
+    step("after volume_end")
+    step("after volume_end, second pass")
+    with pytest.raises(vptmcm.VptError, match="outside volume_begin"):
+        gpu.volume_write_block((0, 0, 0), full[:1, :1, :1])
+    gpu.close()
+
+
 def test_blockwise_volume_ingest_equals_whole():
     """WebGPUVolume.readModality-style per-block writes land where they should."""
     vol = cf.fbm_volume(48, 99, nthreads=8)
@@ -349,8 +401,38 @@ def test_mode_b_gather_single_rank():
     gpu.reset(mvp, 5)
     gpu.render_passes(mvp, cf.seed_stream(4))
     img = gpu.read_rgb()
-    assert np.array_equal(gpu.gather_bands().view(np.uint32), img.view(np.uint32))
     assert not img[:16].any() and not img[48:].any()
+    # one rank's band must cover the frame: rows [0, 16) and [48, 64) are in no band
+    with pytest.raises(vptmcm.VptError, match="covered by 0 ranks") as e:
+        gpu.gather_bands()
+    assert e.value.code == vptmcm.ECOMM
+    gpu.set_band(0, 64)  # the communicator survives a coverage error
+    assert np.array_equal(gpu.gather_bands().view(np.uint32), img.view(np.uint32))
+    gpu.close()
+
+
+def test_comm_init_peer_never_joins():
+    """The RCCL watchdog: a 2-rank communicator whose second rank never joins
+    fails with ECOMM after VPTMCM_COMM_TIMEOUT_MS instead of hanging; the
+    handle stays usable without a communicator."""
+    import os
+    import time
+    gpu, _ = make_pair(32, cf.sphere_in_cube(32), cf.tf_spectral())
+    os.environ["VPTMCM_COMM_TIMEOUT_MS"] = "3000"
+    try:
+        t0 = time.monotonic()
+        with pytest.raises(vptmcm.VptError, match="comm_init") as e:
+            gpu.comm_init(vptmcm.unique_id(), 2, 0)
+        took = time.monotonic() - t0
+    finally:
+        del os.environ["VPTMCM_COMM_TIMEOUT_MS"]
+    assert e.value.code == vptmcm.ECOMM and 2.5 < took < 60.0, (str(e.value), took)
+    with pytest.raises(vptmcm.VptError, match="no communicator"):
+        gpu.barrier()
+    mvp = cf.default_mvp_inverse()
+    gpu.reset(mvp, 3)
+    gpu.render_passes(mvp, cf.seed_stream(2))
+    gpu.synchronize()
     gpu.close()
 
 

@@ -81,8 +81,11 @@ hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSee
                             uint16_t* rgba, float* rgb32, hipStream_t s,
                             hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr,
                             MarchLaunchInfo* info = nullptr);
+// LINEAR -> CORNER8 / BRICK8 relayout of the cell box [c0, c0 + n) (default:
+// every cell of the (W+1)(H+1)(D+1) grid)
 hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, uint32_t BW,
-                          uint32_t BH, void* out, hipStream_t s);
+                          uint32_t BH, void* out, hipStream_t s, const uint32_t c0[3] = nullptr,
+                          const uint32_t n[3] = nullptr);
 hipError_t launch_pack(const MarchParams& P, const float* ph, const float* rgb32, float4* out,
                        hipStream_t s);
 // fn 13 checks bin_of's arithmetic path against the count on the spectrum in P

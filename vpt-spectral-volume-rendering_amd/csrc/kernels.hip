@@ -981,17 +981,20 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
 // cell (cx,cy,cz) in [0,W]x[0,H]x[0,D] holds voxels clamp(c-1), clamp(c) per axis;
 // byte (dz*4 + dy*2 + dx) of the u64 = voxel (x0+dx, y0+dy, z0+dz).
 // BW == 0: raster cell order (CORNER8); else 4x4x4-cell bricks (BRICK8), BW x BH bricks per slab
+// Cells of the box [c0, c0 + n) (cell (cx, cy, cz) holds the 8 clamped voxels
+// (cx-1 .. cx, cy-1 .. cy, cz-1 .. cz)): the whole grid at volume_end, or the
+// cells a block touches as its placement arrives.
 __global__ __launch_bounds__(256) void k_corner8(const uint8_t* __restrict__ lin, uint32_t W,
                                                  uint32_t H, uint32_t D, uint32_t BW, uint32_t BH,
-                                                 uint2* __restrict__ out) {
+                                                 uint2* __restrict__ out, uint3 c0, uint3 n) {
   const uint32_t W1 = W + 1u, H1 = H + 1u;
-  const size_t ncell = (size_t)W1 * H1 * (D + 1u);
-  for (size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncell;
+  const size_t nbox = (size_t)n.x * n.y * n.z;
+  for (size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x; c < nbox;
        c += (size_t)gridDim.x * blockDim.x) {
-    uint32_t cx = (uint32_t)(c % W1);
-    size_t rest = c / W1;
-    uint32_t cy = (uint32_t)(rest % H1);
-    uint32_t cz = (uint32_t)(rest / H1);
+    const uint32_t cx = c0.x + (uint32_t)(c % n.x);
+    const size_t rest = c / n.x;
+    const uint32_t cy = c0.y + (uint32_t)(rest % n.y);
+    const uint32_t cz = c0.z + (uint32_t)(rest / n.y);
     uint32_t x0 = clampi((int)cx - 1, (int)W - 1), x1 = clampi((int)cx, (int)W - 1);
     uint32_t y0 = clampi((int)cy - 1, (int)H - 1), y1 = clampi((int)cy, (int)H - 1);
     uint32_t z0 = clampi((int)cz - 1, (int)D - 1), z1 = clampi((int)cz, (int)D - 1);
@@ -1003,7 +1006,7 @@ __global__ __launch_bounds__(256) void k_corner8(const uint8_t* __restrict__ lin
     v.y = (uint32_t)lin[r01 + x0] | ((uint32_t)lin[r01 + x1] << 8) |
           ((uint32_t)lin[r11 + x0] << 16) | ((uint32_t)lin[r11 + x1] << 24);
     if (BW == 0u) {
-      out[c] = v;
+      out[((size_t)cz * H1 + cy) * W1 + cx] = v;
     } else {
       const size_t brick = ((size_t)(cz >> 2) * BH + (cy >> 2)) * BW + (cx >> 2);
       out[(brick << 6) | brick_inner(cx, cy, cz)] = v;
@@ -1201,12 +1204,17 @@ hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSee
 }
 
 hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, uint32_t BW,
-                          uint32_t BH, void* out, hipStream_t s) {
-  size_t ncell = (size_t)(W + 1) * (H + 1) * (D + 1);
+                          uint32_t BH, void* out, hipStream_t s, const uint32_t c0[3],
+                          const uint32_t n[3]) {
+  const uint3 o = c0 ? make_uint3(c0[0], c0[1], c0[2]) : make_uint3(0u, 0u, 0u);
+  const uint3 e = n ? make_uint3(n[0], n[1], n[2]) : make_uint3(W + 1u, H + 1u, D + 1u);
+  if (o.x + e.x > W + 1u || o.y + e.y > H + 1u || o.z + e.z > D + 1u) return hipErrorInvalidValue;
+  const size_t ncell = (size_t)e.x * e.y * e.z;
+  if (ncell == 0) return hipSuccess;
   size_t blocks = (ncell + 255) / 256;
   if (blocks > 65536) blocks = 65536;
   hipLaunchKernelGGL(k_corner8, dim3((uint32_t)blocks), dim3(256), 0, s, lin, W, H, D, BW, BH,
-                     reinterpret_cast<uint2*>(out));
+                     reinterpret_cast<uint2*>(out), o, e);
   return hipGetLastError();
 }
 

@@ -50,7 +50,8 @@ struct vptmcm {
   uint8_t* vol_lin = nullptr;  // W*H*D (staging for CORNER8; the volume for LINEAR)
   void* vol_c8 = nullptr;      // (W+1)(H+1)(D+1) u64
   uint32_t W = 0, H = 0, D = 0;
-  bool volume_ready = false;
+  bool volume_ready = false;   // renderable: from volume_begin on (unwritten blocks read zero)
+  bool vol_done = false;       // LINEAR after volume_end (its staging copy is the volume)
   uint16_t* tf_rg = nullptr;   // 65536 (albedo | alpha << 8) texels
   uint32_t* tf_b4 = nullptr;   // 257*257 anisotropy corner cells
   uint8_t* tf_brow = nullptr;  // 256 anisotropy rows (valid when b_rows)
@@ -554,6 +555,7 @@ void free_volume(vptmcm* h) {
   h->vol_lin = nullptr;
   h->vol_c8 = nullptr;
   h->volume_ready = false;
+  h->vol_done = false;
   h->W = h->H = h->D = 0;
 }
 
@@ -707,6 +709,12 @@ void vptmcm_destroy(vptmcm* h) {
 
 // ------------------------------------------------------------------- inputs
 
+// Block-wise ingest. begin allocates the staging copy (x-fastest u8, zero like
+// a fresh texture) and, for CORNER8 / BRICK8, the cell array (zero cells = a
+// zero volume); every block is copied into the staging copy and the cells it
+// touches are re-laid out at once, so its bricks are resident in HBM as soon
+// as its placement arrives and the volume is renderable throughout (blocks
+// not yet written read as zero density); end frees the staging copy.
 int vptmcm_volume_begin(vptmcm* h, uint32_t width, uint32_t height, uint32_t depth) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
@@ -722,9 +730,30 @@ int vptmcm_volume_begin(vptmcm* h, uint32_t width, uint32_t height, uint32_t dep
   }
   // a fresh texture is zero; the block copies below run on the same stream, after it
   HIPCHK(h, hipMemsetAsync(h->vol_lin, 0, n, h->stream));
+  if (h->layout != kLayoutLinear) {
+    // CORNER8: (W+1)(H+1)(D+1) cells in raster order; BRICK8: the same cells
+    // in 4x4x4-cell bricks (the brick grid rounds each edge up to whole bricks)
+    const bool brick = h->layout == kLayoutBrick8;
+    const size_t bw = (width + kBrickCells) / kBrickCells, bh = (height + kBrickCells) / kBrickCells,
+                 bd = (depth + kBrickCells) / kBrickCells;
+    const size_t ncell = brick ? bw * bh * bd * 64 : (size_t)(width + 1) * (height + 1) * (depth + 1);
+    // VPTMCM_VOL_ALLOC=contig (measurement knob): a physically contiguous
+    // allocation, for the TLB reach of the 8.6 GB cell array of a 1024^3 volume
+    const char* va = getenv("VPTMCM_VOL_ALLOC");
+    const bool contig = va && strcmp(va, "contig") == 0;
+    if ((contig ? hipExtMallocWithFlags(&h->vol_c8, ncell * 8, hipDeviceMallocContiguous)
+                : hipMalloc(&h->vol_c8, ncell * 8)) != hipSuccess) {
+      h->vol_c8 = nullptr;
+      free_volume(h);
+      FAIL(h, VPTMCM_ENOMEM, "%s volume allocation of %zu bytes failed", brick ? "brick8" : "corner8",
+           ncell * 8);
+    }
+    HIPCHK(h, hipMemsetAsync(h->vol_c8, 0, ncell * 8, h->stream));
+  }
   h->W = width;
   h->H = height;
   h->D = depth;
+  h->volume_ready = true;
   return VPTMCM_OK;
 }
 
@@ -732,28 +761,38 @@ int vptmcm_volume_write_block(vptmcm* h, const uint8_t* data, uint32_t x, uint32
                               uint32_t bw, uint32_t bh, uint32_t bd) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
-  if (!h->vol_lin) FAIL(h, VPTMCM_ESTATE, "volume_write_block before volume_begin");
+  if (!h->vol_lin || h->vol_done)
+    FAIL(h, VPTMCM_ESTATE, "volume_write_block outside volume_begin .. volume_end");
   if (!data) FAIL(h, VPTMCM_EINVAL, "null block data");
   if ((uint64_t)x + bw > h->W || (uint64_t)y + bh > h->H || (uint64_t)z + bd > h->D)
     FAIL(h, VPTMCM_EINVAL, "block [%u,%u,%u]+[%u,%u,%u] exceeds volume %ux%ux%u", x, y, z, bw, bh,
          bd, h->W, h->H, h->D);
+  if (!bw || !bh || !bd) return VPTMCM_OK;
   HIPCHK(h, hipSetDevice(h->device));
-  // Every copy is ordered behind volume_begin's zero-fill on the handle's
-  // stream and completes before returning (the caller keeps the block buffer).
+  // Every copy is ordered behind volume_begin's zero-fill (and the renders
+  // queued before this call) on the handle's stream and completes before
+  // returning (the caller keeps the block buffer).
   if (bw == h->W && bh == h->H && x == 0 && y == 0) {  // whole slices: one contiguous copy
     HIPCHK(h, hipMemcpyAsync(h->vol_lin + (size_t)z * h->W * h->H, data, (size_t)bw * bh * bd,
                              hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    return VPTMCM_OK;
+  } else {
+    hipMemcpy3DParms p;
+    memset(&p, 0, sizeof p);
+    p.srcPtr = make_hipPitchedPtr((void*)data, bw, bw, bh);
+    p.dstPtr = make_hipPitchedPtr(h->vol_lin, h->W, h->W, h->H);
+    p.dstPos = make_hipPos(x, y, z);
+    p.extent = make_hipExtent(bw, bh, bd);
+    p.kind = hipMemcpyHostToDevice;
+    HIPCHK(h, hipMemcpy3DAsync(&p, h->stream));
   }
-  hipMemcpy3DParms p;
-  memset(&p, 0, sizeof p);
-  p.srcPtr = make_hipPitchedPtr((void*)data, bw, bw, bh);
-  p.dstPtr = make_hipPitchedPtr(h->vol_lin, h->W, h->W, h->H);
-  p.dstPos = make_hipPos(x, y, z);
-  p.extent = make_hipExtent(bw, bh, bd);
-  p.kind = hipMemcpyHostToDevice;
-  HIPCHK(h, hipMemcpy3DAsync(&p, h->stream));
+  if (h->layout != kLayoutLinear) {
+    // the cells whose 8 corners include a voxel of the block: x .. x + bw per axis
+    const bool brick = h->layout == kLayoutBrick8;
+    const uint32_t c0[3] = {x, y, z}, n[3] = {bw + 1u, bh + 1u, bd + 1u};
+    HIPCHK(h, launch_corner8(h->vol_lin, h->W, h->H, h->D,
+                             brick ? (h->W + kBrickCells) / kBrickCells : 0u,
+                             brick ? (h->H + kBrickCells) / kBrickCells : 0u, h->vol_c8, h->stream, c0, n));
+  }
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return VPTMCM_OK;
 }
@@ -761,29 +800,15 @@ int vptmcm_volume_write_block(vptmcm* h, const uint8_t* data, uint32_t x, uint32
 int vptmcm_volume_end(vptmcm* h) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
-  if (!h->vol_lin) FAIL(h, VPTMCM_ESTATE, "volume_end before volume_begin");
+  if (!h->vol_lin || h->vol_done) FAIL(h, VPTMCM_ESTATE, "volume_end without volume_begin");
   HIPCHK(h, hipSetDevice(h->device));
-  if (h->layout != kLayoutLinear) {
-    // CORNER8: (W+1)(H+1)(D+1) cells in raster order; BRICK8: the same cells
-    // in 4x4x4-cell bricks (the brick grid rounds each edge up to whole bricks)
-    const bool brick = h->layout == kLayoutBrick8;
-    const size_t bw = (h->W + kBrickCells) / kBrickCells, bh = (h->H + kBrickCells) / kBrickCells,
-                 bd = (h->D + kBrickCells) / kBrickCells;
-    size_t ncell = brick ? bw * bh * bd * 64 : (size_t)(h->W + 1) * (h->H + 1) * (h->D + 1);
-    if (hipMalloc(&h->vol_c8, ncell * 8) != hipSuccess) {
-      h->vol_c8 = nullptr;
-      FAIL(h, VPTMCM_ENOMEM, "%s volume allocation of %zu bytes failed", brick ? "brick8" : "corner8",
-           ncell * 8);
-    }
-    HIPCHK(h, launch_corner8(h->vol_lin, h->W, h->H, h->D, brick ? (uint32_t)bw : 0u,
-                             brick ? (uint32_t)bh : 0u, h->vol_c8, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (h->layout != kLayoutLinear) {  // every cell is current: the staging copy goes
     HIPCHK(h, hipFree(h->vol_lin));
     h->vol_lin = nullptr;
   } else {
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->vol_done = true;  // LINEAR: the staging copy is the volume
   }
-  h->volume_ready = true;
   return VPTMCM_OK;
 }
 

@@ -140,6 +140,21 @@ class MCMComputeRenderer extends PropertyBag {
   }
 
   // ---- extensions ----
+  // n render() calls in one enqueue (fused into 32-pass launches)
+  renderPasses(n) {
+    if (!this._volumeReady) throw new Error('render: no volume loaded (setVolume first)');
+    const m = mvpInverse(this._camera);
+    native().setParams(this._h, this.extinction, this.anisotropy, this.bounces, this.steps, 0);
+    const seeds = new Uint32Array(n);
+    for (let k = 0; k < n; k++) seeds[k] = f32bits(this._random());
+    native().renderPasses(this._h, m, seeds);
+  }
+
+  // What the last march launch ran: { mode, tpl, spec, passes, launches }
+  lastLaunch() {
+    return native().lastLaunch(this._h);
+  }
+
   readPhotons() {  // 64-B Photon records (Photon.wgsl)
     const R = this._resolution;
     const out = new Uint8Array(R * R * 64);

@@ -197,15 +197,27 @@ class Renderer:
         D, H, W = v.shape
         self._ck(self.L.vptmcm_set_volume(self.h, _ptr(v), W, H, D))
 
-    def volume_blocks(self, shape, blocks) -> None:
-        """Block-wise ingest: blocks = iterable of (origin_xyz, uint8 [d,h,w])."""
+    def volume_begin(self, shape) -> None:
+        """Start a block-wise ingest of a [D, H, W] volume (all zero until written)."""
         D, H, W = shape
         self._ck(self.L.vptmcm_volume_begin(self.h, W, H, D))
-        for (x, y, z), b in blocks:
-            b = np.ascontiguousarray(b, dtype=np.uint8)
-            d, hh, w = b.shape
-            self._ck(self.L.vptmcm_volume_write_block(self.h, _ptr(b), x, y, z, w, hh, d))
+
+    def volume_write_block(self, origin, block) -> None:
+        """One placement: uint8 [d, h, w] at origin (x, y, z)."""
+        b = np.ascontiguousarray(block, dtype=np.uint8)
+        d, hh, w = b.shape
+        x, y, z = origin
+        self._ck(self.L.vptmcm_volume_write_block(self.h, _ptr(b), x, y, z, w, hh, d))
+
+    def volume_end(self) -> None:
         self._ck(self.L.vptmcm_volume_end(self.h))
+
+    def volume_blocks(self, shape, blocks) -> None:
+        """Block-wise ingest: blocks = iterable of (origin_xyz, uint8 [d,h,w])."""
+        self.volume_begin(shape)
+        for origin, b in blocks:
+            self.volume_write_block(origin, b)
+        self.volume_end()
 
     def set_material_tf(self, tf: np.ndarray) -> None:
         t = np.ascontiguousarray(tf, dtype=np.uint8)
