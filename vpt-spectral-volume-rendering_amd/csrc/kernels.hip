@@ -15,6 +15,12 @@
 #ifndef VPT_PRIO
 #define VPT_PRIO 1  // s_setprio level of volume waves (0 = off); 11 % faster passes
 #endif
+#ifndef VPT_PRIO_BAL
+// 1: volume waves that share a SIMD balance their progress: at every pass
+// boundary a wave behind its SIMD-mate (fewer passes done, read from LDS)
+// raises its priority above it (experiment; timing only, results identical)
+#define VPT_PRIO_BAL 0
+#endif
 #include "stamp.h"  // measurement-build hooks (VPT_STAMP); empty in the product
 
 namespace vpt {
@@ -347,6 +353,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 
   __shared__ uint32_t s_red[17];
   __shared__ uint32_t s_tile[16];
+#if VPT_PRIO_BAL
+  __shared__ uint32_t s_prog[16];  // passes begun by each volume wave (~0u: not a volume wave)
+  __shared__ uint32_t s_simd[16];  // each wave's SIMD (HW_ID bits 5:4)
+#endif
 
   uint32_t tile;
   if (P.sched == 0u) {
@@ -398,6 +408,14 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     for (uint32_t k = threadIdx.x; k < kBinLutCells + kBinLutCells / 4; k += kMarchBlock)
       s_binlut[k] = bin_lut[k];
   }
+#if VPT_PRIO_BAL
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t my_simd = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u;
+  if ((threadIdx.x & 63u) == 0u) {
+    s_simd[wv] = my_simd;
+    s_prog[wv] = ~0u;
+  }
+#endif
   __syncthreads();
   if (live && !hot0) load_photon(ph, S, i, p);
   if (!live) {
@@ -483,8 +501,25 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   for (uint32_t pass = 0; pass < n_passes; pass++) {
 #if VPT_PRIO
   if (pass > 0u) hot = entered;
+#if VPT_PRIO_BAL
+  if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) {
+    if (lane == 0u) __hip_atomic_store(&s_prog[wv], pass, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    bool behind = false;
+#pragma unroll
+    for (uint32_t m = 0; m < 16u; m++) {
+      const uint32_t pm = __hip_atomic_load(&s_prog[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      behind = behind || (m != wv && s_simd[m] == my_simd && pm != ~0u && pm > pass);
+    }
+    if (__builtin_amdgcn_readfirstlane(behind ? 1u : 0u)) __builtin_amdgcn_s_setprio(VPT_PRIO + 1);
+    else __builtin_amdgcn_s_setprio(VPT_PRIO);
+  } else {
+    if (lane == 0u) __hip_atomic_store(&s_prog[wv], ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_s_setprio(0);
+  }
+#else
   if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) __builtin_amdgcn_s_setprio(VPT_PRIO);
   else __builtin_amdgcn_s_setprio(0);
+#endif
   entered = false;
 #endif
   uint32_t st = hash3(x, y, pass_seed(pass));  // wgsl:122 (state is not carried across passes)
