@@ -114,6 +114,16 @@ def main():
     out["fused_background_wave_us_median_by_simd_load"] = {
         int(k): round(float(np.median(dur[bgw & (bl == k)])), 2) for k in sorted(set(bl[bgw].tolist()))}
     out["fused_volume_wave_us_median"] = round(float(np.median(dur[volw])), 2)
+    # SIMDs holding two volume waves: when the first and the second of the pair end
+    first, second = [], []
+    for sid in ids[cnt == 2]:
+        d = np.sort(dur[(simd == sid) & volw])
+        first.append(d[0])
+        second.append(d[-1])
+    if first:
+        out["fused_pair_wave_us_median"] = {"first": round(float(np.median(first)), 2),
+                                            "second": round(float(np.median(second)), 2),
+                                            "second_max": round(float(np.max(second)), 2)}
     print(json.dumps(out))
 
 
