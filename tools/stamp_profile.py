@@ -71,7 +71,7 @@ def main():
         vol = ((w[:, 5] & 0xff) == 1) & (w[:, 3] > 0)
         lo = lambda x: (x & 0xFFFF).astype(np.float64)  # noqa: E731
         hi = lambda x: (x >> 16).astype(np.float64)  # noqa: E731
-        n = w[vol, 3].astype(np.float64)
+        n = (w[vol, 3] & 0xFFFF).astype(np.float64)
         seg = np.stack([lo(w[vol, 0]), hi(w[vol, 0]), lo(w[vol, 1]), hi(w[vol, 1]), lo(w[vol, 2])], 1)
         segs.append(seg / n[:, None])
         steps.append(n)
@@ -114,6 +114,12 @@ def main():
     out["fused_background_wave_us_median_by_simd_load"] = {
         int(k): round(float(np.median(dur[bgw & (bl == k)])), 2) for k in sorted(set(bl[bgw].tolist()))}
     out["fused_volume_wave_us_median"] = round(float(np.median(dur[volw])), 2)
+    sw, wd = (wf[:, 3] >> 16) & 0xFF, wf[:, 3] >> 24
+    if sw.any() or wd.any():  # tile-swap builds: swaps / withdrawn offers / offer wait per wave
+        out["swap"] = {"swaps_total": int(sw.sum()), "withdrawn_total": int(wd.sum()),
+                       "waves_swapping": int((sw > 0).sum()),
+                       "swaps_per_volume_wave_mean": round(float(sw[volw].mean()), 2),
+                       "withdrawn_per_volume_wave_mean": round(float(wd[volw].mean()), 2)}
     # SIMDs holding two volume waves: when the first and the second of the pair end
     first, second = [], []
     for sid in ids[cnt == 2]:

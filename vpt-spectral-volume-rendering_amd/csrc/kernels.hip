@@ -15,28 +15,6 @@
 #ifndef VPT_PRIO
 #define VPT_PRIO 1  // s_setprio level of volume waves (0 = off); 11 % faster passes
 #endif
-#ifndef VPT_SWAP
-// 1: the two volume waves of a SIMD swap tiles at pass boundaries when one is
-// VPT_SWAP_GAP passes ahead of the other (the issue arbitration favours the
-// older wave, so the lagging tile moves to it); photon state moves through its
-// home slots in HBM, the handshake through LDS. Timing only: every photon's
-// passes run in order with their own seeds, so results are identical.
-#define VPT_SWAP 0
-#endif
-#ifndef VPT_SWAP_GAP
-#define VPT_SWAP_GAP 2
-#endif
-#ifndef VPT_SWAP_HOLD
-// a wave offers only a tile it has run for this many passes: right after a
-// swap the slow wave holds the tile that is ahead, and must not hand it back
-#define VPT_SWAP_HOLD 4
-#endif
-#ifndef VPT_PRIO_BAL
-// 1: volume waves that share a SIMD balance their progress: at every pass
-// boundary a wave behind its SIMD-mate (fewer passes done, read from LDS)
-// raises its priority above it (experiment; timing only, results identical)
-#define VPT_PRIO_BAL 0
-#endif
 #include "stamp.h"  // measurement-build hooks (VPT_STAMP); empty in the product
 
 namespace vpt {
@@ -327,26 +305,6 @@ __device__ __forceinline__ const __attribute__((address_space(4))) float* cmf_ta
                                                                offsetof(MarchParams, xb)) / 4);
 }
 
-#if VPT_SWAP
-// LDS handshake helpers of the tile swap (wave-uniform results)
-__device__ __forceinline__ uint32_t lds_ld(uint32_t* a) {
-  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
-__device__ __forceinline__ void lds_st0(uint32_t* a, uint32_t v, uint32_t lane) {
-  if (lane == 0u) __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ bool lds_cas0(uint32_t* a, uint32_t expect, uint32_t desired, uint32_t lane) {
-  uint32_t ok = 0u;
-  if (lane == 0u) {
-    uint32_t e = expect;
-    ok = __hip_atomic_compare_exchange_strong(a, &e, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
-  }
-  return __builtin_amdgcn_readlane(ok, 0) != 0u;
-}
-constexpr uint64_t kSwapWaitTicks = 4000;  // s_memrealtime (100 MHz): 40 us, then withdraw the offer
-#endif
-
 // MODE: 0 generic; 1 every radiance bin in use (nb >= 12); 2 (FAST, the
 // benchmark configuration) additionally equal-width bins (bin_of's arithmetic
 // path), a wavelength-invariant TF blue channel (LDS row table), blur == 0 with
@@ -389,16 +347,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 
   __shared__ uint32_t s_red[17];
   __shared__ uint32_t s_tile[16];
-#if VPT_PRIO_BAL || VPT_SWAP
-  __shared__ uint32_t s_prog[16];  // passes begun by each volume wave (~0u: not a volume wave)
-  __shared__ uint32_t s_simd[16];  // each wave's SIMD (HW_ID bits 5:4)
-#endif
-#if VPT_SWAP
-  // per SIMD: the swap handshake (0 idle, 4<<8|w slot reserved by wave w,
-  // 1<<8|w offered by w, 3<<8|w being accepted by w, 2<<8|w accepted by w)
-  // and the tiles / passes traded
-  __shared__ uint32_t s_xchg[4], s_xtile[4], s_xpass[4], s_atile[4], s_apass[4];
-#endif
 
   uint32_t tile;
   if (P.sched == 0u) {
@@ -408,9 +356,9 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     if (tile >= P.n_tiles) tile = 0xffffffffu;
   }
   const uint32_t lane = threadIdx.x & 63u;
-  uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
-  uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
-  size_t i = (size_t)tile * 64u + lane;
+  const uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
+  const uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
+  const size_t i = (size_t)tile * 64u + lane;
   // tiles outside the band (whole tiles: band rows are multiples of 8) are idle
   const bool live = tile != 0xffffffffu && x < P.R && y < P.R && y >= P.band_y0 && y < P.band_y1;
   const size_t S = P.npad;
@@ -450,17 +398,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     for (uint32_t k = threadIdx.x; k < kBinLutCells + kBinLutCells / 4; k += kMarchBlock)
       s_binlut[k] = bin_lut[k];
   }
-#if VPT_PRIO_BAL || VPT_SWAP
-  const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t my_simd = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u;
-  if ((threadIdx.x & 63u) == 0u) {
-    s_simd[wv] = my_simd;
-    s_prog[wv] = ~0u;
-  }
-#endif
-#if VPT_SWAP
-  if (threadIdx.x < 4u) s_xchg[threadIdx.x] = 0u;
-#endif
   __syncthreads();
   if (live && !hot0) load_photon(ph, S, i, p);
   if (!live) {
@@ -474,7 +411,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   f3 from{0.0f, 0.0f, 0.0f};
   bool fixed = near_fixed(P, sx, sy, from);
   WaveConst wc = wave_const(p.lambda, s_light);
-  bool slab_hw = __builtin_amdgcn_ballot_w64(!slab_generic(fixed, from)) == 0ull;
+  const bool slab_hw = __builtin_amdgcn_ballot_w64(!slab_generic(fixed, from)) == 0ull;
   // 1 - from, kept in VGPRs for the whole launch (the backend would otherwise
   // recompute it in every step's reset candidate)
   f3 omf{1.0f - from.x, 1.0f - from.y, 1.0f - from.z};
@@ -491,16 +428,9 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   // whose lanes are all in that state (background tiles) skips the distance
   // log, the advance, the bounds test and the ray-start slab test, and
   // materialises the start point once, at the end of the launch.
-  bool rbpix = P.robust != 0u && fixed &&
-               (sx < P.rb_x0 || sx > P.rb_x1 || sy < P.rb_y0 || sy > P.rb_y1);
+  const bool rbpix = P.robust != 0u && fixed &&
+                     (sx < P.rb_x0 || sx > P.rb_x1 || sy < P.rb_y0 || sy > P.rb_y1);
   bool rb = false, stale = false;
-#if VPT_SWAP
-  // swaps trade whole tiles between whole waves: every lane live, scheduled tiles
-  const bool swap_ok = (P.R & 7u) == 0u && P.sched == 0u &&
-                       __builtin_amdgcn_ballot_w64(true) == ~0ull;
-  bool tile_vol = hot0;  // the current tile entered the volume in the previous launch
-  uint32_t held = 0u;    // passes run on the current tile since it was received
-#endif
   // add_radiance of a termination is deferred into the next step's gather
   // shadow (it only touches the radiance bins, applied in the same order),
   // across pass boundaries too: only the launch's last pass applies it at its
@@ -553,132 +483,9 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   for (uint32_t pass = 0; pass < n_passes; pass++) {
 #if VPT_PRIO
   if (pass > 0u) hot = entered;
-#if VPT_PRIO_BAL
-  if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) {
-    if (lane == 0u) __hip_atomic_store(&s_prog[wv], pass, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    bool behind = false;
-#pragma unroll
-    for (uint32_t m = 0; m < 16u; m++) {
-      const uint32_t pm = __hip_atomic_load(&s_prog[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      behind = behind || (m != wv && s_simd[m] == my_simd && pm != ~0u && pm > pass);
-    }
-    if (__builtin_amdgcn_readfirstlane(behind ? 1u : 0u)) __builtin_amdgcn_s_setprio(VPT_PRIO + 1);
-    else __builtin_amdgcn_s_setprio(VPT_PRIO);
-  } else {
-    if (lane == 0u) __hip_atomic_store(&s_prog[wv], ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __builtin_amdgcn_s_setprio(0);
-  }
-#else
   if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) __builtin_amdgcn_s_setprio(VPT_PRIO);
   else __builtin_amdgcn_s_setprio(0);
-#endif
   entered = false;
-#endif
-#if VPT_SWAP
-  // Tile swap at the pass boundary (see VPT_SWAP): the wave ahead of its
-  // SIMD-mate by VPT_SWAP_GAP passes offers its tile and sleeps (its mate
-  // runs alone meanwhile); the mate, at its own boundary, takes the offered
-  // tile and leaves its own. Each tile keeps its pass count, so every photon
-  // runs the same passes in the same order. Whole tiles only (R % 8 == 0).
-  if (swap_ok && pass > 0u) {
-    held++;
-    const bool vol_wave = tile_vol;  // wave-uniform
-    lds_st0(&s_prog[wv], vol_wave ? pass : ~0u, lane);
-    if (vol_wave) {
-      const uint32_t xs = lds_ld(&s_xchg[my_simd]);
-      uint32_t act = 0u;  // 1 accept the mate's offer, 2 offer mine
-      if ((xs >> 8) == 1u && (xs & 0xffu) != wv) {
-        if (pass < lds_ld(&s_xpass[my_simd]) && lds_cas0(&s_xchg[my_simd], xs, (3u << 8) | wv, lane))
-          act = 1u;
-      } else if (xs == 0u && pass + 1u < n_passes && held >= VPT_SWAP_HOLD) {
-        bool ahead = false;
-#pragma unroll
-        for (uint32_t m = 0; m < 16u; m++) {
-          const uint32_t pm = lds_ld(&s_prog[m]);
-          ahead = ahead || (m != wv && s_simd[m] == my_simd && pm != ~0u && pm + VPT_SWAP_GAP <= pass);
-        }
-        if (ahead) act = 2u;
-      }
-#if VPT_SWAP_TEST == 1
-      act = 0u;  // test build: the decision only
-#elif VPT_SWAP_TEST == 2
-      act = 3u;  // test build: every wave stores and reloads its own tile at every boundary
-#endif
-      if (act != 0u) {
-        // the current tile back to its home slots, in a state the next owner resumes exactly
-        apply_pending();
-        if (stale) p.pos = ray_start(from, p.dir);
-        stale = false;
-        rb = false;
-        store_state(ph, S, i, p);
-#pragma unroll
-        for (int b = 0; b < kMaxBins; b++)
-          if (NBF || !VPT_NB_ZERO || (uint32_t)b < P.nb) ph[(kRad0 + b) * S + i] = p.rad[b];
-        uint32_t nt = tile, np = pass;
-        if (act == 3u) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        } else if (act == 1u) {
-          nt = lds_ld(&s_xtile[my_simd]);
-          np = lds_ld(&s_xpass[my_simd]);
-          lds_st0(&s_atile[my_simd], tile, lane);
-          lds_st0(&s_apass[my_simd], pass, lane);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          lds_st0(&s_xchg[my_simd], (2u << 8) | wv, lane);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        } else if (lds_cas0(&s_xchg[my_simd], 0u, (4u << 8) | wv, lane)) {  // slot reserved
-          lds_st0(&s_xtile[my_simd], tile, lane);
-          lds_st0(&s_xpass[my_simd], pass, lane);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          lds_st0(&s_xchg[my_simd], (1u << 8) | wv, lane);
-          {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            for (;;) {
-              const uint32_t v = lds_ld(&s_xchg[my_simd]);
-              if ((v >> 8) == 2u) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                nt = lds_ld(&s_atile[my_simd]);
-                np = lds_ld(&s_apass[my_simd]);
-                lds_st0(&s_xchg[my_simd], 0u, lane);
-                break;
-              }
-              // no taker in time: withdraw (fails once a mate has begun accepting)
-              if ((v >> 8) == 1u && __builtin_amdgcn_s_memrealtime() - t0 > kSwapWaitTicks &&
-                  lds_cas0(&s_xchg[my_simd], v, 0u, lane))
-                break;
-              __builtin_amdgcn_s_sleep(2);
-            }
-          }
-        }
-        if (nt != tile || act == 3u) {
-          tile = nt;
-          pass = np;
-          x = (tile % P.tiles_x) * 8u + (lane & 7u);
-          y = (tile / P.tiles_x) * 8u + (lane >> 3);
-          i = (size_t)tile * 64u + lane;
-          screen_of(P, x, y, sx, sy);
-          from = f3{0.0f, 0.0f, 0.0f};
-          fixed = near_fixed(P, sx, sy, from);
-          slab_hw = __builtin_amdgcn_ballot_w64(!slab_generic(fixed, from)) == 0ull;
-          omf = f3{1.0f - from.x, 1.0f - from.y, 1.0f - from.z};
-          asm volatile("" : "+v"(omf.x), "+v"(omf.y), "+v"(omf.z));
-          rbpix = P.robust != 0u && fixed && (sx < P.rb_x0 || sx > P.rb_x1 || sy < P.rb_y0 || sy > P.rb_y1);
-          load_photon(ph, S, i, p);
-#if VPT_NB_ZERO
-          if constexpr (!NBF) {
-#pragma unroll
-            for (int b = 0; b < kMaxBins; b++)
-              if ((uint32_t)b >= P.nb) p.rad[b] = 0.0f;
-          }
-#endif
-          wc = wave_const(p.lambda, s_light);
-          tile_vol = true;
-          held = 0u;
-          lds_st0(&s_prog[wv], pass, lane);
-        }
-      }
-    }
-  }
 #endif
   uint32_t st = hash3(x, y, pass_seed(pass));  // wgsl:122 (state is not carried across passes)
 
