@@ -180,7 +180,9 @@ int vptmcm_render(vptmcm* h, const float* mvp_inverse /* 16 */, uint32_t seed_bi
 int vptmcm_render_passes(vptmcm* h, const float* mvp_inverse, const uint32_t* seed_bits,
                          uint32_t n);
 
-/* Block until all work enqueued on the handle's streams (march + composite) has finished. */
+/* Block until all work enqueued on the handle's streams (march + composite) has finished.
+ * The wait polls the stream for up to VPTMCM_SYNC_SPIN_US microseconds (environment,
+ * read at create; default 2000, 0 = block at once) before blocking. */
 int vptmcm_synchronize(vptmcm* h);
 
 /* ---- outputs ------------------------------------------------------------- */

@@ -36,6 +36,15 @@ for s in $STEPS; do
   latency)  # first-region and median wall overhead of the driver's 20-pass region
     timeout -k 10 300 python tools/launch_latency.py --passes 20 --regions 40 > $OUT/latency.json 2> $OUT/latency.err
     rc=$?; echo "latency rc=$rc" | tee -a $OUT/status.txt; cat $OUT/latency.json; fault $rc && exit $rc ;;
+  latab)  # spin-then-block vs blocking synchronize: region overhead and the driver's line, ABBA
+    for sp in 0 2000 2000 0; do
+      VPTMCM_SYNC_SPIN_US=$sp timeout -k 10 300 python tools/launch_latency.py --passes 20 --regions 40 > $OUT/lat_$sp.json 2>> $OUT/latency.err
+      rc=$?; [ $rc -ne 0 ] && { echo "latab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      VPTMCM_SYNC_SPIN_US=$sp timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --js-steps 0 > $OUT/drv_$sp.json 2>> $OUT/latency.err
+      rc=$?; [ $rc -ne 0 ] && { echo "latab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      python3 -c "import json,sys; l=json.load(open('$OUT/lat_$sp.json')); d=json.load(open('$OUT/drv_$sp.json')); print(json.dumps({'spin_us': $sp, 'overhead_us': l['overhead_us'], 'first': l['first'], 'drv_value': d['value'], 'drv_ms_step': d['ms_per_step'], 'drv_kern_us': d['roofline']['kernel_avg_us']}))" >> $OUT/latab.jsonl
+    done
+    echo "latab rc=0" | tee -a $OUT/status.txt; cat $OUT/latab.jsonl ;;
   cost)  # floor of a one-pass launch (tools/launch_cost.hip)
     timeout -k 10 120 tools/launch_cost > $OUT/launch_cost.json 2>&1
     rc=$?; echo "cost rc=$rc" | tee -a $OUT/status.txt; cat $OUT/launch_cost.json; fault $rc && exit $rc ;;

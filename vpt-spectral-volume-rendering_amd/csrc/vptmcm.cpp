@@ -88,6 +88,11 @@ struct vptmcm {
   EventPair region;
   uint64_t launches = 0;
   uint64_t march_launches = 0;  // every march launch since create (vptmcm_debug_last_launch)
+  // vptmcm_synchronize / kernel_time poll the stream for up to this long before
+  // blocking (VPTMCM_SYNC_SPIN_US, 0 = block at once): a blocking wait wakes
+  // through an interrupt, whose latency on a busy host adds tens of
+  // microseconds to every short region
+  int64_t sync_spin_us = 2000;
   MarchLaunchInfo last_launch{};
 
   // multi-GPU
@@ -525,8 +530,22 @@ int comm_call(vptmcm* h, ncclResult_t r, const char* what) {
 // RCCL work (or wait on it), so the wait polls the stream and the
 // communicator's asynchronous error, spinning first (a composite is a few
 // hundred microseconds), and gives up after the communicator timeout.
+int64_t now_us() {
+  return std::chrono::duration_cast<std::chrono::microseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int wait_stream(vptmcm* h, hipStream_t s, const char* what) {
   if (!h->comm) {
+    if (h->sync_spin_us > 0) {  // spin, then block
+      const int64_t t0 = now_us();
+      for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return VPTMCM_OK;
+        if (e != hipErrorNotReady) FAIL(h, VPTMCM_EHIP, "%s: %s", what, hipGetErrorString(e));
+        if (now_us() - t0 > h->sync_spin_us) break;
+      }
+    }
     HIPCHK(h, hipStreamSynchronize(s));
     return VPTMCM_OK;
   }
@@ -620,6 +639,7 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
     (void)hipGetDevice(&h->device);
   }
   if (const char* v = getenv("VPTMCM_TIME_STOP")) h->time_stop = v[0] != '0';
+  if (const char* v = getenv("VPTMCM_SYNC_SPIN_US")) h->sync_spin_us = strtoll(v, nullptr, 10);
   h->layout = cfg->volume_layout;
   h->kind = cfg->renderer;
   if (const char* v = getenv("VPTMCM_MARCH_VARIANT")) h->variant = (uint32_t)strtoul(v, nullptr, 0);
@@ -1183,9 +1203,12 @@ int vptmcm_enable_kernel_timing(vptmcm* h, int enable) {
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->timing = enable != 0;
-  if (h->timing && !h->region.beg) {  // created here, outside the region they time
+  if (h->timing && !h->region.beg) {  // created and first recorded here, outside the region they time
     HIPCHK(h, hipEventCreateWithFlags(&h->region.beg, hipEventDisableSystemFence));
     HIPCHK(h, hipEventCreateWithFlags(&h->region.end, hipEventDisableSystemFence));
+    HIPCHK(h, hipEventRecord(h->region.beg, h->stream));
+    HIPCHK(h, hipEventRecord(h->region.end, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
   }
   h->launches = 0;
   h->region_closed = false;
@@ -1199,7 +1222,7 @@ int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
   HIPCHK(h, hipSetDevice(h->device));
   int rc = time_close(h);
   if (rc) return rc;
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if ((rc = wait_stream(h, h->stream, "kernel_time"))) return rc;
   float ms = 0.0f;
   if (h->timing && h->launches) HIPCHK(h, hipEventElapsedTime(&ms, h->region.beg, h->region.end));
   *total_ms = ms;
