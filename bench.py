@@ -220,7 +220,10 @@ def main():
     r.set_spectrum(spec)
     r.set_params(extinction=a.extinction, bounces=8, steps=S)
 
-    multi = world > 1
+    # VPTMCM_BENCH_FORCE_COMM=1: the N > 1 code path (RCCL communicator,
+    # composites, barriers, max-over-ranks) with however many ranks there are,
+    # e.g. one: a hardware check of that path on a one-GPU box
+    multi = world > 1 or os.environ.get("VPTMCM_BENCH_FORCE_COMM") == "1"
     if multi:
         key = rendezvous.job_key()
         uid = rendezvous.exchange_unique_id(rank, vptmcm.unique_id, key=key)

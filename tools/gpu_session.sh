@@ -45,6 +45,9 @@ for s in $STEPS; do
       python3 -c "import json,sys; l=json.load(open('$OUT/lat_$sp.json')); d=json.load(open('$OUT/drv_$sp.json')); print(json.dumps({'spin_us': $sp, 'overhead_us': l['overhead_us'], 'first': l['first'], 'drv_value': d['value'], 'drv_ms_step': d['ms_per_step'], 'drv_kern_us': d['roofline']['kernel_avg_us']}))" >> $OUT/latab.jsonl
     done
     echo "latab rc=0" | tee -a $OUT/status.txt; cat $OUT/latab.jsonl ;;
+  comm1)  # the N > 1 bench path (RCCL communicator, composites, barriers) with one rank
+    VPTMCM_BENCH_FORCE_COMM=1 timeout -k 10 300 python bench.py --steps 64 --warmup 64 --cpu-seconds 0 > $OUT/comm1.json 2> $OUT/comm1.err
+    rc=$?; echo "comm1 rc=$rc" | tee -a $OUT/status.txt; cat $OUT/comm1.json; fault $rc && exit $rc ;;
   cost)  # floor of a one-pass launch (tools/launch_cost.hip)
     timeout -k 10 120 tools/launch_cost > $OUT/launch_cost.json 2>&1
     rc=$?; echo "cost rc=$rc" | tee -a $OUT/status.txt; cat $OUT/launch_cost.json; fault $rc && exit $rc ;;
