@@ -2,8 +2,8 @@
 driver's torch.distributed.run, with the renderer replaced by a recording fake
 whose barrier / max-over-ranks / all-reduce run over gloo. Checks that the
 driver's command line (--steps 20 --warmup 5, fewer passes than the composite
-interval) still ends the timed region with a radiance all-reduce and a
-composite read, that ranks use distinct seed streams, that the rendezvous
+interval) still ends the timed region with a radiance all-reduce (its host
+readback follows the region), that ranks use distinct seed streams, that the rendezvous
 hands every rank the same unique id, and that rank 0 prints one JSON line with
 the whole-job value."""
 import json
