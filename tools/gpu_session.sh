@@ -48,6 +48,9 @@ for s in $STEPS; do
   comm1)  # the N > 1 bench path (RCCL communicator, composites, barriers) with one rank
     VPTMCM_BENCH_FORCE_COMM=1 timeout -k 10 300 python bench.py --steps 64 --warmup 64 --cpu-seconds 0 > $OUT/comm1.json 2> $OUT/comm1.err
     rc=$?; echo "comm1 rc=$rc" | tee -a $OUT/status.txt; cat $OUT/comm1.json; fault $rc && exit $rc ;;
+  commt)  # host timing of each call of the composite path (one rank)
+    timeout -k 10 300 python tools/comm_timing.py > $OUT/comm_timing.json 2> $OUT/comm_timing.err
+    rc=$?; echo "commt rc=$rc" | tee -a $OUT/status.txt; cat $OUT/comm_timing.json; fault $rc && exit $rc ;;
   cost)  # floor of a one-pass launch (tools/launch_cost.hip)
     timeout -k 10 120 tools/launch_cost > $OUT/launch_cost.json 2>&1
     rc=$?; echo "cost rc=$rc" | tee -a $OUT/status.txt; cat $OUT/launch_cost.json; fault $rc && exit $rc ;;
