@@ -505,7 +505,18 @@ def main():
                          "kernel": "k_march", "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                          "passes_per_launch": ppl,
                          "kernel_us_per_pass": round(kern_ms_max * 1e3 / a.steps, 3),
-                         "algorithmic_bytes_per_launch": bytes_per_launch},
+                         "algorithmic_bytes_per_launch": bytes_per_launch,
+                         # SURVEY 8(d)'s per-unit figure (31.0 B per photon-step at
+                         # nb = 12, S = 8: the reference materialises the photon
+                         # state and the image every pass) x the photon-steps of the
+                         # timed region, over the same GPU time; `frac` above counts
+                         # only the bytes this build's fused launches materialise
+                         "per_unit": {
+                             "bytes_per_photon_step": round(cf.algorithmic_bytes_per_pass(R, S) / (R * R * S), 2),
+                             "achieved": round(cf.algorithmic_bytes_per_pass(R, S) * a.steps
+                                               / (kern_ms_max * 1e-3) / 1e9, 1),
+                             "frac": round(cf.algorithmic_bytes_per_pass(R, S) * a.steps
+                                           / (kern_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}},
             "unfused": unfused,
             "render_api": render_api,
             "js_api": js_api,

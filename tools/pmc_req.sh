@@ -33,7 +33,7 @@ done
 for ppl in ${PPL:-20 32}; do
   for grp in ${GROUPS_BENCH:-req fetch write sq}; do
     run "bench$ppl" "$grp" python3 "$GRAFT_REPO_ROOT/bench.py" --steps $ppl --warmup 64 --unfused-steps 0 \
-        --api-steps 0 --general-steps 0 --rgb-steps 0 --settle-ms 0 --cpu-seconds 0 ${BENCH_ARGS:-} || exit 1
+        --api-steps 0 --general-steps 0 --rgb-steps 0 --js-steps 0 --settle-ms 0 --cpu-seconds 0 ${BENCH_ARGS:-} || exit 1
   done
 done
 exit 0

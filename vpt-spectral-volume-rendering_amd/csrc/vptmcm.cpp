@@ -117,6 +117,7 @@ struct vptmcm {
   uint32_t pend_seeds[kMaxFusedPasses];
   float pend_mvp[16];
   double* host_scratch = nullptr;
+  float4* comp_host = nullptr;  // pinned host copy of a composite (vptmcm_comm_read_composite)
 
   std::string err;
 };
@@ -706,6 +707,7 @@ void vptmcm_destroy(vptmcm* h) {
     if (h->comp_done[k]) (void)hipEventDestroy(h->comp_done[k]);
   }
   if (h->host_scratch) (void)hipFree(h->host_scratch);
+  if (h->comp_host) (void)hipHostFree(h->comp_host);
   if (h->region.beg) (void)hipEventDestroy(h->region.beg);
   if (h->region.end) (void)hipEventDestroy(h->region.end);
   free_volume(h);
@@ -1278,6 +1280,7 @@ int vptmcm_comm_init(vptmcm* h, const uint8_t* uid, int nranks, int rank) {
     HIPCHK(h, hipEventRecord(h->comp_done[k], h->comm_stream));
   }
   HIPCHK(h, hipMalloc(&h->host_scratch, 64 * sizeof(double)));
+  HIPCHK(h, hipHostMalloc(reinterpret_cast<void**>(&h->comp_host), bytes, hipHostMallocDefault));
   return VPTMCM_OK;
 }
 
@@ -1309,13 +1312,18 @@ int vptmcm_comm_read_composite(vptmcm* h, float* rgb, float* counts) {
   if (!h->comm || h->comp_last < 0) FAIL(h, VPTMCM_ESTATE, "read_composite: no all-reduce issued");
   if (!rgb) FAIL(h, VPTMCM_EINVAL, "read_composite: null output");
   HIPCHK(h, hipSetDevice(h->device));
+  const size_t npx = (size_t)h->R * h->R;
+  // ordered behind the last all-reduce on its own stream (the march stream
+  // keeps running), into pinned memory
+  HIPCHK(h, hipMemcpyAsync(h->comp_host, h->comp[h->comp_last], npx * sizeof(float4),
+                           hipMemcpyDeviceToHost, h->comm_stream));
   if (int rc = wait_stream(h, h->comm_stream, "comm_read_composite")) return rc;
-  size_t npx = (size_t)h->R * h->R;
-  std::vector<float> buf(npx * 4);
-  HIPCHK(h, hipMemcpy(buf.data(), h->comp[h->comp_last], npx * 16, hipMemcpyDeviceToHost));
+  const float4* buf = h->comp_host;
   for (size_t i = 0; i < npx; i++) {
-    float n = buf[i * 4 + 3];
-    for (int c = 0; c < 3; c++) rgb[i * 3 + c] = n > 0.0f ? buf[i * 4 + c] / n : 0.0f;
+    const float n = buf[i].w;
+    rgb[i * 3 + 0] = n > 0.0f ? buf[i].x / n : 0.0f;
+    rgb[i * 3 + 1] = n > 0.0f ? buf[i].y / n : 0.0f;
+    rgb[i * 3 + 2] = n > 0.0f ? buf[i].z / n : 0.0f;
     if (counts) counts[i] = n;
   }
   return VPTMCM_OK;
