@@ -221,3 +221,20 @@ def test_js_mode_b_band_matches_full_frame(tmp_path):
     assert not rgb_b[:y0].any() and not rgb_b[y1:].any()
     rows = ph_f.reshape(R, R, 36)[y0:y1]
     assert np.array_equal(ph_b.reshape(R, R, 36)[y0:y1], rows)
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+def test_napi_guards_and_extensions():
+    """N-API output arrays are checked against the handle's own R (a caller's
+    smaller R is refused, not written past); renderPasses(n) / lastLaunch() on
+    both JS renderer classes (40 passes = 32 + 8, 33 = 32 + 1)."""
+    r = subprocess.run(["node", str(ROOT / "tests" / "js" / "gpu_guards.js")], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ("small_rgb", "small_rgba", "small_photons"):
+        assert out[k] and "does not match" in out[k], (k, out[k])
+    assert out["short_array"] and "too short" in out["short_array"], out["short_array"]
+    assert out["ok_rgb"] is None
+    assert out["spectral_launches"] == 2 and out["spectral_last"]["passes"] == 8, out
+    assert out["rgb_launches"] == 2 and out["rgb_last"]["passes"] == 1, out
