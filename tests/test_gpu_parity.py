@@ -150,6 +150,22 @@ def test_tf_modes_bitexact(variant, spec, tfname, monkeypatch):
     gpu, cpu = make_pair(64, cf.fbm_volume(64, 7, nthreads=8), tf, spec=spec, ext=24.0)
     run_and_compare(gpu, cpu, cf.default_mvp_inverse(), cf.seed_stream(4, start=0),
                     f"variant {variant} bins {spec} tf {tfname}")
+    # the specialisation that ran: "12" is the only layout with the arithmetic
+    # (equal-width) bin search; every other one takes the exact bin table
+    # (MODE 6 / 7) unless variant bit 6 keeps the comparison search (4 / 5)
+    uniform = spec == "12"
+    if variant == "16":
+        want = 1 if spec in ("12", "12_wide") else 0
+    elif variant == "32":
+        want = 0
+    elif tfname == "many_rows_b":
+        want = 5 if variant == "64" else 7
+    elif uniform:
+        want = 2 if tfname == "materials_const_b" else 3
+    else:
+        want = 4 if variant == "64" else 6
+    info = gpu.last_launch()
+    assert info["mode"] == want, (variant, spec, tfname, info)
     gpu.close()
 
 
