@@ -221,20 +221,26 @@ __device__ __forceinline__ void add_radiance(const MarchParams& P, float* rad, f
 // (a Latin square over w: group k holds one wave per SIMD whether the
 // hardware deals a block's waves to SIMDs by w%4 or by w/4; lb is the
 // XCD-swizzled block). The schedule only changes which wave runs a tile,
-// never a photon's arithmetic. All threads of the block must call this.
+// never a photon's arithmetic. All threads of the block must call this; it
+// returns the wave's tile with its flag in bit 31, or 0xffffffff (idle).
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane) {
-  uint32_t x = v;
+
+// Exclusive wave prefix and wave total of per-lane counts in [0, 7] (a lane's
+// four flag bytes): one ballot + mbcnt per bit, no cross-lane shuffles.
+__device__ __forceinline__ uint32_t wave_scan_small(uint32_t c, uint32_t& total) {
+  uint32_t pre = 0u;
+  total = 0u;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= (uint32_t)o) x += y;
+  for (uint32_t b = 0; b < 3u; b++) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(((c >> b) & 1u) != 0u);
+    pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+    total += (uint32_t)__popcll(m) << b;
   }
-  return x - v;
+  return pre;
 }
 
 __device__ uint32_t schedule_tile(const MarchParams& P, const uint8_t* __restrict__ flags,
@@ -242,22 +248,27 @@ __device__ uint32_t schedule_tile(const MarchParams& P, const uint8_t* __restric
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
   const uint32_t n = P.n_tiles, G = gridDim.x;
   const uint32_t lb = xcd_swizzle(blockIdx.x, G);
-  const uint32_t* f4 = reinterpret_cast<const uint32_t*>(flags);
+  const uint32_t* f4 = reinterpret_cast<const uint32_t*>(flags);  // 0/1 bytes, padded to kSchedChunk
+  const uint32_t f0 = f4[tid];
   if (tid < 16u) s_tile[tid] = 0xffffffffu;  // idle unless a tile is dealt to it
-  if (tid < 17u) s_red[tid] = 0u;
-  __syncthreads();
-  uint32_t mine = 0u;  // number of volume tiles (flags are 0/1 bytes)
-  for (uint32_t base = 0; base < n; base += kSchedChunk) mine += __popc(f4[(base >> 2) + tid]);
-  mine = wave_sum(mine);
-  if (lane == 0u) atomicAdd(&s_red[16], mine);
-  __syncthreads();
-  const uint32_t nv = s_red[16];
+  uint32_t nv = 0u;  // number of volume tiles; one chunk (R <= 512): the scan's total
+  if (n > kSchedChunk) {
+    if (tid == 0u) s_red[16] = 0u;
+    __syncthreads();
+    uint32_t mine = 0u;
+    for (uint32_t base = 0; base < n; base += kSchedChunk)
+      mine += __popc(f4[(base >> 2) + tid] & 0x01010101u);
+    mine = wave_sum(mine);
+    if (lane == 0u) atomicAdd(&s_red[16], mine);
+    __syncthreads();
+    nv = s_red[16];
+  }
   uint32_t run = 0u;  // volume tiles before this chunk
   for (uint32_t base = 0; base < n; base += kSchedChunk) {
-    const uint32_t f = f4[(base >> 2) + tid];
-    const uint32_t c = __popc(f);
-    const uint32_t pre = wave_excl_scan(c, lane);
-    if (lane == 63u) s_red[w] = pre + c;
+    const uint32_t f = (base == 0u ? f0 : f4[(base >> 2) + tid]) & 0x01010101u;
+    uint32_t wt;
+    const uint32_t pre = wave_scan_small(__popc(f), wt);
+    if (lane == 0u) s_red[w] = wt;
     __syncthreads();
     uint32_t before = run, total = 0u;
     for (uint32_t k = 0; k < 16u; k++) {
@@ -265,6 +276,7 @@ __device__ uint32_t schedule_tile(const MarchParams& P, const uint8_t* __restric
       before += (k < w) ? t : 0u;
       total += t;
     }
+    if (n <= kSchedChunk) nv = total;
     uint32_t ones = before + pre;  // volume tiles before tile base + 4*tid
 #pragma unroll
     for (uint32_t q = 0; q < 4u; q++) {
@@ -275,7 +287,7 @@ __device__ uint32_t schedule_tile(const MarchParams& P, const uint8_t* __restric
         const uint32_t k = slot / (4u * G), rem = slot - k * 4u * G;
         if ((rem >> 2) == lb) {
           const uint32_t j = rem & 3u;
-          s_tile[4u * j + ((k + j) & 3u)] = t;
+          s_tile[4u * j + ((k + j) & 3u)] = t | (fl << 31);
         }
       }
       ones += fl;
@@ -284,6 +296,20 @@ __device__ uint32_t schedule_tile(const MarchParams& P, const uint8_t* __restric
     __syncthreads();  // s_red reused by the next chunk; s_tile complete after the last
   }
   return s_tile[w];
+}
+
+// Copies CHUNKS * kMarchBlock uint4 from global memory into LDS with
+// global_load_lds_dwordx4: each wave's instruction writes 64 consecutive
+// uint4 at a wave-uniform LDS base, lane l's from src[base + l]. The copy is
+// complete for the block after a vmcnt(0) wait in every wave and a barrier.
+template <uint32_t CHUNKS>
+__device__ __forceinline__ void stage_lds_16(uint4* dst, const uint4* __restrict__ src) {
+  const uint32_t wb = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+#pragma unroll
+  for (uint32_t k = 0; k < CHUNKS; k++)
+    __builtin_amdgcn_global_load_lds(
+        (__attribute__((address_space(1))) void*)(src + k * kMarchBlock + threadIdx.x),
+        (__attribute__((address_space(3))) void*)(dst + k * kMarchBlock + wb), 16, 0, 0);
 }
 
 // PassSeeds is k_march's first kernel argument: seed[pass] is read straight
@@ -348,13 +374,39 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __shared__ uint32_t s_red[17];
   __shared__ uint32_t s_tile[16];
 
+  TL_DECL();
+  TL_MARK(0);
+  // The TF's (albedo, alpha) planes go from L2 straight into LDS
+  // (global_load_lds_dwordx4: no VGPRs, no ds_write), issued before the tile
+  // schedule so that the 128 KiB copy runs under the schedule's flag read, and
+  // the small tables' loads with it.
+  stage_lds_16<256 * 256 * 2 / 16 / kMarchBlock>(s_tf4, reinterpret_cast<const uint4*>(tf_rg));
+  // (raw bytes here, converted at their LDS store: a conversion here would
+  // wait for the TF copy before the schedule starts)
+  const uint32_t t8 = threadIdx.x & 255u;
+  const uint32_t light_v = light[t8], brow_v = tf_brow[t8];
+  const uint32_t rowmap_v = (DEDUP || (!FAST && P.tf_dedup)) ? tf_rowmap[t8] : 0u;
+  uint32_t binlut_v[2] = {0u, 0u};
+  constexpr uint32_t kLutWords = kBinLutCells + kBinLutCells / 4;
+  static_assert(kLutWords <= 2u * kMarchBlock, "bin table: two words per thread");
+  if constexpr (LUTB) {
+#pragma unroll
+    for (uint32_t k = 0; k < 2u; k++)
+      if (threadIdx.x + k * kMarchBlock < kLutWords) binlut_v[k] = bin_lut[threadIdx.x + k * kMarchBlock];
+  }
+  TL_PROBE(5);
   uint32_t tile;
+  bool hot0;  // the tile entered the volume last launch (its wave is a long one)
   if (P.sched == 0u) {
-    tile = __builtin_amdgcn_readfirstlane(schedule_tile(P, T.flags_in, s_red, s_tile));
+    const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile(P, T.flags_in, s_red, s_tile));
+    tile = s == 0xffffffffu ? s : s & 0x7fffffffu;
+    hot0 = s != 0xffffffffu && (s >> 31) != 0u;
   } else {  // raster: the block's 16 consecutive tiles
     tile = xcd_swizzle(blockIdx.x, gridDim.x) * 16u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (tile >= P.n_tiles) tile = 0xffffffffu;
+    hot0 = true;
   }
+  TL_MARK(1);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
   const uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
@@ -366,10 +418,9 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   STAMP_BEGIN();
   Photon p;
   // Photon state: the waves whose tile entered the volume last launch (the
-  // long ones) issue their loads before the LDS TF fill, the background waves
-  // after it, so the hot waves' state is not queued behind theirs (~1 % per
-  // launch).
-  const bool hot0 = P.sched != 0u || (tile != 0xffffffffu && T.flags_in[tile] != 0u);
+  // long ones) issue their loads before the block's barrier, the background
+  // waves after it, so the hot waves' state is not queued behind theirs (~1 %
+  // per launch).
   if (live && hot0) load_photon(ph, S, i, p);
 #if VPT_NB_ZERO
   // Bins past nb (nb < 12) are never read or written by the reference
@@ -385,21 +436,19 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   }
 #endif
 
-  const uint4* src = reinterpret_cast<const uint4*>(tf_rg);
-#pragma unroll
-  for (uint32_t k = 0; k < 256 * 256 * 2 / 16 / kMarchBlock; k++)
-    s_tf4[threadIdx.x + k * kMarchBlock] = src[threadIdx.x + k * kMarchBlock];
   if (threadIdx.x < 256u) {
-    s_light[threadIdx.x] = (float)light[threadIdx.x];
-    s_brow[threadIdx.x] = (float)tf_brow[threadIdx.x];
-    if (DEDUP || (!FAST && P.tf_dedup)) s_rowmap[threadIdx.x] = (uint32_t)tf_rowmap[threadIdx.x] * 256u;
+    s_light[threadIdx.x] = (float)light_v;
+    s_brow[threadIdx.x] = (float)brow_v;
+    if (DEDUP || (!FAST && P.tf_dedup)) s_rowmap[threadIdx.x] = rowmap_v * 256u;
   }
   if constexpr (LUTB) {
-    for (uint32_t k = threadIdx.x; k < kBinLutCells + kBinLutCells / 4; k += kMarchBlock)
-      s_binlut[k] = bin_lut[k];
+#pragma unroll
+    for (uint32_t k = 0; k < 2u; k++)
+      if (threadIdx.x + k * kMarchBlock < kLutWords) s_binlut[threadIdx.x + k * kMarchBlock] = binlut_v[k];
   }
   __syncthreads();
   if (live && !hot0) load_photon(ph, S, i, p);
+  TL_MARK_WAIT(2);
   if (!live) {
     if (tile < P.n_tiles && lane == 0u) T.flags_out[tile] = 0u;  // an idle out-of-band tile
     return;
@@ -731,6 +780,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   }
   }
   }  // pass
+  TL_MARK(3);
 
   if (stale) p.pos = ray_start(from, p.dir);  // the last robust reset's start point
   store_state(ph, S, i, p);  // uPhotons[globalIndex] = p (wgsl:165), once per launch
@@ -740,6 +790,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 
   if (lane == 0u) T.flags_out[tile] = entered ? 1u : 0u;  // the next pass's schedule
   STAMP_END(rgb32, tile, entered);
+  TL_END(rgb32, tile, entered);
 }
 
 
@@ -811,8 +862,11 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
   __shared__ uint32_t s_tile[16];
   // the SIMD-balanced tile schedule and volume-wave priority of k_march
   uint32_t tile;
+  bool hot = true;
   if (P.sched == 0u) {
-    tile = __builtin_amdgcn_readfirstlane(schedule_tile(P, T.flags_in, s_red, s_tile));
+    const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile(P, T.flags_in, s_red, s_tile));
+    tile = s == 0xffffffffu ? s : s & 0x7fffffffu;
+    hot = s != 0xffffffffu && (s >> 31) != 0u;
   } else {
     tile = xcd_swizzle(blockIdx.x, gridDim.x) * (kMarchBlock / 64) +
            __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -851,7 +905,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
   const bool iso = __builtin_fabsf(g) < kEps;  // uniform
   const float tfw = (float)P.tf_w;
   const int tfm = (int)P.tf_w - 1;
-  bool hot = (P.sched == 0u) ? (T.flags_in[tile] != 0u) : true;
   bool entered = false;
   // robust-miss pixels, as in k_march: once reset with this launch's matrix
   // their rays miss the cube by a margin, so every later step is an exit

@@ -14,8 +14,58 @@
 #define VPT_STAMP 0
 #endif
 
-#if VPT_STAMP
-#define STAMP_BEGIN()                                                 \
+// VPT_STAMP == 2 (timeline build, tools/timeline_profile.py): per wave the
+// 100 MHz s_memrealtime at five points of the launch — [0] entry, [1] tile
+// scheduled, [2] LDS filled and photon state resident, [3] pass loop done,
+// [4] state, image and flag stores complete — plus the words 5 and 7 above.
+#if VPT_STAMP == 2
+#define TL_DECL() uint32_t tl[6] = {0u, 0u, 0u, 0u, 0u, 0u}
+#define TL_MARK(k) (tl[k] = (uint32_t)__builtin_amdgcn_s_memrealtime())
+#define TL_MARK_WAIT(k)                   \
+  do {                                    \
+    __builtin_amdgcn_s_waitcnt(0x0F70);   \
+    TL_MARK(k);                           \
+  } while (0)
+#define TL_END(out, tile, entered)                                                       \
+  do {                                                                                   \
+    TL_MARK_WAIT(4);                                                                     \
+    if (lane == 0u) {                                                                    \
+      uint32_t* _o = reinterpret_cast<uint32_t*>(out) + (size_t)(tile) * 8u;             \
+      for (int _k = 0; _k < 5; _k++) _o[_k] = tl[_k];                                    \
+      _o[5] = ((entered) ? 1u : 0u) | ((__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xffu) << 8); \
+      _o[6] = tl[5];                                                                     \
+      _o[7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);                                 \
+    }                                                                                    \
+  } while (0)
+// -DVPT_TL_PROBE=1: word 6 = the time the TF copy issued at entry has landed
+// (a vmcnt(0) wait right after it: serialises the copy and the schedule)
+#if VPT_TL_PROBE
+#define TL_PROBE(k) TL_MARK_WAIT(k)
+#else
+#define TL_PROBE(k) \
+  do {              \
+  } while (0)
+#endif
+#else
+#define TL_PROBE(k) \
+  do {              \
+  } while (0)
+#define TL_DECL() \
+  do {            \
+  } while (0)
+#define TL_MARK(k) \
+  do {             \
+  } while (0)
+#define TL_MARK_WAIT(k) \
+  do {                  \
+  } while (0)
+#define TL_END(out, tile, entered) \
+  do {                             \
+  } while (0)
+#endif
+
+#if VPT_STAMP == 1
+#define STAMP_BEGIN()                                             \
   uint32_t prof[5] = {0u, 0u, 0u, 0u, 0u};                            \
   uint32_t t_prev = (uint32_t)__builtin_amdgcn_s_memtime();           \
   const uint32_t t_launch = t_prev;                                   \
