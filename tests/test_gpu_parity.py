@@ -588,6 +588,42 @@ def test_camera_change_without_reset():
     gpu.close()
 
 
+def test_schedule_changes_every_launch(monkeypatch):
+    """A wave slot starts loading the photon state of the tile it ran last
+    launch before its schedule is known (TileSched::prev) and reloads when the
+    schedule moved it: one-pass launches that alternate between two cameras
+    (different volume tiles every launch, so most slots change tile), then a
+    band change on the same handle, equal the oracle pass by pass."""
+    monkeypatch.setenv("VPTMCM_MARCH_VARIANT", "4")  # one launch per pass
+    mvps = [cf.default_mvp_inverse(), cf.golden_mvp("near")]
+    gpu, cpu = make_pair(256, cf.fbm_volume(64, 21), cf.tf_spectral(), ext=16.0)
+    seeds = cf.seed_stream(12, start=31)
+    gpu.reset(mvps[0], seeds[0])
+    cpu.reset(mvps[0], seeds[0], nthreads=16)
+    for k, s in enumerate(seeds[1:9]):
+        gpu.render_passes(mvps[k & 1], [s])
+        _, want = cpu.render(mvps[k & 1], s, nthreads=16)
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "alternating schedule")
+    assert_rgba_equal(gpu.read_rgba16f(), want, "alternating schedule")
+    gpu.set_band(64, 192)
+    ref = vptmcm.Renderer(256, device=0)  # the same band on a fresh handle (no previous schedule)
+    ref.set_volume(cf.fbm_volume(64, 21))
+    ref.set_material_tf(cf.tf_spectral())
+    spd, ldir = cf.light_default()
+    ref.set_light(spd, ldir)
+    ref.set_spectrum(cf.spectrum_buffer("12"))
+    ref.set_params(extinction=16.0, bounces=8, steps=8)
+    ref.write_photons(gpu.read_photons())
+    ref.set_band(64, 192)
+    for s in seeds[9:]:
+        gpu.render_passes(mvps[0], [s])
+        ref.render_passes(mvps[0], [s])
+    assert np.array_equal(gpu.read_photons(), ref.read_photons())
+    assert np.array_equal(gpu.read_rgba16f()[64:192], ref.read_rgba16f()[64:192])
+    gpu.close()
+    ref.close()
+
+
 def test_tiny_resolutions_and_empty_volume():
     """R = 1, 2, 3 (one partial tile, pixel centres on the screen axes for odd R:
     the near point is then not hoisted) and an all-zero volume."""

@@ -31,6 +31,10 @@ constexpr uint32_t kTfRowsMax = 128;  // distinct TF rows the LDS holds as u32 t
 struct TileSched {
   const uint8_t* flags_in;
   uint8_t* flags_out;
+  // per wave slot (block * 16 + wave) the packed tile the schedule gave it last
+  // launch (tile | flag << 31, 0xffffffff idle): a hot wave starts loading that
+  // tile's photon state before its own schedule ends, and reloads on a change
+  uint32_t* prev;
 };
 constexpr uint32_t kSchedChunk = 4 * kMarchBlock;  // tiles scanned per block-wide round
 constexpr uint32_t kSchedMaxTiles = 16384;         // larger frames use the raster mapping
@@ -50,6 +54,9 @@ static_assert(offsetof(MarchParams, yb) == offsetof(MarchParams, xb) + 4 * kMaxB
               "cmf_table() reads xb, yb, zb contiguously");
 inline uint32_t sched_flag_bytes(uint32_t n_tiles) {
   return (n_tiles + kSchedChunk - 1) / kSchedChunk * kSchedChunk;
+}
+inline uint32_t sched_slot_words(uint32_t n_tiles) {  // TileSched::prev: 16 wave slots per block
+  return (n_tiles + 15u) / 16u * 16u;
 }
 
 hipError_t launch_reset(const MarchParams& P, float* ph, hipStream_t s);

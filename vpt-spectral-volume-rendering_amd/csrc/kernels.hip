@@ -243,13 +243,17 @@ __device__ __forceinline__ uint32_t wave_scan_small(uint32_t c, uint32_t& total)
   return pre;
 }
 
-__device__ uint32_t schedule_tile(const MarchParams& P, const uint8_t* __restrict__ flags,
+// f0 = the thread's first flag word (sched_flags_first), loaded by the caller
+// ahead of its other prologue loads.
+__device__ __forceinline__ uint32_t sched_flags_first(const uint8_t* __restrict__ flags) {
+  return reinterpret_cast<const uint32_t*>(flags)[threadIdx.x];
+}
+__device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8_t* __restrict__ flags,
                                   uint32_t* s_red, uint32_t* s_tile) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
   const uint32_t n = P.n_tiles, G = gridDim.x;
   const uint32_t lb = xcd_swizzle(blockIdx.x, G);
   const uint32_t* f4 = reinterpret_cast<const uint32_t*>(flags);  // 0/1 bytes, padded to kSchedChunk
-  const uint32_t f0 = f4[tid];
   if (tid < 16u) s_tile[tid] = 0xffffffffu;  // idle unless a tile is dealt to it
   uint32_t nv = 0u;  // number of volume tiles; one chunk (R <= 512): the scan's total
   if (n > kSchedChunk) {
@@ -376,11 +380,24 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 
   TL_DECL();
   TL_MARK(0);
-  // The TF's (albedo, alpha) planes go from L2 straight into LDS
-  // (global_load_lds_dwordx4: no VGPRs, no ds_write), issued before the tile
-  // schedule so that the 128 KiB copy runs under the schedule's flag read, and
-  // the small tables' loads with it.
+  const uint32_t lane = threadIdx.x & 63u;
+  const size_t S = P.npad;
+  // Prologue, in issue order: the schedule's flag word; the TF's (albedo,
+  // alpha) planes from L2 straight into LDS (global_load_lds_dwordx4: no
+  // VGPRs, no ds_write) and the small tables' loads; and, for a wave whose
+  // slot held a volume tile last launch, that tile's photon state — the
+  // schedule almost never changes between launches, so the hot waves' state
+  // is in flight while the schedule runs (reloaded below if it did change).
+  const uint32_t f0 = P.sched == 0u ? sched_flags_first(T.flags_in) : 0u;
   stage_lds_16<256 * 256 * 2 / 16 / kMarchBlock>(s_tf4, reinterpret_cast<const uint4*>(tf_rg));
+  Photon p;
+  uint32_t prev = 0xffffffffu;
+  if (P.sched == 0u) {  // a scalar load (lgkmcnt): its use does not wait for the TF copy
+    const auto pt = (const __attribute__((address_space(4))) uint32_t*)T.prev;
+    prev = pt[blockIdx.x * 16u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+    if (prev != 0xffffffffu && (prev >> 31) != 0u && (prev & 0x7fffffffu) < P.n_tiles)
+      load_photon(ph, S, (size_t)(prev & 0x7fffffffu) * 64u + lane, p);
+  }
   // (raw bytes here, converted at their LDS store: a conversion here would
   // wait for the TF copy before the schedule starts)
   const uint32_t t8 = threadIdx.x & 255u;
@@ -397,31 +414,31 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   TL_PROBE(5);
   uint32_t tile;
   bool hot0;  // the tile entered the volume last launch (its wave is a long one)
+  bool have = false;  // p already holds this tile's state (the slot's tile did not change)
   if (P.sched == 0u) {
-    const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile(P, T.flags_in, s_red, s_tile));
+    const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile(P, f0, T.flags_in, s_red, s_tile));
     tile = s == 0xffffffffu ? s : s & 0x7fffffffu;
     hot0 = s != 0xffffffffu && (s >> 31) != 0u;
+    have = hot0 && s == prev;
+    if (lane == 0u && s != prev) T.prev[blockIdx.x * 16u + (threadIdx.x >> 6)] = s;
   } else {  // raster: the block's 16 consecutive tiles
     tile = xcd_swizzle(blockIdx.x, gridDim.x) * 16u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (tile >= P.n_tiles) tile = 0xffffffffu;
     hot0 = true;
   }
   TL_MARK(1);
-  const uint32_t lane = threadIdx.x & 63u;
   const uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
   const uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
   const size_t i = (size_t)tile * 64u + lane;
   // tiles outside the band (whole tiles: band rows are multiples of 8) are idle
   const bool live = tile != 0xffffffffu && x < P.R && y < P.R && y >= P.band_y0 && y < P.band_y1;
-  const size_t S = P.npad;
   bool entered = false;  // wave-uniform: some lane of this wave was inside the volume
   STAMP_BEGIN();
-  Photon p;
   // Photon state: the waves whose tile entered the volume last launch (the
-  // long ones) issue their loads before the block's barrier, the background
-  // waves after it, so the hot waves' state is not queued behind theirs (~1 %
-  // per launch).
-  if (live && hot0) load_photon(ph, S, i, p);
+  // long ones) have theirs in flight or issue it now, before the block's
+  // barrier; the background waves after it, so the hot waves' state is not
+  // queued behind theirs (~1 % per launch).
+  if (live && hot0 && !have) load_photon(ph, S, i, p);
 #if VPT_NB_ZERO
   // Bins past nb (nb < 12) are never read or written by the reference
   // (wgsl:296, :310): their registers start at 0 and are left out of the final
@@ -864,7 +881,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
   uint32_t tile;
   bool hot = true;
   if (P.sched == 0u) {
-    const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile(P, T.flags_in, s_red, s_tile));
+    const uint32_t s = __builtin_amdgcn_readfirstlane(
+        schedule_tile(P, sched_flags_first(T.flags_in), T.flags_in, s_red, s_tile));
     tile = s == 0xffffffffu ? s : s & 0x7fffffffu;
     hot = s != 0xffffffffu && (s >> 31) != 0u;
   } else {

@@ -67,6 +67,7 @@ struct vptmcm {
   uint32_t tf_rgb_w = 0;
   float env[4] = {1.0f, 1.0f, 1.0f, 1.0f};  // RGB sibling: 1x1 white (WebGPURenderingContext.js:97-108)
   uint8_t* sched = nullptr;    // tile schedule flags: [2][sched_flag_bytes(n_tiles)]
+  uint32_t* sched_prev = nullptr;  // each wave slot's last scheduled tile (TileSched::prev)
   uint32_t sched_cur = 0;      // which flag row the next march reads
 
   float spectrum[VPTMCM_SPECTRUM_FLOATS] = {};
@@ -452,7 +453,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   if (h->timing && h->time_stop) ee = h->region.end;
   const uint8_t* vol = h->layout != kLayoutLinear ? (const uint8_t*)h->vol_c8 : h->vol_lin;
   const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
-  TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf};
+  TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev};
   P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : 0u;
   if (h->kind == VPTMCM_RENDERER_RGB)
     HIPCHK(h, launch_march_rgb(h->layout, P, PS, T, h->photons, vol, h->tf_rgb, h->rgba, h->rgb32,
@@ -683,6 +684,8 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   CK(hipMalloc(&h->tf_rgb, kRgbTfMax * sizeof(float4)));
   CK(hipMalloc(&h->sched, 2 * (size_t)sched_flag_bytes(h->n_tiles)));
   CK(hipMemsetAsync(h->sched, 0, 2 * (size_t)sched_flag_bytes(h->n_tiles), h->stream));
+  CK(hipMalloc(&h->sched_prev, sched_slot_words(h->n_tiles) * sizeof(uint32_t)));
+  CK(hipMemsetAsync(h->sched_prev, 0xff, sched_slot_words(h->n_tiles) * sizeof(uint32_t), h->stream));
   if (h->kind == VPTMCM_RENDERER_RGB) {  // WebGPUAbstractComputeRenderer.js:23-28
     static const uint8_t kDefaultTf[8] = {255, 0, 0, 0, 255, 0, 0, 255};
     if (vptmcm_set_transfer_function(h, kDefaultTf, 2, 1)) return fail(VPTMCM_EHIP);
@@ -724,6 +727,7 @@ void vptmcm_destroy(vptmcm* h) {
   if (h->bin_lut) (void)hipFree(h->bin_lut);
   if (h->light) (void)hipFree(h->light);
   if (h->sched) (void)hipFree(h->sched);
+  if (h->sched_prev) (void)hipFree(h->sched_prev);
   if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
