@@ -301,6 +301,16 @@ int vptmcm_debug_verify(vptmcm* h, int fn, uint32_t lo, uint64_t count, uint64_t
  * march launch since create. */
 int vptmcm_debug_last_launch(vptmcm* h, uint32_t info[4], uint64_t* launches);
 
+/* The tile schedule of the last spectral march launch (after launching any
+ * queued render() passes): per wave slot (block * 16 + wave of the march grid)
+ * the tile it ran, with bit 31 set when the tile entered the volume in the
+ * launch before (the schedule's volume class), 0xffffffff for an idle slot.
+ * *n_slots receives the slot count; out (may be NULL to query the count)
+ * must hold n_words >= *n_slots words. Only launches with the balanced
+ * schedule (R <= 1024, not the raster variant) write it; a fresh handle reports
+ * every slot idle. */
+int vptmcm_debug_schedule(vptmcm* h, uint32_t* out, uint32_t n_words, uint32_t* n_slots);
+
 /* Library version string. */
 const char* vptmcm_version(void);
 

@@ -624,6 +624,62 @@ def test_schedule_changes_every_launch(monkeypatch):
     ref.close()
 
 
+def _xcd_unswizzle(lb: int, G: int) -> int:
+    """Inverse of march.h xcd_swizzle: the hardware block of swizzled block lb."""
+    if G % 8:
+        return lb
+    x, r = divmod(lb, G // 8)
+    return r * 8 + x
+
+
+def _expected_schedule(table: np.ndarray, n_tiles: int) -> np.ndarray:
+    """schedule_tile's deal (kernels.hip), restated: tiles ordered [volume
+    tiles, background tiles], each class ascending; slot q = k*4G + lb*4 + j
+    goes to wave 4j + ((k + j) & 3) of block unswizzle(lb). The volume class is
+    taken from the table's own bit 31."""
+    G = table.size // 16
+    used = table != 0xFFFFFFFF
+    vol = np.zeros(n_tiles, bool)
+    vol[(table[used] & 0x7FFFFFFF)[(table[used] >> 31) == 1]] = True
+    order = np.concatenate([np.flatnonzero(vol), np.flatnonzero(~vol)])
+    exp = np.full(table.size, 0xFFFFFFFF, np.uint32)
+    for q, t in enumerate(order):
+        k, rem = divmod(q, 4 * G)
+        lb, j = divmod(rem, 4)
+        exp[_xcd_unswizzle(lb, G) * 16 + 4 * j + ((k + j) & 3)] = t | (int(vol[t]) << 31)
+    return exp
+
+
+@pytest.mark.parametrize("R", [256, 512])
+def test_tile_schedule_is_the_latin_square_deal(R):
+    """N2, checked directly: after each launch every tile ran on exactly one
+    wave slot, volume tiles first, dealt over the slots exactly as
+    schedule_tile's ballot / prefix scan intends (vptmcm_debug_schedule); a
+    camera change re-deals it."""
+    gpu = vptmcm.Renderer(R, device=0)
+    assert (gpu.debug_schedule() == 0xFFFFFFFF).all()  # fresh handle: no launch yet
+    gpu.set_volume(cf.fbm_volume(128, 77))
+    gpu.set_material_tf(cf.tf_spectral())
+    spd, ldir = cf.light_default()
+    gpu.set_light(spd, ldir)
+    gpu.set_spectrum(cf.spectrum_buffer("12"))
+    gpu.set_params(extinction=32.0, bounces=8, steps=8)
+    n_tiles = (R // 8) ** 2
+    seeds = cf.seed_stream(12, start=3)
+    gpu.reset(cf.default_mvp_inverse(), seeds[0])
+    vset = []
+    for k, mvp in enumerate([cf.default_mvp_inverse()] * 3 + [cf.golden_mvp("near")] * 2):
+        gpu.render_passes(mvp, seeds[1 + 2 * k:3 + 2 * k])
+        tab = gpu.debug_schedule()
+        used = tab[tab != 0xFFFFFFFF]
+        assert np.array_equal(np.sort(used & 0x7FFFFFFF), np.arange(n_tiles)), f"launch {k}: not a permutation"
+        assert np.array_equal(tab, _expected_schedule(tab, n_tiles)), f"launch {k}: deal differs"
+        vset.append(frozenset((used[(used >> 31) == 1] & 0x7FFFFFFF).tolist()))
+    assert not vset[0] and 0 < len(vset[1]) < n_tiles  # flags start clear, then a volume class
+    assert vset[4] != vset[2]  # the second camera's tiles, one launch after it took over
+    gpu.close()
+
+
 def test_tiny_resolutions_and_empty_volume():
     """R = 1, 2, 3 (one partial tile, pixel centres on the screen axes for odd R:
     the near point is then not hoisted) and an all-zero volume."""

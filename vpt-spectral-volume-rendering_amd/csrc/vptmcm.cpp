@@ -1410,6 +1410,21 @@ int vptmcm_debug_last_launch(vptmcm* h, uint32_t info[4], uint64_t* launches) {
   return VPTMCM_OK;
 }
 
+int vptmcm_debug_schedule(vptmcm* h, uint32_t* out, uint32_t n_words, uint32_t* n_slots) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
+  if (!n_slots) FAIL(h, VPTMCM_EINVAL, "debug_schedule: null slot count");
+  const uint32_t n = sched_slot_words(h->n_tiles);
+  *n_slots = n;
+  if (!out) return VPTMCM_OK;
+  if (n_words < n) FAIL(h, VPTMCM_EINVAL, "debug_schedule: output holds fewer words than slots");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipMemcpyAsync(out, h->sched_prev, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return VPTMCM_OK;
+}
+
 // --------------------------------------------------------------- diagnostics
 
 int vptmcm_debug_eval(vptmcm* h, int fn, const uint32_t* in, uint32_t* out, uint32_t n) {

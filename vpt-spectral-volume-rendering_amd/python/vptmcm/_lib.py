@@ -34,7 +34,7 @@ EXPORTS = [
     "vptmcm_enable_kernel_timing", "vptmcm_kernel_time", "vptmcm_comm_unique_id",
     "vptmcm_comm_init", "vptmcm_comm_allreduce_radiance", "vptmcm_comm_read_composite",
     "vptmcm_comm_barrier", "vptmcm_comm_allreduce_host", "vptmcm_debug_eval",
-    "vptmcm_debug_verify", "vptmcm_debug_last_launch", "vptmcm_version",
+    "vptmcm_debug_verify", "vptmcm_debug_last_launch", "vptmcm_debug_schedule", "vptmcm_version",
 ]
 
 
@@ -118,6 +118,7 @@ def load() -> C.CDLL:
         "vptmcm_debug_verify": (C.c_int, [vp, C.c_int, C.c_uint32, C.c_uint64,
                                           C.POINTER(C.c_uint64), u32p, C.c_uint32]),
         "vptmcm_debug_last_launch": (C.c_int, [vp, u32p, C.POINTER(C.c_uint64)]),
+        "vptmcm_debug_schedule": (C.c_int, [vp, u32p, C.c_uint32, u32p]),
         "vptmcm_version": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
@@ -384,6 +385,15 @@ class Renderer:
         self._ck(self.L.vptmcm_debug_last_launch(self.h, _u32p(info), C.byref(n)))
         return {"mode": int(info[0]), "tpl": int(info[1]), "spec": bool(info[2]),
                 "passes": int(info[3]), "launches": n.value}
+
+    def debug_schedule(self) -> np.ndarray:
+        """Per wave slot the packed tile of the last balanced-schedule march
+        launch (tile | volume << 31, 0xffffffff idle; vptmcm_debug_schedule)."""
+        n = np.zeros(1, np.uint32)
+        self._ck(self.L.vptmcm_debug_schedule(self.h, None, 0, _u32p(n)))
+        out = np.empty(int(n[0]), np.uint32)
+        self._ck(self.L.vptmcm_debug_schedule(self.h, _u32p(out), out.size, _u32p(n)))
+        return out
 
     def uniform_bins(self) -> bool:
         """True when the current spectrum takes the arithmetic bin search."""
