@@ -188,6 +188,22 @@ def js_api_line(vol, tf, spec, R, S, ext, passes, settle_ms):
                     "library fuses the queued passes into 32-pass launches"}
 
 
+def stdout_to_stderr(fn):
+    """Run fn with the process's stdout (fd 1) pointed at stderr: RCCL prints
+    a version banner on stdout when a process creates its first communicator,
+    and rank 0's stdout must carry the JSON line only."""
+    import ctypes
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        return fn()
+    finally:
+        ctypes.CDLL(None).fflush(None)  # C stdio buffers, before fd 1 is restored
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def main():
     a = parse()
     rank, world, local = rendezvous.env_world()
@@ -226,8 +242,8 @@ def main():
     multi = world > 1 or os.environ.get("VPTMCM_BENCH_FORCE_COMM") == "1"
     if multi:
         key = rendezvous.job_key()
-        uid = rendezvous.exchange_unique_id(rank, vptmcm.unique_id, key=key)
-        r.comm_init(uid, world, rank)
+        uid = stdout_to_stderr(lambda: rendezvous.exchange_unique_id(rank, vptmcm.unique_id, key=key))
+        stdout_to_stderr(lambda: r.comm_init(uid, world, rank))
         r.barrier()
         if rank == 0:
             rendezvous.cleanup(key)
@@ -534,4 +550,16 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except vptmcm.VptError as e:
+        if e.code != vptmcm.ECOMM:
+            raise
+        # a failed or abandoned RCCL communicator (a peer rank died or never
+        # joined): report and end the process at once — RCCL threads still
+        # blocked on the dead peer must not hold up interpreter shutdown
+        import traceback
+        traceback.print_exc()
+        sys.stderr.flush()
+        sys.stdout.flush()
+        os._exit(3)

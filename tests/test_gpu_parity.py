@@ -443,6 +443,7 @@ def test_comm_init_peer_never_joins():
     finally:
         del os.environ["VPTMCM_COMM_TIMEOUT_MS"]
     assert e.value.code == vptmcm.ECOMM and 2.5 < took < 60.0, (str(e.value), took)
+    print(f"comm_init failed after {took:.2f} s: {e.value}")
     with pytest.raises(vptmcm.VptError, match="no communicator"):
         gpu.barrier()
     mvp = cf.default_mvp_inverse()
@@ -632,11 +633,12 @@ def _xcd_unswizzle(lb: int, G: int) -> int:
     return r * 8 + x
 
 
-def _expected_schedule(table: np.ndarray, n_tiles: int) -> np.ndarray:
+def _expected_schedule(table: np.ndarray, n_tiles: int, xcd_by_xcd: bool = False) -> np.ndarray:
     """schedule_tile's deal (kernels.hip), restated: tiles ordered [volume
     tiles, background tiles], each class ascending; slot q = k*4G + lb*4 + j
-    goes to wave 4j + ((k + j) & 3) of block unswizzle(lb). The volume class is
-    taken from the table's own bit 31."""
+    goes to wave 4j + ((k + j) & 3) of hardware block lb (consecutive blocks
+    rotate over the XCDs), or of block unswizzle(lb) with round 2's XCD-by-XCD
+    order (variant bit 7). The volume class is taken from the table's own bit 31."""
     G = table.size // 16
     used = table != 0xFFFFFFFF
     vol = np.zeros(n_tiles, bool)
@@ -646,16 +648,19 @@ def _expected_schedule(table: np.ndarray, n_tiles: int) -> np.ndarray:
     for q, t in enumerate(order):
         k, rem = divmod(q, 4 * G)
         lb, j = divmod(rem, 4)
-        exp[_xcd_unswizzle(lb, G) * 16 + 4 * j + ((k + j) & 3)] = t | (int(vol[t]) << 31)
+        b = _xcd_unswizzle(lb, G) if xcd_by_xcd else lb
+        exp[b * 16 + 4 * j + ((k + j) & 3)] = t | (int(vol[t]) << 31)
     return exp
 
 
-@pytest.mark.parametrize("R", [256, 512])
-def test_tile_schedule_is_the_latin_square_deal(R):
+@pytest.mark.parametrize("R,variant", [(256, "0"), (512, "0"), (512, "128")])
+def test_tile_schedule_is_the_latin_square_deal(R, variant, monkeypatch):
     """N2, checked directly: after each launch every tile ran on exactly one
     wave slot, volume tiles first, dealt over the slots exactly as
-    schedule_tile's ballot / prefix scan intends (vptmcm_debug_schedule); a
-    camera change re-deals it."""
+    schedule_tile's ballot / prefix scan intends (vptmcm_debug_schedule), in
+    the XCD round-robin slot order and in round 2's XCD-by-XCD one (variant
+    bit 7); a camera change re-deals it."""
+    monkeypatch.setenv("VPTMCM_MARCH_VARIANT", variant)
     gpu = vptmcm.Renderer(R, device=0)
     assert (gpu.debug_schedule() == 0xFFFFFFFF).all()  # fresh handle: no launch yet
     gpu.set_volume(cf.fbm_volume(128, 77))
@@ -673,7 +678,8 @@ def test_tile_schedule_is_the_latin_square_deal(R):
         tab = gpu.debug_schedule()
         used = tab[tab != 0xFFFFFFFF]
         assert np.array_equal(np.sort(used & 0x7FFFFFFF), np.arange(n_tiles)), f"launch {k}: not a permutation"
-        assert np.array_equal(tab, _expected_schedule(tab, n_tiles)), f"launch {k}: deal differs"
+        assert np.array_equal(tab, _expected_schedule(tab, n_tiles, variant == "128")), \
+            f"launch {k}: deal differs"
         vset.append(frozenset((used[(used >> 31) == 1] & 0x7FFFFFFF).tolist()))
     assert not vset[0] and 0 < len(vset[1]) < n_tiles  # flags start clear, then a volume class
     assert vset[4] != vset[2]  # the second camera's tiles, one launch after it took over

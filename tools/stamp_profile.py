@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--bins", default="12")
     ap.add_argument("--fused", type=int, default=32,
                     help="passes of a final fused launch whose clock is reported")
+    ap.add_argument("--dump", default="", help="save the raw per-tile records (npz)")
     a = ap.parse_args()
     R, S = 512, 8
     layout = {"corner8": vptmcm.LAYOUT_CORNER8, "brick8": vptmcm.LAYOUT_BRICK8}[a.layout]
@@ -64,6 +65,8 @@ def main():
     r.synchronize()
     wf = r.read_rgb().reshape(-1).view(np.uint32)[: (R * R // 64) * 8].reshape(-1, 8).copy()
     r.close()
+    if a.dump:
+        np.savez_compressed(a.dump, fused=wf, **{f"one_pass_{k}": w for k, w in enumerate(acc)})
     live = wf[:, 6] > 0
     clk = wf[live, 4].astype(np.float64) / wf[live, 6] * 100.0  # MHz
     segs, walls, steps = [], [], []

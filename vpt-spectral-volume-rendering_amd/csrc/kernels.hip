@@ -220,7 +220,8 @@ __device__ __forceinline__ void add_radiance(const MarchParams& P, float* rad, f
 //   slot = k * 4G + lb * 4 + j,  wave w = 4j + ((k + j) & 3)
 // (a Latin square over w: group k holds one wave per SIMD whether the
 // hardware deals a block's waves to SIMDs by w%4 or by w/4; lb is the
-// XCD-swizzled block). The schedule only changes which wave runs a tile,
+// hardware block, so consecutive slots rotate over the XCDs). The schedule
+// only changes which wave runs a tile,
 // never a photon's arithmetic. All threads of the block must call this; it
 // returns the wave's tile with its flag in bit 31, or 0xffffffff (idle).
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
@@ -252,7 +253,12 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
                                   uint32_t* s_red, uint32_t* s_tile) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
   const uint32_t n = P.n_tiles, G = gridDim.x;
-  const uint32_t lb = xcd_swizzle(blockIdx.x, G);
+  // Consecutive slots go to consecutive hardware blocks, i.e. round-robin over
+  // the 8 XCDs, so the SIMDs that hold two volume waves are spread evenly over
+  // the XCDs (72 per XCD on the benchmark instead of 128 on each of XCDs 0-3):
+  // a fully paired XCD runs its pairs ~4 % slower.
+  // sched 2 keeps round 2's XCD-by-XCD order (the XCD-swizzled block).
+  const uint32_t lb = P.sched == 2u ? xcd_swizzle(blockIdx.x, G) : blockIdx.x;
   const uint32_t* f4 = reinterpret_cast<const uint32_t*>(flags);  // 0/1 bytes, padded to kSchedChunk
   if (tid < 16u) s_tile[tid] = 0xffffffffu;  // idle unless a tile is dealt to it
   uint32_t nv = 0u;  // number of volume tiles; one chunk (R <= 512): the scan's total
@@ -388,11 +394,11 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   // slot held a volume tile last launch, that tile's photon state — the
   // schedule almost never changes between launches, so the hot waves' state
   // is in flight while the schedule runs (reloaded below if it did change).
-  const uint32_t f0 = P.sched == 0u ? sched_flags_first(T.flags_in) : 0u;
+  const uint32_t f0 = P.sched != 1u ? sched_flags_first(T.flags_in) : 0u;
   stage_lds_16<256 * 256 * 2 / 16 / kMarchBlock>(s_tf4, reinterpret_cast<const uint4*>(tf_rg));
   Photon p;
   uint32_t prev = 0xffffffffu;
-  if (P.sched == 0u) {  // a scalar load (lgkmcnt): its use does not wait for the TF copy
+  if (P.sched != 1u) {  // a scalar load (lgkmcnt): its use does not wait for the TF copy
     const auto pt = (const __attribute__((address_space(4))) uint32_t*)T.prev;
     prev = pt[blockIdx.x * 16u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     if (prev != 0xffffffffu && (prev >> 31) != 0u && (prev & 0x7fffffffu) < P.n_tiles)
@@ -415,7 +421,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   uint32_t tile;
   bool hot0;  // the tile entered the volume last launch (its wave is a long one)
   bool have = false;  // p already holds this tile's state (the slot's tile did not change)
-  if (P.sched == 0u) {
+  if (P.sched != 1u) {
     const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile(P, f0, T.flags_in, s_red, s_tile));
     tile = s == 0xffffffffu ? s : s & 0x7fffffffu;
     hot0 = s != 0xffffffffu && (s >> 31) != 0u;
@@ -880,7 +886,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
   // the SIMD-balanced tile schedule and volume-wave priority of k_march
   uint32_t tile;
   bool hot = true;
-  if (P.sched == 0u) {
+  if (P.sched != 1u) {
     const uint32_t s = __builtin_amdgcn_readfirstlane(
         schedule_tile(P, sched_flags_first(T.flags_in), T.flags_in, s_red, s_tile));
     tile = s == 0xffffffffu ? s : s & 0x7fffffffu;

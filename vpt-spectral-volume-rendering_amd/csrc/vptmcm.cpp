@@ -9,11 +9,14 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <utility>
@@ -454,7 +457,8 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   const uint8_t* vol = h->layout != kLayoutLinear ? (const uint8_t*)h->vol_c8 : h->vol_lin;
   const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
   TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev};
-  P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : 0u;
+  // variant bit 1: raster mapping; bit 7: round 2's XCD-by-XCD slot order
+  P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : (h->variant & 128u) ? 2u : 0u;
   if (h->kind == VPTMCM_RENDERER_RGB)
     HIPCHK(h, launch_march_rgb(h->layout, P, PS, T, h->photons, vol, h->tf_rgb, h->rgba, h->rgb32,
                                h->stream, eb, ee, &h->last_launch));
@@ -483,14 +487,54 @@ int64_t now_ms() {
              std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+constexpr int64_t kAbortWaitMs = 2000;  // longest wait for ncclCommAbort (comm_abort_bounded)
+
+// VPTMCM_COMM_TRACE=1: timestamped lines on stderr at each stage of the
+// communicator's setup and failure handling (diagnostics of RCCL hangs).
+void comm_trace(const char* fmt, ...) {
+  static const bool on = [] {
+    const char* v = getenv("VPTMCM_COMM_TRACE");
+    return v && v[0] == '1';
+  }();
+  if (!on) return;
+  char b[256];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(b, sizeof b, fmt, ap);
+  va_end(ap);
+  fprintf(stderr, "[vptmcm comm %lld ms] %s\n", (long long)now_ms(), b);
+  fflush(stderr);
+}
+
 // Abort the communicator after an error or a timeout: RCCL kernels still
 // waiting for a peer observe the abort flag and exit, so the handle's streams
 // drain. Every later communicator call returns VPTMCM_ECOMM.
+// ncclCommAbort of a communicator whose initialisation still waits for a peer
+// in the bootstrap can block far past any timeout (seen on the GPU pool: more
+// than 120 s, in one of several runs of test_comm_init_peer_never_joins). The
+// abort runs on a detached helper thread; the caller waits for it at most
+// wait_ms and otherwise leaves it (the communicator is never used again, and
+// the helper ends with the process).
+bool comm_abort_bounded(ncclComm_t c, int64_t wait_ms) {
+  if (!c) return true;
+  auto done = std::make_shared<std::atomic<bool>>(false);
+  comm_trace("abort: start");
+  std::thread([c, done] {
+    (void)ncclCommAbort(c);
+    done->store(true, std::memory_order_release);
+    comm_trace("abort: returned");
+  }).detach();
+  const int64_t t0 = now_ms();
+  while (!done->load(std::memory_order_acquire) && now_ms() - t0 < wait_ms)
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  return done->load(std::memory_order_acquire);
+}
+
 int comm_fail(vptmcm* h, const char* what, const char* why) {
-  if (h->comm) (void)ncclCommAbort(h->comm);
+  const bool aborted = comm_abort_bounded(h->comm, kAbortWaitMs);
   h->comm = nullptr;
-  FAIL(h, VPTMCM_ECOMM, "%s: %s (communicator aborted; rank %d of %d)", what, why, h->rank,
-       h->nranks);
+  FAIL(h, VPTMCM_ECOMM, "%s: %s (communicator %s; rank %d of %d)", what, why,
+       aborted ? "aborted" : "abandoned: its abort had not returned after 2 s", h->rank, h->nranks);
 }
 
 // The communicator's asynchronous state: OK, 1 (still in progress) or the
@@ -508,9 +552,17 @@ int comm_state(vptmcm* h, const char* what) {
 // returned ncclInProgress) has completed.
 int comm_settle(vptmcm* h, const char* what) {
   const int64_t t0 = now_ms();
+  int64_t last = t0;
   for (uint32_t spin = 0;; spin++) {
     const int rc = comm_state(h, what);
-    if (rc <= 0) return rc;
+    if (rc <= 0) {
+      comm_trace("%s: settled rc=%d after %lld ms", what, rc, (long long)(now_ms() - t0));
+      return rc;
+    }
+    if (now_ms() - last >= 1000) {
+      last = now_ms();
+      comm_trace("%s: in progress after %lld ms", what, (long long)(last - t0));
+    }
     if (now_ms() - t0 > h->comm_timeout_ms) {
       char b[96];
       snprintf(b, sizeof b, "no progress after %lld ms (a peer rank died or hangs?)",
@@ -1241,7 +1293,10 @@ int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
 int vptmcm_comm_unique_id(uint8_t* out) {
   if (!out) return VPTMCM_EINVAL;
   ncclUniqueId id;
-  if (ncclGetUniqueId(&id) != ncclSuccess) {
+  comm_trace("unique_id: ncclGetUniqueId");
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  comm_trace("unique_id: returned %d", (int)r);
+  if (r != ncclSuccess) {
     g_create_error = "ncclGetUniqueId failed";
     return VPTMCM_ECOMM;
   }
@@ -1263,14 +1318,50 @@ int vptmcm_comm_init(vptmcm* h, const uint8_t* uid, int nranks, int rank) {
   }
   ncclUniqueId id;
   memcpy(&id, uid, sizeof id);
-  // non-blocking: a peer that never joins ends in VPTMCM_ECOMM after the timeout
+  // Bounded: a peer that never joins ends in VPTMCM_ECOMM after the timeout.
+  // The initialisation runs on a helper thread that the handle waits for at
+  // most comm_timeout_ms and otherwise abandons: a non-blocking config
+  // (blocking = 0, round 3's first version) still blocked inside
+  // ncclCommInitRankConfig for the first communicator of a process whose peer
+  // never joined (tools/comm_abort_repeat.py), and its asynchronous group job
+  // lives in the calling thread's thread-local storage, so the helper runs the
+  // blocking form (the whole initialisation inside the call, nothing left
+  // behind in its TLS when it exits). Collectives on the communicator are
+  // watched as before (comm_state / wait_stream: ncclCommGetAsyncError, bounded
+  // waits, ncclCommAbort).
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-  cfg.blocking = 0;
+  cfg.blocking = 1;
   h->nranks = nranks;
   h->rank = rank;
-  const ncclResult_t r = ncclCommInitRankConfig(&h->comm, nranks, id, rank, &cfg);
+  struct InitJob {
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = ncclInternalError;
+    std::atomic<bool> done{false};
+  };
+  auto job = std::make_shared<InitJob>();
+  comm_trace("comm_init: ncclCommInitRankConfig nranks=%d rank=%d", nranks, rank);
+  std::thread([job, nranks, id, rank, cfg, dev = h->device]() mutable {
+    (void)hipSetDevice(dev);  // RCCL binds the communicator to the calling thread's device
+    ncclComm_t c = nullptr;
+    const ncclResult_t res = ncclCommInitRankConfig(&c, nranks, id, rank, &cfg);
+    job->comm = c;
+    job->r = res;
+    job->done.store(true, std::memory_order_release);
+  }).detach();
+  const int64_t t0 = now_ms();
+  for (uint32_t spin = 0; !job->done.load(std::memory_order_acquire); spin++) {
+    if (now_ms() - t0 > h->comm_timeout_ms)
+      FAIL(h, VPTMCM_ECOMM,
+           "comm_init: ncclCommInitRankConfig had not returned after %lld ms (a peer rank never "
+           "joined?); the initialisation is abandoned (rank %d of %d)",
+           (long long)h->comm_timeout_ms, rank, nranks);
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  h->comm = job->comm;
+  const ncclResult_t r = job->r;
+  comm_trace("comm_init: ncclCommInitRankConfig returned %d", (int)r);
   if (r != ncclSuccess && r != ncclInProgress) {
-    if (h->comm) (void)ncclCommAbort(h->comm);
+    comm_abort_bounded(h->comm, kAbortWaitMs);
     h->comm = nullptr;
     FAIL(h, VPTMCM_ECOMM, "ncclCommInitRankConfig: %s", ncclGetErrorString(r));
   }
