@@ -9,7 +9,7 @@
 //   rocprofv3 --kernel-trace --pmc FETCH_SIZE
 // (FETCH_SIZE per gather = the counter's tally for one scattered 8-B load).
 //   hipcc -O3 --offload-arch=gfx950 tools/gather_calib.hip -o tools/gather_calib
-//   tools/gather_calib <table MiB> [gathers per lane] [blocks]
+//   tools/gather_calib <table MiB> [gathers per lane] [blocks] [load flavour 0-4]
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
@@ -30,7 +30,25 @@ __device__ __forceinline__ uint32_t pcg(uint32_t v) {
   return (w >> 22u) ^ w;
 }
 
+// One 8-B gather with the cache-policy bits of load flavour V: 0 plain, 1
+// nontemporal (nt), 2 sc1, 3 sc0 sc1, 4 nt sc1. The asm forms leave the wait
+// to the caller (vmcnt(0) after the round's 8 loads).
+template <int V>
+__device__ __forceinline__ uint2 gload(const uint2* p) {
+  if constexpr (V == 0) return *p;
+  if constexpr (V == 1) {
+    const uint64_t u = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
+    return make_uint2((uint32_t)u, (uint32_t)(u >> 32));
+  }
+  uint2 v;
+  if constexpr (V == 2) asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(v) : "v"(p));
+  if constexpr (V == 3) asm volatile("global_load_dwordx2 %0, %1, off sc0 sc1" : "=v"(v) : "v"(p));
+  if constexpr (V == 4) asm volatile("global_load_dwordx2 %0, %1, off nt sc1" : "=v"(v) : "v"(p));
+  return v;
+}
+
 // 8 gathers in flight per lane per round; `mask` = cells - 1 (power of two)
+template <int V>
 __global__ __launch_bounds__(256) void k_gather(const uint2* __restrict__ tab, uint32_t mask,
                                                 uint32_t rounds, uint32_t* __restrict__ out) {
   const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
@@ -40,13 +58,21 @@ __global__ __launch_bounds__(256) void k_gather(const uint2* __restrict__ tab, u
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       h = pcg(h);
-      v[k] = tab[h & mask];
+      v[k] = gload<V>(tab + (h & mask));
     }
+    if constexpr (V >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int k = 0; k < 8; k++) acc += v[k].x ^ v[k].y;
   }
   out[gid] = acc;
 }
+
+template <int V>
+void launch(uint32_t blocks, const uint2* tab, uint32_t mask, uint32_t rounds, uint32_t* out) {
+  k_gather<V><<<blocks, 256>>>(tab, mask, rounds, out);
+}
+using Launch = void (*)(uint32_t, const uint2*, uint32_t, uint32_t, uint32_t*);
+static const Launch kLaunch[5] = {launch<0>, launch<1>, launch<2>, launch<3>, launch<4>};
 
 __global__ void k_fill(uint2* tab, size_t n) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -57,6 +83,11 @@ int main(int argc, char** argv) {
   const size_t mib = argc > 1 ? strtoull(argv[1], 0, 10) : 1024;
   const uint32_t per_lane = argc > 2 ? (uint32_t)atoi(argv[2]) : 256;
   const uint32_t blocks = argc > 3 ? (uint32_t)atoi(argv[3]) : 4096;
+  const int flavour = argc > 4 ? atoi(argv[4]) : 0;  // gload<V>
+  if (flavour < 0 || flavour > 4) {
+    fprintf(stderr, "load flavour must be 0-4\n");
+    return 2;
+  }
   size_t cells = mib * 1024 * 1024 / 8;
   if (cells & (cells - 1)) {
     fprintf(stderr, "table size must be a power of two MiB\n");
@@ -76,19 +107,19 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  k_gather<<<blocks, 256>>>(tab, (uint32_t)(cells - 1), rounds, out);  // warm-up
+  kLaunch[flavour](blocks, tab, (uint32_t)(cells - 1), rounds, out);  // warm-up
   const int reps = 5;
   CK(hipEventRecord(a));
-  for (int r = 0; r < reps; r++) k_gather<<<blocks, 256>>>(tab, (uint32_t)(cells - 1), rounds, out);
+  for (int r = 0; r < reps; r++) kLaunch[flavour](blocks, tab, (uint32_t)(cells - 1), rounds, out);
   CK(hipEventRecord(b));
   CK(hipEventSynchronize(b));
   float ms;
   CK(hipEventElapsedTime(&ms, a, b));
   const double g = (double)blocks * 256 * rounds * 8;  // gathers per launch
   const double s = ms * 1e-3 / reps;
-  printf("{\"table_bytes\": %zu, \"gathers_per_launch\": %.0f, \"launch_us\": %.2f, "
+  printf("{\"flavour\": %d, \"table_bytes\": %zu, \"gathers_per_launch\": %.0f, \"launch_us\": %.2f, "
          "\"ggathers_per_s\": %.2f, \"tbps_if_64B\": %.2f, \"tbps_if_128B\": %.2f}\n",
-         cells * 8, g, s * 1e6, g / s * 1e-9, g * 64 / s * 1e-12, g * 128 / s * 1e-12);
+         flavour, cells * 8, g, s * 1e6, g / s * 1e-9, g * 64 / s * 1e-12, g * 128 / s * 1e-12);
   CK(hipFree(tab));
   CK(hipFree(out));
   return 0;
