@@ -30,21 +30,45 @@ __device__ __forceinline__ uint32_t pcg(uint32_t v) {
   return (w >> 22u) ^ w;
 }
 
-// One 8-B gather with the cache-policy bits of load flavour V: 0 plain, 1
-// nontemporal (nt), 2 sc1, 3 sc0 sc1, 4 nt sc1. The asm forms leave the wait
-// to the caller (vmcnt(0) after the round's 8 loads).
+// Eight 8-B gathers with the cache-policy bits of load flavour V: 0 plain, 1
+// nontemporal (nt), 2 sc1, 3 sc0 sc1, 4 nt sc1. The asm flavours issue all
+// eight loads and their vmcnt(0) in ONE asm statement with early-clobber
+// outputs: the results exist only after the wait, and no output register may
+// share a VGPR with an address still to be issued.
+#define VPT_G8(POL)                                                                      \
+  asm volatile("global_load_dwordx2 %0, %8, off " POL "\n"                              \
+               "global_load_dwordx2 %1, %9, off " POL "\n"                              \
+               "global_load_dwordx2 %2, %10, off " POL "\n"                             \
+               "global_load_dwordx2 %3, %11, off " POL "\n"                             \
+               "global_load_dwordx2 %4, %12, off " POL "\n"                             \
+               "global_load_dwordx2 %5, %13, off " POL "\n"                             \
+               "global_load_dwordx2 %6, %14, off " POL "\n"                             \
+               "global_load_dwordx2 %7, %15, off " POL "\n"                             \
+               "s_waitcnt vmcnt(0)"                                                      \
+               : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]),       \
+                 "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])                                  \
+               : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]),      \
+                 "v"(p[6]), "v"(p[7])                                                   \
+               : "memory")
+
 template <int V>
-__device__ __forceinline__ uint2 gload(const uint2* p) {
-  if constexpr (V == 0) return *p;
-  if constexpr (V == 1) {
-    const uint64_t u = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
-    return make_uint2((uint32_t)u, (uint32_t)(u >> 32));
+__device__ __forceinline__ void gload8(const uint2* const p[8], uint2 v[8]) {
+  if constexpr (V == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = *p[k];
+  } else if constexpr (V == 1) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint64_t u = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p[k]));
+      v[k] = make_uint2((uint32_t)u, (uint32_t)(u >> 32));
+    }
+  } else if constexpr (V == 2) {
+    VPT_G8("sc1");
+  } else if constexpr (V == 3) {
+    VPT_G8("sc0 sc1");
+  } else {
+    VPT_G8("nt sc1");
   }
-  uint2 v;
-  if constexpr (V == 2) asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(v) : "v"(p));
-  if constexpr (V == 3) asm volatile("global_load_dwordx2 %0, %1, off sc0 sc1" : "=v"(v) : "v"(p));
-  if constexpr (V == 4) asm volatile("global_load_dwordx2 %0, %1, off nt sc1" : "=v"(v) : "v"(p));
-  return v;
 }
 
 // 8 gathers in flight per lane per round; `mask` = cells - 1 (power of two)
@@ -54,13 +78,14 @@ __global__ __launch_bounds__(256) void k_gather(const uint2* __restrict__ tab, u
   const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
   uint32_t h = pcg(gid * 2654435761u + 12345u), acc = 0u;
   for (uint32_t r = 0; r < rounds; r++) {
-    uint2 v[8];
+    const uint2* p[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       h = pcg(h);
-      v[k] = gload<V>(tab + (h & mask));
+      p[k] = tab + (h & mask);
     }
-    if constexpr (V >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint2 v[8];
+    gload8<V>(p, v);
 #pragma unroll
     for (int k = 0; k < 8; k++) acc += v[k].x ^ v[k].y;
   }
