@@ -35,13 +35,7 @@ struct TileSched {
   // launch (tile | flag << 31, 0xffffffff idle): a hot wave starts loading that
   // tile's photon state before its own schedule ends, and reloads on a change
   uint32_t* prev;
-  // XCD-speed-aware deal (MarchParams::sched 3): per-XCD pair quotas and the
-  // per-XCD longest volume-wave time of the last launches (kXcdStateWords
-  // words, see xcd_quotas in kernels.hip), and this launch's sequence number
-  uint32_t* xcd;
-  uint32_t seq;
 };
-constexpr uint32_t kXcdStateWords = 40;
 constexpr uint32_t kSchedChunk = 4 * kMarchBlock;  // tiles scanned per block-wide round
 constexpr uint32_t kSchedMaxTiles = 16384;         // larger frames use the raster mapping
 // Seeds of the passes one march launch runs back to back (render_passes): the

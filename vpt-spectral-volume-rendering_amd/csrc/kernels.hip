@@ -244,86 +244,13 @@ __device__ __forceinline__ uint32_t wave_scan_small(uint32_t c, uint32_t& total)
   return pre;
 }
 
-// XCD-speed-aware deal (MarchParams::sched 3). The one slot group that holds
-// both volume and background tiles (the doubly loaded SIMDs at R = 512) is
-// dealt XCD-major with per-XCD quotas of volume slots instead of round-robin;
-// the quotas follow the XCDs' measured speed: every launch starts from the
-// previous launch's quotas (rescaled to this launch's count) and moves up to
-// two doubly loaded SIMDs from the XCD whose volume waves ended last to the one
-// whose ended first, when they differ by more than 1/128. TileSched::xcd words:
-//   [0, 16)   quotas q[2][8]: launch s reads q[s & 1], block 0 writes q[(s+1) & 1]
-//   [16, 40)  per-XCD longest volume-wave pass loop t[3][8] (s_memrealtime ticks):
-//             launch s reads t[s % 3], its volume waves atomicMax t[(s+1) % 3],
-//             block 0 zeroes t[(s+2) % 3]
-// Every block computes the same quotas from the same words, so the deal is a
-// bijection; only which wave runs a tile depends on timing, never the bits.
-__device__ __forceinline__ void xcd_quotas(const uint32_t* __restrict__ st, uint32_t seq, uint32_t V1,
-                                           uint32_t cap, uint32_t q[8]) {
-  // (every index below is a compile-time constant: q stays in registers)
-  const uint32_t* qp = st + (seq & 1u) * 8u;
-  const uint32_t* tp = st + 16u + (seq % 3u) * 8u;
-  uint32_t sum = 0u, t[8];
-#pragma unroll
-  for (int x = 0; x < 8; x++) {
-    q[x] = qp[x] < cap ? qp[x] : cap;
-    sum += q[x];
-    t[x] = tp[x];
-  }
-  // start over from equal quotas when the count moved by more than 16 (a new
-  // camera), else absorb the difference XCD by XCD (no division anywhere)
-  if (sum == 0u || sum + 16u < V1 || V1 + 16u < sum) {
-#pragma unroll
-    for (uint32_t x = 0; x < 8u; x++) q[x] = (V1 >> 3) + (x < (V1 & 7u) ? 1u : 0u);
-  } else if (sum > V1) {
-    uint32_t E = sum - V1;
-#pragma unroll
-    for (int x = 7; x >= 0; x--) {
-      const uint32_t r = E < q[x] ? E : q[x];
-      q[x] -= r;
-      E -= r;
-    }
-  } else {
-    uint32_t D = V1 - sum;  // one pass suffices: 8 * cap >= V1
-#pragma unroll
-    for (int x = 0; x < 8; x++) {
-      const uint32_t add = D < cap - q[x] ? D : cap - q[x];
-      q[x] += add;
-      D -= add;
-    }
-  }
-  // feedback: the slowest XCD with doubly loaded SIMDs gives up to two of them
-  // to the fastest XCD with room, when their longest volume waves differ by > 1/128
-  uint32_t ts = 0u, tf = 0xffffffffu;
-  int slow = -1, fast = -1;
-#pragma unroll
-  for (int x = 0; x < 8; x++) {
-    if (q[x] > 0u && t[x] > 0u && t[x] > ts) { ts = t[x]; slow = x; }
-    if (q[x] < cap && t[x] > 0u && t[x] < tf) { tf = t[x]; fast = x; }
-  }
-  if (slow >= 0 && fast >= 0 && slow != fast && ts > tf + tf / 128u) {
-    uint32_t qs = 0u, qf = 0u;
-#pragma unroll
-    for (int x = 0; x < 8; x++) {
-      qs = x == slow ? q[x] : qs;
-      qf = x == fast ? q[x] : qf;
-    }
-    uint32_t d = qs < 2u ? qs : 2u;
-    d = d < cap - qf ? d : cap - qf;
-#pragma unroll
-    for (int x = 0; x < 8; x++) {
-      if (x == slow) q[x] -= d;
-      if (x == fast) q[x] += d;
-    }
-  }
-}
-
 // f0 = the thread's first flag word (sched_flags_first), loaded by the caller
 // ahead of its other prologue loads.
 __device__ __forceinline__ uint32_t sched_flags_first(const uint8_t* __restrict__ flags) {
   return reinterpret_cast<const uint32_t*>(flags)[threadIdx.x];
 }
-__device__ uint32_t schedule_tile(const MarchParams& P, const TileSched& T, uint32_t f0,
-                                  const uint8_t* __restrict__ flags, uint32_t* s_red, uint32_t* s_tile) {
+__device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8_t* __restrict__ flags,
+                                  uint32_t* s_red, uint32_t* s_tile) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
   const uint32_t n = P.n_tiles, G = gridDim.x;
   // Consecutive slots go to consecutive hardware blocks, i.e. round-robin over
@@ -360,20 +287,6 @@ __device__ uint32_t schedule_tile(const MarchParams& P, const TileSched& T, uint
       total += t;
     }
     if (n <= kSchedChunk) nv = total;
-    // sched 3: the partial group's per-XCD quotas (identical in every block)
-    const bool xq = P.sched == 3u && (G & 7u) == 0u;
-    const uint32_t kp = nv / (4u * G), V1 = nv - kp * 4u * G, cap = G / 2u;
-    uint32_t quota[8];
-    if (xq) {
-      xcd_quotas(T.xcd, T.seq, V1, cap, quota);
-      if (blockIdx.x == 0u && tid < 8u && base == 0u) {
-        uint32_t mine = 0u;
-#pragma unroll
-        for (uint32_t x = 0; x < 8u; x++) mine = tid == x ? quota[x] : mine;
-        T.xcd[((T.seq + 1u) & 1u) * 8u + tid] = mine;
-        T.xcd[16u + ((T.seq + 2u) % 3u) * 8u + tid] = 0u;
-      }
-    }
     uint32_t ones = before + pre;  // volume tiles before tile base + 4*tid
 #pragma unroll
     for (uint32_t q = 0; q < 4u; q++) {
@@ -382,26 +295,10 @@ __device__ uint32_t schedule_tile(const MarchParams& P, const TileSched& T, uint
       if (t < n) {
         const uint32_t slot = fl ? ones : nv + (t - ones);
         const uint32_t k = slot / (4u * G), rem = slot - k * 4u * G;
-        uint32_t blk = rem >> 2, j = rem & 3u;
-        if (xq && k == kp) {  // XCD-major: volume slots by quota, then the background
-          const bool v = rem < V1;
-          const uint32_t p = v ? rem : rem - V1;
-          uint32_t acc = 0u, bx = 0u, bl = 0u;
-          bool found = false;
-#pragma unroll
-          for (uint32_t x = 0; x < 8u; x++) {
-            const uint32_t w = v ? quota[x] : cap - quota[x];  // this XCD's volume / background slots
-            if (!found && p < acc + w) {
-              bx = x;
-              bl = (v ? 0u : quota[x]) + (p - acc);
-              found = true;
-            }
-            acc += w;
-          }
-          blk = bx + 8u * (bl >> 2);
-          j = bl & 3u;
+        if ((rem >> 2) == lb) {
+          const uint32_t j = rem & 3u;
+          s_tile[4u * j + ((k + j) & 3u)] = t | (fl << 31);
         }
-        if (blk == lb) s_tile[4u * j + ((k + j) & 3u)] = t | (fl << 31);
       }
       ones += fl;
     }
@@ -525,7 +422,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   bool hot0;  // the tile entered the volume last launch (its wave is a long one)
   bool have = false;  // p already holds this tile's state (the slot's tile did not change)
   if (P.sched != 1u) {
-    const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile(P, T, f0, T.flags_in, s_red, s_tile));
+    const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile(P, f0, T.flags_in, s_red, s_tile));
     tile = s == 0xffffffffu ? s : s & 0x7fffffffu;
     hot0 = s != 0xffffffffu && (s >> 31) != 0u;
     have = hot0 && s == prev;
@@ -655,8 +552,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     rb = rbpix;
   };
   const uint32_t n_passes = PS.n;
-  // sched 3: the pass loop's duration of the volume waves, per (logical) XCD
-  const uint32_t t_loop0 = P.sched == 3u ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
   for (uint32_t pass = 0; pass < n_passes; pass++) {
 #if VPT_PRIO
   if (pass > 0u) hot = entered;
@@ -909,9 +804,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   }
   }  // pass
   TL_MARK(3);
-  if (P.sched == 3u && hot0 && lane == 0u)
-    atomicMax(&T.xcd[16u + ((T.seq + 1u) % 3u) * 8u + (blockIdx.x & 7u)],
-              (uint32_t)__builtin_amdgcn_s_memrealtime() - t_loop0);
 
   if (stale) p.pos = ray_start(from, p.dir);  // the last robust reset's start point
   store_state(ph, S, i, p);  // uPhotons[globalIndex] = p (wgsl:165), once per launch
@@ -996,7 +888,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
   bool hot = true;
   if (P.sched != 1u) {
     const uint32_t s = __builtin_amdgcn_readfirstlane(
-        schedule_tile(P, T, sched_flags_first(T.flags_in), T.flags_in, s_red, s_tile));
+        schedule_tile(P, sched_flags_first(T.flags_in), T.flags_in, s_red, s_tile));
     tile = s == 0xffffffffu ? s : s & 0x7fffffffu;
     hot = s != 0xffffffffu && (s >> 31) != 0u;
   } else {

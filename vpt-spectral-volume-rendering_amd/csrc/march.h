@@ -76,8 +76,7 @@ struct MarchParams {
   uint32_t light_iso;    // length(light_direction) < EPS
   uint32_t b_rows;       // TF blue channel column-invariant: use the LDS row table
   uint32_t sched;        // march tile mapping: 0 scheduled (TileSched flags, slots round-robin over
-                         // the XCDs), 1 raster, 2 scheduled XCD by XCD (round 2's order), 3 scheduled
-                         // with per-XCD pair quotas fed back from the XCDs' measured speed
+                         // the XCDs), 1 raster, 2 scheduled XCD by XCD (round 2's order)
   // Robust-miss screen region (NDC, host-derived from the forward matrix):
   // with blur 0, every ray of a pixel whose centre lies outside
   // [rb_x0, rb_x1] x [rb_y0, rb_y1] misses the unit cube by a margin, so each

@@ -71,7 +71,6 @@ struct vptmcm {
   float env[4] = {1.0f, 1.0f, 1.0f, 1.0f};  // RGB sibling: 1x1 white (WebGPURenderingContext.js:97-108)
   uint8_t* sched = nullptr;    // tile schedule flags: [2][sched_flag_bytes(n_tiles)]
   uint32_t* sched_prev = nullptr;  // each wave slot's last scheduled tile (TileSched::prev)
-  uint32_t* sched_xcd = nullptr;   // XCD-speed-aware deal state (TileSched::xcd)
   uint32_t sched_cur = 0;      // which flag row the next march reads
 
   float spectrum[VPTMCM_SPECTRUM_FLOATS] = {};
@@ -457,12 +456,9 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   if (h->timing && h->time_stop) ee = h->region.end;
   const uint8_t* vol = h->layout != kLayoutLinear ? (const uint8_t*)h->vol_c8 : h->vol_lin;
   const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
-  TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev, h->sched_xcd,
-              (uint32_t)h->march_launches};
-  // variant bit 1: raster mapping; bit 7: round 2's XCD-by-XCD slot order;
-  // bit 8: per-XCD pair quotas from the XCDs' measured speed
-  P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u
-            : (h->variant & 128u) ? 2u : (h->variant & 256u) ? 3u : 0u;
+  TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev};
+  // variant bit 1: raster mapping; bit 7: round 2's XCD-by-XCD slot order
+  P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : (h->variant & 128u) ? 2u : 0u;
   if (h->kind == VPTMCM_RENDERER_RGB)
     HIPCHK(h, launch_march_rgb(h->layout, P, PS, T, h->photons, vol, h->tf_rgb, h->rgba, h->rgb32,
                                h->stream, eb, ee, &h->last_launch));
@@ -740,8 +736,6 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   CK(hipMalloc(&h->tf_rgb, kRgbTfMax * sizeof(float4)));
   CK(hipMalloc(&h->sched, 2 * (size_t)sched_flag_bytes(h->n_tiles)));
   CK(hipMemsetAsync(h->sched, 0, 2 * (size_t)sched_flag_bytes(h->n_tiles), h->stream));
-  CK(hipMalloc(&h->sched_xcd, kXcdStateWords * sizeof(uint32_t)));
-  CK(hipMemsetAsync(h->sched_xcd, 0, kXcdStateWords * sizeof(uint32_t), h->stream));
   CK(hipMalloc(&h->sched_prev, sched_slot_words(h->n_tiles) * sizeof(uint32_t)));
   CK(hipMemsetAsync(h->sched_prev, 0xff, sched_slot_words(h->n_tiles) * sizeof(uint32_t), h->stream));
   if (h->kind == VPTMCM_RENDERER_RGB) {  // WebGPUAbstractComputeRenderer.js:23-28
@@ -786,7 +780,6 @@ void vptmcm_destroy(vptmcm* h) {
   if (h->light) (void)hipFree(h->light);
   if (h->sched) (void)hipFree(h->sched);
   if (h->sched_prev) (void)hipFree(h->sched_prev);
-  if (h->sched_xcd) (void)hipFree(h->sched_xcd);
   if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
