@@ -211,6 +211,11 @@ def main():
         if "WORLD_SIZE" in os.environ:
             raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
         world = 1
+    if rank != 0:
+        # only rank 0's stdout carries the JSON line: everything the other
+        # ranks' libraries print (RCCL's banner, warnings) goes to stderr
+        sys.stdout.flush()
+        os.dup2(2, 1)
     R, S = a.resolution, a.photon_steps
     layout = {"corner8": vptmcm.LAYOUT_CORNER8, "brick8": vptmcm.LAYOUT_BRICK8,
               "linear": vptmcm.LAYOUT_LINEAR}[a.layout]
