@@ -40,6 +40,7 @@ DRIVER = textwrap.dedent('''
         def set_params(self, **kw): pass
         def comm_init(self, uid, world, rank):
             LOG.append(["comm_init", bytes(uid).hex()[:16], world, rank])
+            os.write(1, ("RCCL version : (banner on fd 1, as RCCL writes it)" + chr(10)).encode())
             dist.init_process_group("gloo", rank=rank, world_size=world,
                                     timeout=__import__("datetime").timedelta(seconds=60))
         def barrier(self): dist.barrier()
@@ -98,6 +99,10 @@ def test_bench_two_ranks_driver_command_line(tmp_path, world):
         assert p.returncode == 0, o + e
     line = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
     assert len(line) == 1 and not [ln for o in outs[1:] for ln in o[0].splitlines() if ln.startswith("{")]
+    # stdout carries rank 0's JSON line and nothing else (RCCL's banner goes to stderr)
+    assert [ln for ln in outs[0][0].splitlines() if ln.strip()] == line
+    assert all(not o[0].strip() for o in outs[1:])
+    assert all("RCCL version" in o[1] for o in outs)
     rec = json.loads(line[0])
     assert rec["n_gpus"] == world and rec["steps"] == 20 and rec["warmup"] == 5
     assert rec["value"] > 0 and rec["config"]["workload"].startswith("C4")
