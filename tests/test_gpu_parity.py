@@ -653,7 +653,7 @@ def _expected_schedule(table: np.ndarray, n_tiles: int, xcd_by_xcd: bool = False
     return exp
 
 
-@pytest.mark.parametrize("R,variant", [(256, "0"), (512, "0"), (512, "128")])
+@pytest.mark.parametrize("R,variant", [(256, "0"), (512, "0"), (512, "128"), (1024, "0")])
 def test_tile_schedule_is_the_latin_square_deal(R, variant, monkeypatch):
     """N2, checked directly: after each launch every tile ran on exactly one
     wave slot, volume tiles first, dealt over the slots exactly as
@@ -720,6 +720,31 @@ def test_large_frame_rows_against_oracle():
         assert_photons_equal(got[y0:y1].reshape(-1, got.shape[-1]), exp[y0:y1].reshape(-1, exp.shape[-1]),
                              f"R=2048 rows {y0}:{y1}")
         assert_rgba_equal(gpu.read_rgba16f()[y0:y1], want[y0:y1], f"R=2048 rows {y0}:{y1}")
+    gpu.close()
+
+
+def test_multi_chunk_schedule_rows_against_oracle():
+    """R = 1024 (16384 tiles: the largest frame with the balanced schedule, whose
+    ballot / prefix scan runs in four 4096-tile chunks after a counting pass): a
+    band of rows through the cube, checked against the oracle after a one-pass
+    launch (flags all clear) and a fused launch dealt from the first one's flags."""
+    R = 1024
+    gpu, cpu = make_pair(R, cf.fbm_volume(128, 98), cf.tf_spectral(), ext=32.0)
+    mvp = cf.default_mvp_inverse()
+    seeds = cf.seed_stream(5, start=21)
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0], nthreads=16)
+    gpu.render_passes(mvp, seeds[1:2])
+    gpu.render_passes(mvp, seeds[2:])
+    rows = (480, 528)
+    for s in seeds[1:]:
+        _, want = cpu.render(mvp, s, nthreads=16, rows=rows)
+    got = gpu.read_photons().reshape(R, R, -1)[rows[0]:rows[1]]
+    exp = cpu.photons.reshape(R, R, -1)[rows[0]:rows[1]]
+    assert_photons_equal(got.reshape(-1, got.shape[-1]), exp.reshape(-1, exp.shape[-1]), "R=1024 rows")
+    assert_rgba_equal(gpu.read_rgba16f()[rows[0]:rows[1]], want[rows[0]:rows[1]], "R=1024 rows")
+    tab = gpu.debug_schedule()
+    assert int((tab[tab != 0xFFFFFFFF] >> 31).sum()) > 0  # the second launch had a volume class
     gpu.close()
 
 
