@@ -24,6 +24,12 @@
 __global__ void k_empty(uint32_t* p) {
   if (p && threadIdx.x == 1023u && blockIdx.x == 100000u) p[0] = 1u;
 }
+struct Big {  // a kernarg block the size of the march's (PassSeeds + MarchParams + pointers)
+  uint32_t w[240];
+};
+__global__ void k_empty_big(Big b, uint32_t* p) {
+  if (p && threadIdx.x == 1023u && blockIdx.x == 100000u) p[0] = b.w[7];
+}
 
 static double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -104,7 +110,8 @@ int main(int argc, char** argv) {
   // the HIP floor: enqueue of an empty 256 x 1024 launch
   hipStream_t s;
   if (hipStreamCreate(&s) != hipSuccess) return 1;
-  std::vector<double> plain, ext, ext_ev, ext_b, ext_e;
+  std::vector<double> plain, ext, ext_ev, ext_b, ext_e, big;
+  Big bg{};
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -129,16 +136,39 @@ int main(int argc, char** argv) {
     hipExtLaunchKernelGGL(k_empty, dim3(256), dim3(1024), 0, s, nullptr, e1, 0, nullptr);
     double t9 = now_us();
     (void)hipStreamSynchronize(s);
+    bg.w[7] = (uint32_t)k;
+    double t10 = now_us();
+    hipLaunchKernelGGL(k_empty_big, dim3(256), dim3(1024), 0, s, bg, nullptr);
+    double t11 = now_us();
+    (void)hipStreamSynchronize(s);
     if (k >= 50) {
       plain.push_back(t1 - t0);
       ext.push_back(t3 - t2);
       ext_ev.push_back(t5 - t4);
       ext_b.push_back(t7 - t6);
       ext_e.push_back(t9 - t8);
+      big.push_back(t11 - t10);
     }
   }
+  std::vector<double> setdev, lasterr, getdev;
+  for (int k = 0; k < 2000; k++) {
+    const double a = now_us();
+    (void)hipSetDevice(0);
+    const double b = now_us();
+    (void)hipGetLastError();
+    const double c = now_us();
+    int d = -1;
+    (void)hipGetDevice(&d);
+    const double e = now_us();
+    setdev.push_back(b - a);
+    lasterr.push_back(c - b);
+    getdev.push_back(e - c);
+  }
+  printf(", \"api_us\": {\"hipSetDevice\": %.3f, \"hipGetLastError\": %.3f, \"hipGetDevice\": %.3f}",
+         med(setdev), med(lasterr), med(getdev));
   printf(", \"empty_kernel_enqueue_us\": {\"hipLaunchKernelGGL\": %.2f, \"hipExtLaunchKernelGGL\": %.2f, "
-         "\"begin_and_end_events\": %.2f, \"begin_event\": %.2f, \"end_event\": %.2f}}\n",
-         med(plain), med(ext), med(ext_ev), med(ext_b), med(ext_e));
+         "\"begin_and_end_events\": %.2f, \"begin_event\": %.2f, \"end_event\": %.2f, "
+         "\"hipLaunchKernelGGL_960B_kernarg\": %.2f}}\n",
+         med(plain), med(ext), med(ext_ev), med(ext_b), med(ext_e), med(big));
   return hipStreamDestroy(s) == hipSuccess ? 0 : 1;
 }
