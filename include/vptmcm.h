@@ -242,13 +242,15 @@ int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches);
 /* ncclGetUniqueId on rank 0; the caller ships the 128 bytes to other ranks. */
 int vptmcm_comm_unique_id(uint8_t* out /* 128 */);
 
-/* Non-blocking ncclCommInitRankConfig on the handle's device. Every wait on
- * the communicator (this init, an RCCL enqueue in progress, synchronize and
- * the composite reads while RCCL work is queued) polls ncclCommGetAsyncError
- * and is bounded by VPTMCM_COMM_TIMEOUT_MS (environment, read here; default
- * 120000): on an asynchronous error or the timeout the communicator is
- * aborted (ncclCommAbort) and the call returns VPTMCM_ECOMM, so a dead or
- * hung peer ends every rank instead of hanging it. */
+/* ncclCommInitRankConfig on the handle's device, run on a helper thread that
+ * this call waits for at most VPTMCM_COMM_TIMEOUT_MS (environment, read here;
+ * default 120000; an initialisation still blocked then — a peer that never
+ * joined — is abandoned). Every later wait on the communicator (an RCCL
+ * enqueue in progress, synchronize and the composite reads while RCCL work is
+ * queued) polls ncclCommGetAsyncError under the same limit: on an
+ * asynchronous error or the timeout the communicator is aborted
+ * (ncclCommAbort, itself bounded to 2 s) and the call returns VPTMCM_ECOMM, so
+ * a dead or hung peer ends every rank instead of hanging it. */
 int vptmcm_comm_init(vptmcm* h, const uint8_t* unique_id, int nranks, int rank);
 
 /* Enqueue the cross-rank radiance composite of the current pass:
