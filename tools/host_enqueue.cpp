@@ -110,7 +110,7 @@ int main(int argc, char** argv) {
   // the HIP floor: enqueue of an empty 256 x 1024 launch
   hipStream_t s;
   if (hipStreamCreate(&s) != hipSuccess) return 1;
-  std::vector<double> plain, ext, ext_ev, ext_b, ext_e, big;
+  std::vector<double> plain, ext, ext_ev, ext_b, ext_e, big, marker_enq, marker_wall, stamp_wall;
   Big bg{};
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
@@ -136,6 +136,23 @@ int main(int argc, char** argv) {
     hipExtLaunchKernelGGL(k_empty, dim3(256), dim3(1024), 0, s, nullptr, e1, 0, nullptr);
     double t9 = now_us();
     (void)hipStreamSynchronize(s);
+    // an explicit begin marker + an end stamp from the dispatch, against the
+    // begin stamp from the dispatch (t5 - t4 / t7 - t6): enqueue and wall
+    const double m0 = now_us();
+    (void)hipEventRecord(e0, s);
+    hipExtLaunchKernelGGL(k_empty, dim3(256), dim3(1024), 0, s, nullptr, e1, 0, nullptr);
+    const double m1 = now_us();
+    (void)hipStreamSynchronize(s);
+    const double m2 = now_us();
+    hipExtLaunchKernelGGL(k_empty, dim3(256), dim3(1024), 0, s, e0, e1, 0, nullptr);
+    const double m3 = now_us();
+    (void)hipStreamSynchronize(s);
+    const double m4 = now_us();
+    if (k >= 50) {
+      marker_enq.push_back(m1 - m0);
+      marker_wall.push_back(m2 - m0);
+      stamp_wall.push_back(m4 - m2);
+    }
     bg.w[7] = (uint32_t)k;
     double t10 = now_us();
     hipLaunchKernelGGL(k_empty_big, dim3(256), dim3(1024), 0, s, bg, nullptr);
@@ -150,6 +167,8 @@ int main(int argc, char** argv) {
       big.push_back(t11 - t10);
     }
   }
+  printf(", \"region_begin\": {\"marker_then_launch_enqueue_us\": %.2f, \"marker_then_launch_wall_us\": %.2f, "
+         "\"dispatch_stamped_wall_us\": %.2f}", med(marker_enq), med(marker_wall), med(stamp_wall));
   std::vector<double> setdev, lasterr, getdev;
   for (int k = 0; k < 2000; k++) {
     const double a = now_us();

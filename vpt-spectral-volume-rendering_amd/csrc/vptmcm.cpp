@@ -88,6 +88,9 @@ struct vptmcm {
   // bracketed.
   bool timing = false;
   bool time_stop = true;  // the last launch stamps region.end itself (VPTMCM_TIME_STOP=0: a marker)
+  // VPTMCM_TIME_BEGIN=marker: region.beg is a marker recorded just before the
+  // region's first launch instead of a stamp from that launch's dispatch packet
+  bool time_begin_marker = false;
   bool region_closed = false;
   EventPair region;
   uint64_t launches = 0;
@@ -425,7 +428,10 @@ int time_slot(vptmcm* h, hipEvent_t* beg) {
     HIPCHK(h, hipEventCreateWithFlags(&h->region.beg, hipEventDisableSystemFence));
     HIPCHK(h, hipEventCreateWithFlags(&h->region.end, hipEventDisableSystemFence));
   }
-  if (h->launches++ == 0) *beg = h->region.beg;
+  if (h->launches++ == 0) {
+    if (h->time_begin_marker) HIPCHK(h, hipEventRecord(h->region.beg, h->stream));
+    else *beg = h->region.beg;
+  }
   h->region_closed = false;
   return VPTMCM_OK;
 }
@@ -693,6 +699,7 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
     (void)hipGetDevice(&h->device);
   }
   if (const char* v = getenv("VPTMCM_TIME_STOP")) h->time_stop = v[0] != '0';
+  if (const char* v = getenv("VPTMCM_TIME_BEGIN")) h->time_begin_marker = strcmp(v, "marker") == 0;
   if (const char* v = getenv("VPTMCM_SYNC_SPIN_US")) h->sync_spin_us = strtoll(v, nullptr, 10);
   h->layout = cfg->volume_layout;
   h->kind = cfg->renderer;
