@@ -17,6 +17,7 @@ Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -287,6 +288,10 @@ def main():
         return launches
 
     r.reset(mvp, seeds[0])
+    # no garbage-collector pause inside a timed region (a ~330 us driver region
+    # is short enough for one to show): collect now, then keep it off
+    gc.collect()
+    gc.disable()
     # clock settling: launches of F passes (seeds from a stream of their own)
     # until settle_ms of wall time have passed, then the W warm-up passes
     settle_passes, t_settle = 0, time.perf_counter()
