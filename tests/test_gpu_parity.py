@@ -169,6 +169,32 @@ def test_tf_modes_bitexact(variant, spec, tfname, monkeypatch):
     gpu.close()
 
 
+def test_bin_table_falls_back_for_close_boundaries():
+    """build_bin_lut (vptmcm.cpp) keeps the comparison search when two distinct
+    bin thresholds fall into one of its 1024 wavelength cells (~0.29 nm wide on
+    [400, 700]): boundaries 0.05 nm apart must run MODE 4 (no table), not 6, and
+    still match the oracle bit for bit; the same layout with the pair spread
+    apart takes the table (MODE 6)."""
+    base = cf.spectrum_buffer("8_uneven").copy()
+    nb = int(base[0] + 0.5)
+    assert nb == 8
+    for lams, want in [([400, 450, 500, 500.05, 550, 600, 640, 680, 700], 4),
+                       ([400, 450, 500, 510, 550, 600, 640, 680, 700], 6)]:
+        buf = base.copy()
+        buf[1:2 + nb] = np.float32(lams)
+        cells = ((np.float32(lams) - 400) / 300 * 1024).astype(int)
+        assert (cells[2] == cells[3]) == (want == 4)  # the close pair shares a cell
+        gpu, cpu = make_pair(64, cf.fbm_volume(64, 7, nthreads=8), cf.tf_materials(True), ext=24.0,
+                             upload_spectrum=False)
+        gpu.set_spectrum(buf)
+        cpu.set_spectrum(buf)
+        run_and_compare(gpu, cpu, cf.default_mvp_inverse(), cf.seed_stream(3, start=0),
+                        f"bins {lams}")
+        info = gpu.last_launch()
+        assert info["mode"] == want, (lams, info)
+        gpu.close()
+
+
 @pytest.mark.parametrize("camera", ["near", "orbit", "orbit_tilted"])
 def test_cameras_and_bins(camera):
     for spec in ("6", "3", "8_uneven", "12_wide"):
