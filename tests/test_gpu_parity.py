@@ -812,6 +812,45 @@ def test_c4_two_replica_composite_bitexact():
     assert np.isfinite(comp).all() and (n > 0).mean() > 0.99
 
 
+def test_c4_full_size_eight_replica_packs():
+    """C4 at its own size on one GPU: the C3 workload (512^3 fBm, spectral TF,
+    R = 512, S = 8, extinction 32) as the eight replicas of an 8-GPU job, i.e.
+    the rank seed streams seed_bits(k, 0..7), one after the other on one
+    renderer. Every replica's photons and its k_pack (rgb*n, n) buffer are
+    bit-exact against the oracle. The 8-term composite is exact per replica
+    only: RCCL's summation order is its own, so the f32 sum is held to the f64
+    sum within 8 ulp of the
+    summed magnitudes."""
+    R, passes, world = 512, 2, 8
+    vol, tf, mvp = cf.fbm_volume(512, 512, nthreads=8), cf.tf_spectral(), cf.default_mvp_inverse()
+    gpu, cpu = make_pair(R, vol, tf, ext=32.0)
+    packs = []
+    for rank in range(world):
+        seeds = cf.seed_stream(passes + 1, start=0, rank=rank)
+        gpu.reset(mvp, seeds[0])
+        cpu.reset(mvp, seeds[0], nthreads=16)
+        gpu.render_passes(mvp, seeds[1:])
+        for s in seeds[1:]:
+            rgb, _ = cpu.render(mvp, s, nthreads=16)
+        assert_photons_equal(gpu.read_photons(), cpu.photons, f"C4 replica {rank}")
+        got = gpu.pack_radiance()
+        assert np.array_equal(got.view(np.uint32), _oracle_pack(cpu, rgb).view(np.uint32)), \
+            f"C4 k_pack replica {rank}"
+        packs.append(got)
+    gpu.close()
+    assert len({p.tobytes() for p in packs}) == world, "rank seed streams must differ"
+    tot32 = np.zeros_like(packs[0])
+    for p in packs:
+        tot32 += p
+    tot64 = np.sum([p.astype(np.float64) for p in packs], axis=0)
+    mag = np.sum([np.abs(p.astype(np.float64)) for p in packs], axis=0)
+    assert (np.abs(tot32 - tot64) <= 8 * 2.0 ** -24 * mag).all()  # any summation order
+    n = tot32[..., 3]
+    assert (n == tot64[..., 3]).all()  # sample counts are small integers: exact in f32
+    comp = tot32[..., :3] / np.where(n > 0, n, 1)[..., None]
+    assert np.isfinite(comp).all() and (n > 0).mean() > 0.99
+
+
 @pytest.mark.parametrize("layout", [vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_BRICK8])
 def test_wide_gather_template_bitexact(layout, monkeypatch):
     """The 64-bit-offset CORNER8 / BRICK8 gathers (selected for cell arrays >= 4
