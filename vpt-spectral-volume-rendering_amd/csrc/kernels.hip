@@ -503,8 +503,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   const bool rbpix = P.robust != 0u && fixed &&
                      (sx < P.rb_x0 || sx > P.rb_x1 || sy < P.rb_y0 || sy > P.rb_y1);
   bool rb = false, stale = false;
-  // add_radiance of a termination is deferred into the next step's gather
-  // shadow (it only touches the radiance bins, applied in the same order),
+  // add_radiance of a termination is deferred to the start of the next step
+  // (it only touches the radiance bins, applied in the same order),
   // across pass boundaries too: only the launch's last pass applies it at its
   // end (for radiance_to_rgb and the state store).
   float pend_n = 0.0f, pend_l = 0.0f;
@@ -564,13 +564,17 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   if constexpr (SPEC) {
     for (uint32_t step = 0; step < P.steps; step++) {
       STAMP_RESTART();
+      // The previous step's deferred add_radiance, once, ahead of every path:
+      // one definition of the bins for the loop's back edge (per-path updates
+      // left 12 + 14 register copies in the volume and all-exit latches), and
+      // the scheduler places it (-1.7 % per fused pass).
+      apply_pending();
       if (__builtin_amdgcn_ballot_w64(!rb) == 0ull) {
         // Robust path: the exit of wgsl:142-150 and the reset, minus what a
         // certain exit does not need (the distance only moves the photon
         // further along a ray that misses the cube).
         uint32_t s1 = pcg_hash(st);
         uint32_t sw = pcg_hash(s1);
-        apply_pending();
         uint32_t h1 = pcg_hash(sw), h2 = pcg_hash(h1), h3 = pcg_hash(h2);
         uint32_t h4 = pcg_hash(h3), h5 = pcg_hash(h4);
         p.samples++;
@@ -608,7 +612,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         // Every lane of the wave leaves the volume this step (background tiles:
         // ~60% of wave-steps on the benchmark). The volume/TF samples, whose
         // values are unused on exit (wgsl:142), and the scatter half are skipped.
-        apply_pending();
         uint32_t h1 = pcg_hash(sw), h2 = pcg_hash(h1), h3 = pcg_hash(h2);
         uint32_t h4 = pcg_hash(h3), h5 = pcg_hash(h4);
         float dx = 0.0f, dy = 0.0f;
@@ -626,12 +629,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       entered = true;
       STAMP_AT(0);
       const VolTap vt = vol_fetch<L>(P, vol, p.pos);  // gather in flight from here
-      apply_pending();
-      // keep the update here, in the gather's shadow (the backend otherwise
-      // sinks it past the decision, after the wait)
-      asm volatile("" : "+v"(p.rad[0]), "+v"(p.rad[1]), "+v"(p.rad[2]), "+v"(p.rad[3]),
-                   "+v"(p.rad[4]), "+v"(p.rad[5]), "+v"(p.rad[6]), "+v"(p.rad[7]),
-                   "+v"(p.rad[8]), "+v"(p.rad[9]), "+v"(p.rad[10]), "+v"(p.rad[11]));
 
       // Speculative candidates, all derived from the state after the wheel
       // draw and independent of the gather: the reset (draws h1..h5) and the
