@@ -113,15 +113,14 @@ def cpu_baseline(vol, tf, spec, spd, ldir, mvp, R, S, ext, budget_s):
     import js_march  # test-infrastructure restatement, timed here as the CPU baseline
     import oracle as orc  # test-infrastructure checker, timed as the secondary baseline
 
-    # threads = the CPUs in this process's affinity mask, capped by
-    # OMP_NUM_THREADS when set; the machine may report many more CPUs
+    # threads = the CPUs in this process's affinity mask, capped by the cgroup's
+    # CPU quota and by OMP_NUM_THREADS when set; the machine may report many more
     threads = cf.host_threads()
-    try:
-        aff = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        aff = os.cpu_count()
-    share = (f"{threads} threads: affinity mask {aff} CPUs, OMP_NUM_THREADS="
-             f"{os.environ.get('OMP_NUM_THREADS', 'unset')}, os.cpu_count() {os.cpu_count()}")
+    hs = cf.host_cpu_share()
+    q = hs["cgroup_quota_cpus"]
+    share = (f"{threads} threads = min(affinity mask {hs['affinity']} CPUs, cgroup cpu quota "
+             f"{'unlimited' if q is None else f'{q:g} CPUs'}, OMP_NUM_THREADS="
+             f"{hs['omp_num_threads'] or 'unset'}); os.cpu_count() {hs['os_cpu_count']}")
     out = None
     if js_march.node():
         j = js_march.run_bench(R, vol, tf, spd, ldir, spec, mvp, cf.seed_stream(64, start=0),
@@ -248,11 +247,14 @@ def main():
     multi = world > 1 or os.environ.get("VPTMCM_BENCH_FORCE_COMM") == "1"
     if multi:
         key = rendezvous.job_key()
+        # every peer alive before any rank enters RCCL's bootstrap (bounded;
+        # a missing rank ends the job here with ECOMM)
+        rendezvous.join(rank, world, key=key)
         uid = stdout_to_stderr(lambda: rendezvous.exchange_unique_id(rank, vptmcm.unique_id, key=key))
         stdout_to_stderr(lambda: r.comm_init(uid, world, rank))
         r.barrier()
         if rank == 0:
-            rendezvous.cleanup(key)
+            rendezvous.cleanup(key, world)
 
     n_unfused = a.unfused_steps if not multi else 0
     n_api = a.api_steps if not multi else 0
@@ -559,17 +561,27 @@ def main():
     r.close()
 
 
-if __name__ == "__main__":
+def entry() -> None:
     try:
         main()
+    except rendezvous.RendezvousError:
+        # a peer never reached the rendezvous: no communicator exists, so the
+        # process ends normally with the communicator failure's exit code
+        import traceback
+        traceback.print_exc()
+        sys.exit(3)
     except vptmcm.VptError as e:
         if e.code != vptmcm.ECOMM:
             raise
-        # a failed or abandoned RCCL communicator (a peer rank died or never
-        # joined): report and end the process at once — RCCL threads still
-        # blocked on the dead peer must not hold up interpreter shutdown
+        # a failed RCCL communicator (a peer rank died mid-run): report and end
+        # the process at once — RCCL's own threads still blocked on the dead
+        # peer must not hold up interpreter shutdown
         import traceback
         traceback.print_exc()
         sys.stderr.flush()
         sys.stdout.flush()
         os._exit(3)
+
+
+if __name__ == "__main__":
+    entry()

@@ -59,15 +59,36 @@ extern "C" {
 #define VPTMCM_LAYOUT_CORNER8 1  /* one u64 of the 8 trilinear corners per cell */
 #define VPTMCM_LAYOUT_BRICK8 2   /* CORNER8 cells in 4x4x4-cell bricks (512 B), Z-ordered inside */
 
+/* Multi-device handles (one process driving several GPUs, SURVEY 8(b)
+ * "device list/mode"): how the replicas' radiance is composited. */
+#define VPTMCM_MAX_DEVICES 8
+#define VPTMCM_GROUP_PEER 0 /* ordered xGMI peer gather to devices[0] + k_composite (deterministic;
+                               a device may repeat: replicas then share a GPU)     */
+#define VPTMCM_GROUP_RCCL 1 /* ncclCommInitAll over the (distinct) devices, grouped ncclReduce to
+                               devices[0] + k_composite (RCCL's summation order)   */
+
 typedef struct vptmcm vptmcm;
 
 typedef struct vptmcm_config {
     uint32_t resolution;    /* R: render target is R x R, R*R photons;
                                options.resolution, WebGPUAbstractComputeRenderer.js:11 */
     uint32_t max_bins;      /* must be VPTMCM_MAX_BINS (12)                        */
-    int32_t device;         /* HIP device ordinal; -1 = current device             */
+    int32_t device;         /* HIP device ordinal; -1 = current device (n_devices == 0) */
     uint32_t volume_layout; /* VPTMCM_LAYOUT_*                                     */
     uint32_t renderer;      /* VPTMCM_RENDERER_* (0 = spectral, the default)       */
+    /* Device list (0 = the single device above). With n_devices = N >= 1 the
+     * handle holds N photon-parallel replicas, replica k on devices[k] with the
+     * seed stream of rank k (seed bits s -> s for k = 0, pcg(s ^ k*0x9E3779B9)
+     * otherwise; the same streams as N one-GPU processes). Every input goes to
+     * every replica; render/reset run on all of them; the render target
+     * (read_rgba16f, read_rgb, tonemap) is the composite sum(rgb*n)/sum(n) over
+     * the replicas, computed on devices[0] (N = 1: the replica's own image,
+     * bit for bit). read/write_photons and the diagnostics see replica 0. The
+     * reference's renderer owns one GPUDevice (WebGPUAbstractComputeRenderer.js:8-17):
+     * the device list is this build's addition for the north_star's N-GPU split. */
+    uint32_t n_devices;
+    int32_t devices[VPTMCM_MAX_DEVICES];
+    uint32_t group_transport; /* VPTMCM_GROUP_PEER (default) or VPTMCM_GROUP_RCCL */
 } vptmcm_config;
 
 /* Per-pass parameters (render UBO fields other than the matrix and seed;
@@ -260,8 +281,27 @@ int vptmcm_comm_init(vptmcm* h, const uint8_t* unique_id, int nranks, int rank);
 int vptmcm_comm_allreduce_radiance(vptmcm* h);
 
 /* Wait for the last all-reduce and return the composite rgb = sum(rgb*n)/sum(n)
- * (R*R*3 floats) and, if counts != NULL, the summed n per pixel. */
+ * (R*R*3 floats) and, if counts != NULL, the summed n per pixel. The division
+ * and the rgba16float conversion run on the device (k_composite). */
 int vptmcm_comm_read_composite(vptmcm* h, float* rgb, float* counts);
+
+/* The composite of a multi-replica frame, computed on the device (k_composite:
+ * sum(rgb*n)/sum(n) per pixel in f32 with a correctly rounded division, 0
+ * where sum(n) == 0; rgba16float with round-to-nearest-even, alpha 1):
+ *   - a communicator handle: over the last vptmcm_comm_allreduce_radiance;
+ *   - a device-list handle: over its replicas, for the current frame.
+ * Any output may be NULL: rgba16f R*R*4 halfs, rgb R*R*3 floats, counts R*R
+ * floats (sum(n)). Blocking. */
+int vptmcm_read_composite(vptmcm* h, uint16_t* rgba16f, float* rgb, float* counts);
+
+/* Device-list handle: enqueue the composite of the current frame on
+ * devices[0] (asynchronous; the progressive display calls it once per shown
+ * frame, the reads below then find it done). A no-op for one replica. */
+int vptmcm_composite(vptmcm* h);
+
+/* The replicas of a handle: *n receives N (1 for a single-device handle) and,
+ * if devices != NULL, devices[0..N) their HIP ordinals. */
+int vptmcm_group_devices(vptmcm* h, int32_t* devices, uint32_t* n);
 
 /* Mode B composite: sum over ranks of the fp32 radiance_to_rgb image (each
  * rank's rows outside its band are zero, so the sum IS the single-GPU image,

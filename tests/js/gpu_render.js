@@ -22,7 +22,7 @@ const V = require(path.join(ROOT, 'vpt-spectral-volume-rendering_amd', 'js'));
   const rgb = c.renderer === 'mcm-compute';
   const env = rgb && c.env ? { width: 1, height: 1, data: Uint8Array.from(c.env) } : null;
   const renderer = new (V.RendererFactory(c.renderer || 'mcm-spectral-compute'))(
-    V.createDevice(0, c.layout), null, new V.Camera(c.camera || {}), env,
+    V.createDevice(c.devices || 0, c.layout), null, new V.Camera(c.camera || {}), env,
     { resolution: c.R, cie, random });
   renderer.extinction = c.extinction;
   renderer.bounces = c.bounces;
@@ -81,6 +81,6 @@ const V = require(path.join(ROOT, 'vpt-spectral-volume-rendering_amd', 'js'));
     tm.destroy();
   }
   fs.writeFileSync(path.join(out, 'meta.json'), JSON.stringify({ seeds_used: k,
-    march_launches: marchLaunches, last_launch: launched }));
+    march_launches: marchLaunches, last_launch: launched, devices: renderer.devices ? renderer.devices() : null }));
   renderer.destroy();
 })().catch(e => { console.error(e.stack); process.exit(1); });

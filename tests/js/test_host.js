@@ -135,7 +135,7 @@ test('addon loads; renderer construction fails loudly without a GPU', () => {
     'setMaterialTF', 'setLight', 'setSpectrum', 'setParams', 'reset', 'render', 'renderPasses',
     'synchronize', 'readRGBA16F', 'readPhotons', 'writePhotons', 'enableKernelTiming', 'kernelTime',
     'commUniqueId', 'commInit', 'commAllreduceRadiance', 'commReadComposite', 'commBarrier', 'setBand', 'commGatherBands', 'version',
-    'tonemapArtistic', 'readRGB', 'lastLaunch']) {
+    'tonemapArtistic', 'readRGB', 'lastLaunch', 'composite', 'readComposite', 'groupDevices']) {
     assert.strictEqual(typeof A[f], 'function', f);
   }
   assert.ok(/gfx950/.test(A.version()));
@@ -145,6 +145,23 @@ test('addon loads; renderer construction fails loudly without a GPU', () => {
   assert.throws(() => new V.MCMSpectralComputeRenderer(V.createDevice(0), null, new V.Camera(), null,
     { resolution: 16, cie: gold('cie1931.json') }), e => e.vptmcmCode === -2 && /HIP device/.test(e.message));
   assert.throws(() => A.create(0, -1, 1), /resolution/);
+  // device lists: validated in the shim / the JS class before any device call
+  assert.throws(() => A.create(16, -1, 1, 0, []), /1 to VPTMCM_MAX_DEVICES/);
+  assert.throws(() => A.create(16, -1, 1, 0, [0, 1, 2, 3, 4, 5, 6, 7, 8]), /1 to VPTMCM_MAX_DEVICES/);
+  assert.throws(() => A.create(16, -1, 1, 0, ['x']), /integer ordinals/);
+  assert.throws(() => new V.MCMSpectralComputeRenderer(V.createDevice([0, 1], 'corner8', 'nccl'), null,
+    new V.Camera(), null, { resolution: 16, cie: gold('cie1931.json') }), /unknown transport/);
+  assert.throws(() => new V.MCMSpectralComputeRenderer({ devices: [] }, null, new V.Camera(), null,
+    { resolution: 16, cie: gold('cie1931.json') }), /1 to 8 device ordinals/);
+  // a valid list reaches the library, which fails loudly without a device
+  assert.throws(() => new V.MCMSpectralComputeRenderer(V.createDevice([0, 1]), null, new V.Camera(), null,
+    { resolution: 16, cie: gold('cie1931.json') }), e => e.vptmcmCode === -2 && /HIP device/.test(e.message));
+});
+
+test('createDevice: an ordinal or a device list', () => {
+  assert.deepStrictEqual(V.createDevice(3), { ordinal: 3, layout: 'corner8' });
+  assert.deepStrictEqual(V.createDevice([0, 1, 2], 'brick8'), { devices: [0, 1, 2], layout: 'brick8', transport: 'peer' });
+  assert.deepStrictEqual(V.createDevice([4, 5], 'corner8', 'rccl').transport, 'rccl');
 });
 
 test('tone mapper surface mirrors WebGPUArtisticToneMapper (properties, factory)', () => {

@@ -69,7 +69,7 @@ DRIVER = textwrap.dedent('''
 
     bench.vptmcm.Renderer = Fake
     bench.vptmcm.unique_id = lambda: os.urandom(128)
-    bench.main()
+    bench.entry()
     Path = __import__("pathlib").Path
     Path(os.environ["LOG_OUT"]).write_text(json.dumps(LOG))
 ''')
@@ -156,3 +156,26 @@ def test_bench_rank_death_ends_the_job(tmp_path):
     assert procs[0].returncode != 0, outs[0]
     assert not [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
     assert took < 200, took
+
+
+def test_bench_missing_rank_fails_in_the_rendezvous(tmp_path):
+    """World 2 where rank 1 never starts: rank 0 must fail in the all-ranks-present
+    rendezvous with ECOMM before any communicator call (no comm_init is made, so
+    no RCCL bootstrap is left waiting for the missing peer), within the bound."""
+    import time
+    port = _free_port()
+    argv = ["--gpus", "2", "--steps", "20", "--warmup", "5", "--volume", "16",
+            "--resolution", "16", "--cpu-seconds", "0"]
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="2",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BENCH_ARGV=json.dumps(argv),
+               BENCH_PATH=str(REPO / "bench.py"), LOG_OUT=str(tmp_path / "log0.json"),
+               TORCHELASTIC_RUN_ID=f"m{port}", VPTMCM_COMM_TIMEOUT_MS="1500")
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, "-c", DRIVER], env=env, capture_output=True, text=True,
+                       cwd=str(tmp_path), timeout=120)
+    took = time.monotonic() - t0
+    assert p.returncode == 3, p.stdout + p.stderr
+    assert "vptmcm error -5" in p.stderr and "never joined" in p.stderr and "[1]" in p.stderr
+    assert "RCCL version" not in p.stderr  # the fake comm_init (and its banner) never ran
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert took < 60, took

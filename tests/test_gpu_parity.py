@@ -918,3 +918,28 @@ def test_c5_1024_volume_streamed_rows_against_oracle():
     assert rad.min() >= 0 and rad[smp >= 1].max() <= 5 * 100 / 255 + 1e-6
     assert (rad[smp == 0] == 1.0).all()
     gpu.close()
+
+
+def test_c3_driver_shaped_launch_bitexact():
+    """The benchmarked launch shape itself: BASELINE C3
+    (512^3 fBm seed 512, spectral TF, R = 512, S = 8, 12 bins, extinction 32,
+    default camera) from a reset, the driver's 5 warm-up passes as one launch,
+    then its timed `--steps 20` region as ONE 20-pass fused launch (the FAST
+    MODE 2 kernel on CORNER8), with the bench's own seed stream: photons, the
+    fp32 image and the rgba16f image bit-exact against the oracle."""
+    R, S = 512, 8
+    vol, tf, mvp = cf.fbm_volume(512, 512, nthreads=8), cf.tf_spectral(), cf.default_mvp_inverse()
+    gpu, cpu = make_pair(R, vol, tf, ext=32.0, steps=S)
+    seeds = cf.seed_stream(1 + 5 + 20, start=0, rank=0)  # bench.py's stream at N = 1
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0], nthreads=16)
+    gpu.render_passes(mvp, seeds[1:6])
+    gpu.render_passes(mvp, seeds[6:26])
+    info = gpu.last_launch()
+    assert (info["passes"], info["mode"], info["tpl"], info["spec"]) == (20, 2, 1, True), info
+    for s in seeds[1:]:
+        rgb, want = cpu.render(mvp, s, nthreads=16)
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "C3 20-pass launch")
+    assert_rgb32_equal(gpu.read_rgb(), rgb, "C3 20-pass launch")
+    assert_rgba_equal(gpu.read_rgba16f(), want, "C3 20-pass launch")
+    gpu.close()

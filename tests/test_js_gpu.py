@@ -22,7 +22,8 @@ ROOT = Path(__file__).resolve().parents[1]
 
 
 def run_case(tmp_path, vol, tf, R=64, passes=3, ext=32.0, layout="corner8", stream=True,
-             change_event=False, tonemap=None, bvp=None, ui=None, band=None, render_passes=False):
+             change_event=False, tonemap=None, bvp=None, ui=None, band=None, render_passes=False,
+             devices=None):
     D, H, W = vol.shape
     (tmp_path / "vol.raw").write_bytes(np.ascontiguousarray(vol).tobytes())
     (tmp_path / "tf.bin").write_bytes(np.ascontiguousarray(tf).tobytes())
@@ -30,7 +31,7 @@ def run_case(tmp_path, vol, tf, R=64, passes=3, ext=32.0, layout="corner8", stre
     case = dict(R=R, passes=passes, extinction=ext, bounces=8, steps=8, layout=layout,
                 W=W, H=H, D=D, volume_path=str(tmp_path / "vol.raw"), tf_path=str(tmp_path / "tf.bin"),
                 seeds=seeds, stream_volume=stream, change_event=change_event, tonemap=tonemap,
-                bvp_path=None, ui=ui, band=band, render_passes=render_passes)
+                bvp_path=None, ui=ui, band=band, render_passes=render_passes, devices=devices)
     if bvp is not None:
         (tmp_path / "vol.bvp").write_bytes(bvp)
         case["bvp_path"] = str(tmp_path / "vol.bvp")
@@ -238,3 +239,34 @@ def test_napi_guards_and_extensions():
     assert out["ok_rgb"] is None
     assert out["spectral_launches"] == 2 and out["spectral_last"]["passes"] == 8, out
     assert out["rgb_launches"] == 2 and out["rgb_last"]["passes"] == 1, out
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+def test_js_device_list_renderer_composites(tmp_path):
+    """The JS drop-in driving a device list (createDevice([0, 0]): two replicas;
+    on an N-GPU node the list names N GPUs): render() per pass as the reference
+    loop calls it, getTexture() returns the composite sum(rgb*n)/sum(n) of the
+    replicas, bit-exact against two oracle replays (replica 1 on rank 1's seed
+    stream) composited in replica order; readPhotons() is replica 0's."""
+    from test_gpu_group import _composite
+    vol, tf = cf.sphere_in_cube(64), cf.tf_spectral()
+    ph, rgba, seeds, used = run_case(tmp_path, vol, tf, passes=5, devices=[0, 0])
+    assert run_case.meta["devices"] == [0, 0]
+    R = 64
+    bits = [int(np.float32(s).view(np.uint32)) for s in seeds]
+    reps = []
+    mvp = cf.default_mvp_inverse()
+    for k in (0, 1):  # the JS call sequence of oracle_replay, on replica k's seed bits
+        rs = [b if k == 0 else cf.pcg(b ^ ((k * 0x9E3779B9) & 0xFFFFFFFF)) for b in bits]
+        o = orc.Oracle(R)
+        o.volume, o.tf, o.light = vol, tf, np.full(256, 100, np.uint8)
+        o.params.update(extinction=32.0, bounces=8, steps=8)
+        o.reset(mvp, rs[0])
+        o.set_spectrum(cf.spectrum_buffer("12"))
+        for p in range(5):
+            rgb32, _ = o.render(mvp, rs[1 + p])
+        reps.append((o, rgb32))
+    assert same(ph[:, :34], reps[0][0].photons[:, :34])
+    want_rgb, want_rgba, _ = _composite(reps)
+    assert np.array_equal(rgba, want_rgba)
+    assert same(run_case.rgb32.view(np.uint32), want_rgb.view(np.uint32))

@@ -54,3 +54,48 @@ def test_stale_payload_of_another_attempt_is_ignored(monkeypatch):
         assert rendezvous.exchange_unique_id(1, None, key=key, timeout_s=5) == bytes(range(128))
     finally:
         rendezvous.cleanup(key)
+
+
+def _join_worker(rank, world, key, q):
+    rendezvous.join(rank, world, key=key, timeout_s=30)
+    q.put(rank)
+
+
+def test_join_all_ranks_present():
+    key = f"join-{os.getpid()}"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_join_worker, args=(r, 3, key, q)) for r in (2, 0, 1)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=60) for _ in procs)
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    assert got == [0, 1, 2]
+    rendezvous.cleanup(key, 3)
+    assert not any(rendezvous.join_path(key, r).exists() for r in range(3))
+
+
+def test_join_missing_rank_is_ecomm():
+    """Rank 1 never arrives: rank 0 fails in the rendezvous, bounded, with the
+    communicator error code, naming the missing rank."""
+    import time
+
+    import pytest
+    import vptmcm
+    key = f"join-missing-{os.getpid()}"
+    t0 = time.monotonic()
+    with pytest.raises(rendezvous.RendezvousError) as ei:
+        rendezvous.join(0, 2, key=key, timeout_s=0.5)
+    assert 0.5 <= time.monotonic() - t0 < 10
+    assert ei.value.code == vptmcm.ECOMM and isinstance(ei.value, vptmcm.VptError)
+    assert "[1]" in str(ei.value)
+    rendezvous.cleanup(key, 2)
+
+
+def test_join_timeout_from_environment(monkeypatch):
+    monkeypatch.setenv("VPTMCM_COMM_TIMEOUT_MS", "2500")
+    assert rendezvous.default_timeout_s() == 2.5
+    monkeypatch.setenv("VPTMCM_COMM_TIMEOUT_MS", "junk")
+    assert rendezvous.default_timeout_s() == 120.0

@@ -54,6 +54,11 @@ for s in $STEPS; do
   cost)  # floor of a one-pass launch (tools/launch_cost.hip)
     timeout -k 10 120 tools/launch_cost > $OUT/launch_cost.json 2>&1
     rc=$?; echo "cost rc=$rc" | tee -a $OUT/status.txt; cat $OUT/launch_cost.json; fault $rc && exit $rc ;;
+  commdiag)  # where RCCL blocks when a peer never joins: one run per mode (tools/comm_diag.cpp)
+    for m in ${DIAG_MODES:-nb nb2 blk}; do
+      NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,BOOTSTRAP timeout -k 10 90 tools/comm_diag $m > $OUT/comm_diag_$m.log 2>&1
+      rc=$?; echo "commdiag $m rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
+    done ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)

@@ -95,6 +95,16 @@ hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D
                           const uint32_t n[3] = nullptr);
 hipError_t launch_pack(const MarchParams& P, const float* ph, const float* rgb32, float4* out,
                        hipStream_t s);
+// Multi-replica composite (k_composite): the n source buffers of R^2 (rgb*n, n)
+// float4 summed in source order, / sum(n) -> fp32 rgb and rgba16float (either
+// output and counts may be null).
+constexpr uint32_t kMaxReplicas = 8;
+struct CompositeSrc {
+  const float4* p[kMaxReplicas];
+  uint32_t n;
+};
+hipError_t launch_composite(const CompositeSrc& S, uint32_t npx, float* rgb32, uint16_t* rgba,
+                            float* counts, hipStream_t s);
 // fn 13 checks bin_of's arithmetic path against the count on the spectrum in P
 hipError_t launch_verify(int fn, const MarchParams& P, uint32_t lo, uint32_t n,
                          unsigned long long* bad, uint32_t* first, uint32_t nfirst, hipStream_t s);

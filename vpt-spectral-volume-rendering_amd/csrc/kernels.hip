@@ -6,6 +6,7 @@
 //                 (wgsl:107-179); L = volume layout
 //   k_corner8     LINEAR u8 volume -> CORNER8 (one u64 of 8 corners per cell)
 //   k_pack        (rgb*n, n) float4 per pixel for the cross-rank all-reduce
+//   k_composite   sum over replicas of those, / sum(n), -> fp32 + rgba16float
 //   k_debug_eval  spec-math primitives, for device-vs-oracle parity tests
 #include "kernels.h"
 
@@ -308,6 +309,10 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
   return s_tile[w];
 }
 
+// s_waitcnt immediate (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8]
+// | vmcnt_hi[15:14]) for vmcnt(0) with expcnt and lgkmcnt left unconstrained.
+constexpr uint32_t kWaitVmcnt0 = 0x0F70u;
+
 // Copies CHUNKS * kMarchBlock uint4 from global memory into LDS with
 // global_load_lds_dwordx4: each wave's instruction writes 64 consecutive
 // uint4 at a wave-uniform LDS base, lane l's from src[base + l]. The copy is
@@ -440,6 +445,13 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   const bool live = tile != 0xffffffffu && x < P.R && y < P.R && y >= P.band_y0 && y < P.band_y1;
   bool entered = false;  // wave-uniform: some lane of this wave was inside the volume
   STAMP_BEGIN();
+  // The TF copy into LDS (global_load_lds, issued at entry) is complete for
+  // the block only after every wave has waited for its own share (LDS-DMA
+  // completion is tracked per wave by vmcnt) and then the barrier below: the
+  // barrier itself waits for nothing, so the wait is explicit, in every wave,
+  // before the hot waves issue their state loads (which stay in flight across
+  // the barrier). The slot's speculative state loads above are waited too.
+  __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
   // Photon state: the waves whose tile entered the volume last launch (the
   // long ones) have theirs in flight or issue it now, before the block's
   // barrier; the background waves after it, so the hot waves' state is not
@@ -1105,6 +1117,42 @@ __global__ __launch_bounds__(256) void k_pack(const MarchParams P, const float* 
   out[pix] = make_float4(c[0] * n, c[1] * n, c[2] * n, n);
 }
 
+// The composite of R^2 (rgb*n, n) float4 buffers (k_pack's, one per replica,
+// or one already summed by an RCCL all-reduce / reduce): per pixel the sum over
+// the sources in source order (f32 adds: deterministic for a fixed order), then
+// rgb = sum(rgb*n) / sum(n) with a correctly rounded division (0 where no
+// samples), stored as fp32 and as rgba16float (round-to-nearest-even, alpha 1).
+__global__ __launch_bounds__(256) void k_composite(const CompositeSrc S, uint32_t npx,
+                                                   float* __restrict__ rgb32,
+                                                   uint16_t* __restrict__ rgba,
+                                                   float* __restrict__ counts) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= npx) return;
+  float4 s = S.p[0][i];
+  for (uint32_t k = 1; k < S.n; k++) {
+    const float4 t = S.p[k][i];
+    s.x += t.x;
+    s.y += t.y;
+    s.z += t.z;
+    s.w += t.w;
+  }
+  const float n = s.w;
+  const bool any = n > 0.0f;
+  const float r = any ? s.x / n : 0.0f, g = any ? s.y / n : 0.0f, b = any ? s.z / n : 0.0f;
+  if (rgb32) {
+    rgb32[3u * i] = r;
+    rgb32[3u * i + 1u] = g;
+    rgb32[3u * i + 2u] = b;
+  }
+  if (rgba) {
+    uint2 px;
+    px.x = (uint32_t)f2h(r) | ((uint32_t)f2h(g) << 16);
+    px.y = (uint32_t)f2h(b) | (0x3c00u << 16);
+    reinterpret_cast<uint2*>(rgba)[i] = px;
+  }
+  if (counts) counts[i] = n;
+}
+
 // ------------------------------------------------------------ tone mapping
 // The artistic tone mapper (ArtisticToneMapper.wgsl:38-48, run by
 // WebGPUArtisticToneMapper._renderFrame, js:77-122) on the rgba16float render
@@ -1295,6 +1343,14 @@ hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D
 hipError_t launch_pack(const MarchParams& P, const float* ph, const float* rgb32, float4* out,
                        hipStream_t s) {
   hipLaunchKernelGGL(k_pack, dim3(march_blocks(P)), dim3(kBlock), 0, s, P, ph, rgb32, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_composite(const CompositeSrc& S, uint32_t npx, float* rgb32, uint16_t* rgba,
+                            float* counts, hipStream_t s) {
+  if (npx == 0) return hipSuccess;
+  if (S.n < 1 || S.n > kMaxReplicas) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_composite, dim3((npx + 255u) / 256u), dim3(256), 0, s, S, npx, rgb32, rgba, counts);
   return hipGetLastError();
 }
 

@@ -124,7 +124,27 @@ struct vptmcm {
   uint32_t pend_seeds[kMaxFusedPasses];
   float pend_mvp[16];
   double* host_scratch = nullptr;
-  float4* comp_host = nullptr;  // pinned host copy of a composite (vptmcm_comm_read_composite)
+  // Mode A composite target: k_composite over comp[comp_last] (vptmcm_read_composite)
+  float* comp_rgb32 = nullptr;
+  uint16_t* comp_rgba = nullptr;
+  float* comp_counts = nullptr;
+
+  // Multi-device handle (vptmcm_config::n_devices): replica 0 is this handle,
+  // replicas 1..N-1 are full single-device handles of their own; every input
+  // and every pass is forwarded to them (their seed stream: replica_seed), and
+  // the render target is the composite of all replicas, made on this device.
+  std::vector<vptmcm*> peers;
+  uint32_t replica = 0;            // the replica index (seed stream) of this handle
+  bool grouped = false;            // created from a device list (even of one device)
+  uint32_t group_transport = VPTMCM_GROUP_PEER;
+  bool grp_dirty = true;           // a march / reset since the last composite
+  float4* grp_pack = nullptr;      // this replica's (rgb*n, n), on its device
+  float4* grp_gather = nullptr;    // replica 0: the peers' packs (PEER) / the reduced sum (RCCL)
+  float* grp_rgb32 = nullptr;      // replica 0: the composite, fp32
+  uint16_t* grp_rgba = nullptr;    // replica 0: the composite, rgba16float
+  hipEvent_t grp_packed = nullptr; // this replica's pack is complete
+  hipEvent_t grp_done = nullptr;   // replica 0: the last composite has read every pack
+  std::vector<ncclComm_t> grp_comms;  // RCCL transport: one communicator per replica (InitAll)
 
   std::string err;
 };
@@ -474,6 +494,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
                            h->tf_rowmap, h->bin_lut, &h->last_launch));
   h->march_launches++;
   h->sched_cur = c ^ 1u;
+  h->grp_dirty = true;
   return VPTMCM_OK;
 }
 
@@ -628,6 +649,43 @@ int wait_stream(vptmcm* h, hipStream_t s, const char* what) {
   }
 }
 
+// PCG-RXS-M-XS (pcg.wgsl:3-7) on the host, for the replicas' seed streams.
+uint32_t pcg_host(uint32_t v) {
+  uint32_t x = v * 747796405u + 2891336453u;
+  x = ((x >> ((x >> 28u) + 4u)) ^ x) * 277803737u;
+  return (x >> 22u) ^ x;
+}
+
+// Seed bits of replica k for the pass whose replica-0 seed bits are s: the
+// seed stream of rank k of the one-process-per-GPU path (bench.py,
+// configs.seed_bits), so N replicas in one process and N processes render the
+// same photons.
+uint32_t replica_seed(uint32_t s, uint32_t k) { return k ? pcg_host(s ^ (k * 0x9E3779B9u)) : s; }
+
+// Run the same single-replica operation on every peer replica of a
+// device-list handle; a peer's failure is reported on h, naming the replica.
+template <class F>
+int for_peers(vptmcm* h, F&& f) {
+  for (vptmcm* c : h->peers) {
+    const int rc = f(c);
+    if (rc != VPTMCM_OK) {
+      h->err = "replica " + std::to_string(c->replica) + " (device " + std::to_string(c->device) +
+               "): " + c->err;
+      return rc;
+    }
+  }
+  return VPTMCM_OK;
+}
+
+// Replica 0 (h) and its peers, in replica order.
+template <class F>
+int for_replicas(vptmcm* h, F&& f) {
+  if (int rc = f(h)) return rc;
+  return for_peers(h, f);
+}
+
+bool composited(const vptmcm* h) { return !h->peers.empty(); }
+
 void free_volume(vptmcm* h) {
   if (h->vol_lin) (void)hipFree(h->vol_lin);
   if (h->vol_c8) (void)hipFree(h->vol_c8);
@@ -646,6 +704,168 @@ const char* vptmcm_version(void) { return "vptmcm 0.1.0 (gfx950)"; }
 
 const char* vptmcm_last_error(const vptmcm* h) {
   return h ? h->err.c_str() : g_create_error.c_str();
+}
+
+// ---- device-list handles (vptmcm_config::n_devices)
+
+// The composite's buffers and events: a pack buffer per replica on its device;
+// on devices[0] the peers' packs (PEER) or the reduced sum (RCCL) and the
+// composite image. PEER enables xGMI peer access from devices[0] to each other
+// device (copies then run device to device over the link); RCCL builds one
+// communicator per replica with ncclCommInitAll (one process: no bootstrap
+// peers that could fail to arrive).
+static int group_alloc(vptmcm* h, const int32_t* devs, uint32_t n) {
+  const size_t npx = (size_t)h->R * h->R;
+  int rc = for_replicas(h, [&](vptmcm* c) {
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMalloc(&c->grp_pack, npx * sizeof(float4)));
+    HIPCHK(c, hipEventCreateWithFlags(&c->grp_packed, hipEventDisableTiming));
+    return VPTMCM_OK;
+  });
+  if (rc) return rc;
+  HIPCHK(h, hipSetDevice(h->device));
+  const size_t slots = h->group_transport == VPTMCM_GROUP_RCCL ? 1 : n - 1;
+  if (slots) HIPCHK(h, hipMalloc(&h->grp_gather, slots * npx * sizeof(float4)));
+  HIPCHK(h, hipMalloc(&h->grp_rgb32, npx * 3 * sizeof(float)));
+  HIPCHK(h, hipMemsetAsync(h->grp_rgb32, 0, npx * 3 * sizeof(float), h->stream));
+  HIPCHK(h, hipMalloc(&h->grp_rgba, npx * 4 * sizeof(uint16_t)));
+  HIPCHK(h, hipMemsetAsync(h->grp_rgba, 0, npx * 4 * sizeof(uint16_t), h->stream));
+  HIPCHK(h, hipEventCreateWithFlags(&h->grp_done, hipEventDisableTiming));
+  HIPCHK(h, hipEventRecord(h->grp_done, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (h->group_transport == VPTMCM_GROUP_PEER) {
+    for (uint32_t k = 1; k < n; k++) {
+      if (devs[k] == h->device) continue;
+      int can = 0;
+      HIPCHK(h, hipDeviceCanAccessPeer(&can, h->device, devs[k]));
+      if (!can) continue;  // hipMemcpyPeerAsync then stages through the host
+      const hipError_t e = hipDeviceEnablePeerAccess(devs[k], 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+        FAIL(h, VPTMCM_EHIP, "hipDeviceEnablePeerAccess(%d -> %d): %s", h->device, devs[k],
+             hipGetErrorString(e));
+      (void)hipGetLastError();  // clear an already-enabled status
+    }
+  } else {
+    h->grp_comms.assign(n, nullptr);
+    std::vector<int> dl(devs, devs + n);
+    comm_trace("group: ncclCommInitAll n=%u", n);
+    const ncclResult_t r = ncclCommInitAll(h->grp_comms.data(), (int)n, dl.data());
+    if (r != ncclSuccess) {
+      h->grp_comms.clear();
+      FAIL(h, VPTMCM_ECOMM, "ncclCommInitAll over %u devices: %s", n, ncclGetErrorString(r));
+    }
+  }
+  return VPTMCM_OK;
+}
+
+static int create_group(const vptmcm_config* cfg, vptmcm** out) {
+  const uint32_t n = cfg->n_devices;
+  if (n > VPTMCM_MAX_DEVICES) {
+    g_create_error = "vptmcm_create: at most VPTMCM_MAX_DEVICES (8) devices";
+    return VPTMCM_EINVAL;
+  }
+  if (cfg->group_transport > VPTMCM_GROUP_RCCL) {
+    g_create_error = "vptmcm_create: unknown group transport";
+    return VPTMCM_EINVAL;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    g_create_error = "vptmcm_create: no HIP device available";
+    return VPTMCM_EHIP;
+  }
+  for (uint32_t k = 0; k < n; k++) {
+    if (cfg->devices[k] < 0 || cfg->devices[k] >= ndev) {
+      g_create_error = "vptmcm_create: devices[" + std::to_string(k) + "] = " +
+                       std::to_string(cfg->devices[k]) + " is not a device ordinal (" +
+                       std::to_string(ndev) + " devices)";
+      return VPTMCM_EINVAL;
+    }
+    for (uint32_t j = 0; j < k && cfg->group_transport == VPTMCM_GROUP_RCCL; j++)
+      if (cfg->devices[j] == cfg->devices[k]) {
+        g_create_error = "vptmcm_create: the RCCL group transport needs distinct devices (RCCL "
+                         "refuses two ranks on one GPU); VPTMCM_GROUP_PEER allows repeats";
+        return VPTMCM_EINVAL;
+      }
+  }
+  vptmcm_config one = *cfg;
+  one.n_devices = 0;
+  one.device = cfg->devices[0];
+  vptmcm* h = nullptr;
+  int rc = vptmcm_create(&one, &h);
+  if (rc) return rc;
+  h->grouped = true;
+  h->group_transport = cfg->group_transport;
+  auto fail = [&](int code, const std::string& msg) {
+    vptmcm_destroy(h);
+    g_create_error = msg;
+    return code;
+  };
+  for (uint32_t k = 1; k < n; k++) {
+    one.device = cfg->devices[k];
+    vptmcm* c = nullptr;
+    rc = vptmcm_create(&one, &c);
+    if (rc) return fail(rc, "replica " + std::to_string(k) + ": " + g_create_error);
+    c->replica = k;
+    h->peers.push_back(c);
+  }
+  if (n > 1 || h->group_transport == VPTMCM_GROUP_RCCL) {
+    if ((rc = group_alloc(h, cfg->devices, n))) return fail(rc, "vptmcm_create: " + h->err);
+  }
+  *out = h;
+  return VPTMCM_OK;
+}
+
+// The composite of the current frame over every replica, enqueued on replica
+// 0's stream: each replica packs (rgb*n, n) on its own stream; PEER copies the
+// peers' packs to devices[0] in replica order (a peer copy over xGMI, or a
+// device copy for a repeated device) and k_composite sums them in that order;
+// RCCL reduces the packs to devices[0] (grouped ncclReduce) and k_composite
+// divides. Asynchronous.
+static int group_composite(vptmcm* h) {
+  const uint32_t n = 1u + (uint32_t)h->peers.size();
+  const size_t npx = (size_t)h->R * h->R, bytes = npx * sizeof(float4);
+  int rc = for_replicas(h, [&](vptmcm* c) {
+    if (int r = flush_renders(c)) return r;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, h->grp_done, 0));  // the last composite read the pack
+    const MarchParams P = make_params(c, kNoMatrix, 0);
+    HIPCHK(c, launch_pack(P, c->photons, c->rgb32, c->grp_pack, c->stream));
+    HIPCHK(c, hipEventRecord(c->grp_packed, c->stream));
+    return VPTMCM_OK;
+  });
+  if (rc) return rc;
+  CompositeSrc S;
+  memset(&S, 0, sizeof S);
+  if (h->group_transport == VPTMCM_GROUP_RCCL) {
+    if (ncclGroupStart() != ncclSuccess) FAIL(h, VPTMCM_ECOMM, "composite: ncclGroupStart failed");
+    ncclResult_t r = ncclSuccess;
+    for (uint32_t k = 0; k < n && r == ncclSuccess; k++) {
+      vptmcm* c = k ? h->peers[k - 1] : h;
+      r = ncclReduce(c->grp_pack, k ? c->grp_pack : h->grp_gather, npx * 4, ncclFloat32, ncclSum, 0,
+                     h->grp_comms[k], c->stream);
+    }
+    const ncclResult_t re = ncclGroupEnd();
+    if (r != ncclSuccess || re != ncclSuccess)
+      FAIL(h, VPTMCM_ECOMM, "composite: ncclReduce: %s", ncclGetErrorString(r != ncclSuccess ? r : re));
+    HIPCHK(h, hipSetDevice(h->device));
+    S.n = 1;
+    S.p[0] = h->grp_gather;
+  } else {
+    HIPCHK(h, hipSetDevice(h->device));
+    S.n = n;
+    S.p[0] = h->grp_pack;
+    for (uint32_t k = 1; k < n; k++) {
+      vptmcm* c = h->peers[k - 1];
+      float4* dst = h->grp_gather + (size_t)(k - 1) * npx;
+      HIPCHK(h, hipStreamWaitEvent(h->stream, c->grp_packed, 0));
+      HIPCHK(h, hipMemcpyPeerAsync(dst, h->device, c->grp_pack, c->device, bytes, h->stream));
+      S.p[k] = dst;
+    }
+  }
+  HIPCHK(h, launch_composite(S, (uint32_t)npx, h->grp_rgb32, h->grp_rgba, nullptr, h->stream));
+  HIPCHK(h, hipEventRecord(h->grp_done, h->stream));
+  h->grp_dirty = false;
+  return VPTMCM_OK;
 }
 
 int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
@@ -671,6 +891,7 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
     g_create_error = "vptmcm_create: unknown volume layout";
     return VPTMCM_EINVAL;
   }
+  if (cfg->n_devices > 0) return create_group(cfg, out);
   vptmcm* h = new vptmcm();
   auto fail = [&](int code) {
     g_create_error = h->err;
@@ -757,6 +978,30 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
 
 void vptmcm_destroy(vptmcm* h) {
   if (!h) return;
+  for (vptmcm* c : h->peers) {  // replicas first: their streams may feed this one's composite
+    if (c->stream) (void)wait_stream(c, c->stream, "destroy");
+  }
+  if (h->stream) (void)wait_stream(h, h->stream, "destroy");
+  for (ncclComm_t c : h->grp_comms)
+    if (c) (void)ncclCommDestroy(c);
+  for (vptmcm* c : h->peers) {
+    if (c->grp_pack) (void)hipFree(c->grp_pack);
+    if (c->grp_packed) (void)hipEventDestroy(c->grp_packed);
+    c->grp_pack = nullptr;
+    c->grp_packed = nullptr;
+    vptmcm_destroy(c);
+  }
+  h->peers.clear();
+  (void)hipSetDevice(h->device);
+  if (h->grp_pack) (void)hipFree(h->grp_pack);
+  if (h->grp_packed) (void)hipEventDestroy(h->grp_packed);
+  if (h->grp_gather) (void)hipFree(h->grp_gather);
+  if (h->grp_rgb32) (void)hipFree(h->grp_rgb32);
+  if (h->grp_rgba) (void)hipFree(h->grp_rgba);
+  if (h->grp_done) (void)hipEventDestroy(h->grp_done);
+  if (h->comp_rgb32) (void)hipFree(h->comp_rgb32);
+  if (h->comp_rgba) (void)hipFree(h->comp_rgba);
+  if (h->comp_counts) (void)hipFree(h->comp_counts);
   // bounded waits while a communicator exists (a failed one is aborted)
   if (h->comm_stream) (void)wait_stream(h, h->comm_stream, "destroy");
   if (h->stream) (void)wait_stream(h, h->stream, "destroy");
@@ -769,7 +1014,6 @@ void vptmcm_destroy(vptmcm* h) {
     if (h->comp_done[k]) (void)hipEventDestroy(h->comp_done[k]);
   }
   if (h->host_scratch) (void)hipFree(h->host_scratch);
-  if (h->comp_host) (void)hipHostFree(h->comp_host);
   if (h->region.beg) (void)hipEventDestroy(h->region.beg);
   if (h->region.end) (void)hipEventDestroy(h->region.end);
   free_volume(h);
@@ -800,7 +1044,7 @@ void vptmcm_destroy(vptmcm* h) {
 // touches are re-laid out at once, so its bricks are resident in HBM as soon
 // as its placement arrives and the volume is renderable throughout (blocks
 // not yet written read as zero density); end frees the staging copy.
-int vptmcm_volume_begin(vptmcm* h, uint32_t width, uint32_t height, uint32_t depth) {
+static int volume_begin_one(vptmcm* h, uint32_t width, uint32_t height, uint32_t depth) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!width || !height || !depth || width > 8192 || height > 8192 || depth > 8192)
@@ -842,7 +1086,7 @@ int vptmcm_volume_begin(vptmcm* h, uint32_t width, uint32_t height, uint32_t dep
   return VPTMCM_OK;
 }
 
-int vptmcm_volume_write_block(vptmcm* h, const uint8_t* data, uint32_t x, uint32_t y, uint32_t z,
+static int volume_write_block_one(vptmcm* h, const uint8_t* data, uint32_t x, uint32_t y, uint32_t z,
                               uint32_t bw, uint32_t bh, uint32_t bd) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
@@ -882,7 +1126,7 @@ int vptmcm_volume_write_block(vptmcm* h, const uint8_t* data, uint32_t x, uint32
   return VPTMCM_OK;
 }
 
-int vptmcm_volume_end(vptmcm* h) {
+static int volume_end_one(vptmcm* h) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!h->vol_lin || h->vol_done) FAIL(h, VPTMCM_ESTATE, "volume_end without volume_begin");
@@ -909,7 +1153,7 @@ int vptmcm_set_volume(vptmcm* h, const uint8_t* voxels, uint32_t width, uint32_t
   return vptmcm_volume_end(h);
 }
 
-int vptmcm_set_material_tf(vptmcm* h, const uint8_t* rgba) {
+static int set_material_tf_one(vptmcm* h, const uint8_t* rgba) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!rgba) FAIL(h, VPTMCM_EINVAL, "set_material_tf: null data");
@@ -975,7 +1219,7 @@ int vptmcm_set_material_tf(vptmcm* h, const uint8_t* rgba) {
   return VPTMCM_OK;
 }
 
-int vptmcm_set_light(vptmcm* h, const uint8_t* spd, const float dir[3]) {
+static int set_light_one(vptmcm* h, const uint8_t* spd, const float dir[3]) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!spd || !dir) FAIL(h, VPTMCM_EINVAL, "set_light: null argument");
@@ -987,7 +1231,7 @@ int vptmcm_set_light(vptmcm* h, const uint8_t* spd, const float dir[3]) {
   return VPTMCM_OK;
 }
 
-int vptmcm_set_spectrum(vptmcm* h, const float* buf) {
+static int set_spectrum_one(vptmcm* h, const float* buf) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!buf) FAIL(h, VPTMCM_EINVAL, "set_spectrum: null buffer");
@@ -999,7 +1243,7 @@ int vptmcm_set_spectrum(vptmcm* h, const float* buf) {
   return build_bin_lut(h);
 }
 
-int vptmcm_set_transfer_function(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height) {
+static int set_transfer_function_one(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (h->kind != VPTMCM_RENDERER_RGB)
@@ -1022,7 +1266,7 @@ int vptmcm_set_transfer_function(vptmcm* h, const uint8_t* rgba, uint32_t width,
   return VPTMCM_OK;
 }
 
-int vptmcm_set_environment(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height) {
+static int set_environment_one(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!rgba || width != 1 || height != 1)
@@ -1032,7 +1276,7 @@ int vptmcm_set_environment(vptmcm* h, const uint8_t* rgba, uint32_t width, uint3
   return VPTMCM_OK;
 }
 
-int vptmcm_set_band(vptmcm* h, uint32_t y0, uint32_t y1) {
+static int set_band_one(vptmcm* h, uint32_t y0, uint32_t y1) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!(y0 < y1 && y1 <= h->R && y0 % 8u == 0u && (y1 % 8u == 0u || y1 == h->R)))
@@ -1044,10 +1288,11 @@ int vptmcm_set_band(vptmcm* h, uint32_t y0, uint32_t y1) {
   if (y0 > 0) HIPCHK(h, hipMemsetAsync(h->rgb32, 0, y0 * row, h->stream));
   if (y1 < h->R)
     HIPCHK(h, hipMemsetAsync((char*)h->rgb32 + y1 * row, 0, (h->R - y1) * row, h->stream));
+  h->grp_dirty = true;
   return VPTMCM_OK;
 }
 
-int vptmcm_set_params(vptmcm* h, const vptmcm_params* p) {
+static int set_params_one(vptmcm* h, const vptmcm_params* p) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (!p) FAIL(h, VPTMCM_EINVAL, "set_params: null params");
   // The reference rewrites the same uniform values before every pass
@@ -1061,7 +1306,7 @@ int vptmcm_set_params(vptmcm* h, const vptmcm_params* p) {
 
 // ------------------------------------------------------------------ hot path
 
-int vptmcm_reset(vptmcm* h, const float* mvp, uint32_t seed_bits) {
+static int reset_one(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!mvp) FAIL(h, VPTMCM_EINVAL, "reset: null matrix");
@@ -1071,10 +1316,11 @@ int vptmcm_reset(vptmcm* h, const float* mvp, uint32_t seed_bits) {
     HIPCHK(h, launch_reset_rgb(P, h->photons, h->stream));
   else
     HIPCHK(h, launch_reset(P, h->photons, h->stream));
+  h->grp_dirty = true;
   return VPTMCM_OK;
 }
 
-int vptmcm_render(vptmcm* h, const float* mvp, uint32_t seed_bits) {
+static int render_one(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (!mvp) FAIL(h, VPTMCM_EINVAL, "render: null matrix");
   if (!h->volume_ready) FAIL(h, VPTMCM_ESTATE, "render: no volume set (setVolume first)");
@@ -1089,7 +1335,7 @@ int vptmcm_render(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   return VPTMCM_OK;
 }
 
-int vptmcm_render_passes(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
+static int render_passes_one(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!mvp || (!seeds && n)) FAIL(h, VPTMCM_EINVAL, "render_passes: null argument");
@@ -1102,7 +1348,7 @@ int vptmcm_render_passes(vptmcm* h, const float* mvp, const uint32_t* seeds, uin
   return VPTMCM_OK;
 }
 
-int vptmcm_synchronize(vptmcm* h) {
+static int synchronize_one(vptmcm* h) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   HIPCHK(h, hipSetDevice(h->device));
@@ -1119,9 +1365,11 @@ int vptmcm_read_rgba16f(vptmcm* h, uint16_t* out) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!out) FAIL(h, VPTMCM_EINVAL, "read_rgba16f: null output");
+  if (composited(h) && h->grp_dirty)
+    if (int rc = group_composite(h)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipMemcpyAsync(out, h->rgba, (size_t)h->R * h->R * 8, hipMemcpyDeviceToHost,
-                           h->stream));
+  HIPCHK(h, hipMemcpyAsync(out, composited(h) ? h->grp_rgba : h->rgba, (size_t)h->R * h->R * 8,
+                           hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return VPTMCM_OK;
 }
@@ -1130,9 +1378,11 @@ int vptmcm_read_rgb(vptmcm* h, float* out) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!out) FAIL(h, VPTMCM_EINVAL, "read_rgb: null output");
+  if (composited(h) && h->grp_dirty)
+    if (int rc = group_composite(h)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipMemcpyAsync(out, h->rgb32, (size_t)h->R * h->R * 3 * sizeof(float),
-                           hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipMemcpyAsync(out, composited(h) ? h->grp_rgb32 : h->rgb32,
+                           (size_t)h->R * h->R * 3 * sizeof(float), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return VPTMCM_OK;
 }
@@ -1158,6 +1408,8 @@ int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!params) FAIL(h, VPTMCM_EINVAL, "tonemap_artistic: null params");
+  if (composited(h) && h->grp_dirty)
+    if (int rc = group_composite(h)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
   const size_t npx = (size_t)h->R * h->R;
   if (!h->ldr) HIPCHK(h, hipMalloc(&h->ldr, npx * 4));
@@ -1170,7 +1422,8 @@ int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out
   T.saturation = params[3];
   const float midpoint = (mid - low) / range;
   T.exponent = (float)(-std::log((double)midpoint) / std::log(2.0)) / params[4];
-  HIPCHK(h, launch_tonemap_artistic(h->rgba, (uint32_t)npx, T, h->ldr, h->stream));
+  HIPCHK(h, launch_tonemap_artistic(composited(h) ? h->grp_rgba : h->rgba, (uint32_t)npx, T, h->ldr,
+                                    h->stream));
   if (rgba8_out) {
     HIPCHK(h, hipMemcpyAsync(rgba8_out, h->ldr, npx * 4, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -1257,12 +1510,13 @@ int vptmcm_write_photons(vptmcm* h, const void* in) {
   HIPCHK(h, hipMemcpyAsync(h->photons, planes.data(), planes.size() * 4, hipMemcpyHostToDevice,
                            h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->grp_dirty = true;
   return VPTMCM_OK;
 }
 
 // --------------------------------------------------------------- measurement
 
-int vptmcm_enable_kernel_timing(vptmcm* h, int enable) {
+static int enable_kernel_timing_one(vptmcm* h, int enable) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   HIPCHK(h, hipSetDevice(h->device));
@@ -1318,6 +1572,8 @@ int vptmcm_comm_init(vptmcm* h, const uint8_t* uid, int nranks, int rank) {
   if (!uid || nranks < 1 || rank < 0 || rank >= nranks)
     FAIL(h, VPTMCM_EINVAL, "comm_init: bad arguments (nranks=%d rank=%d)", nranks, rank);
   if (h->comm) FAIL(h, VPTMCM_ESTATE, "comm_init: communicator already initialised");
+  if (h->grouped && (composited(h) || !h->grp_comms.empty()))
+    FAIL(h, VPTMCM_ESTATE, "comm_init: a device-list handle composites its replicas itself");
   HIPCHK(h, hipSetDevice(h->device));
   if (const char* v = getenv("VPTMCM_COMM_TIMEOUT_MS")) {
     const long long t = strtoll(v, nullptr, 10);
@@ -1382,7 +1638,6 @@ int vptmcm_comm_init(vptmcm* h, const uint8_t* uid, int nranks, int rank) {
     HIPCHK(h, hipEventRecord(h->comp_done[k], h->comm_stream));
   }
   HIPCHK(h, hipMalloc(&h->host_scratch, 64 * sizeof(double)));
-  HIPCHK(h, hipHostMalloc(reinterpret_cast<void**>(&h->comp_host), bytes, hipHostMallocDefault));
   return VPTMCM_OK;
 }
 
@@ -1410,25 +1665,69 @@ int vptmcm_comm_allreduce_radiance(vptmcm* h) {
 
 int vptmcm_comm_read_composite(vptmcm* h, float* rgb, float* counts) {
   if (check_handle(h)) return VPTMCM_EINVAL;
-  if (int rc_ = flush_renders(h)) return rc_;
-  if (!h->comm || h->comp_last < 0) FAIL(h, VPTMCM_ESTATE, "read_composite: no all-reduce issued");
   if (!rgb) FAIL(h, VPTMCM_EINVAL, "read_composite: null output");
-  HIPCHK(h, hipSetDevice(h->device));
+  if (!h->comm || h->comp_last < 0) FAIL(h, VPTMCM_ESTATE, "read_composite: no all-reduce issued");
+  return vptmcm_read_composite(h, nullptr, rgb, counts);
+}
+
+int vptmcm_read_composite(vptmcm* h, uint16_t* rgba16f, float* rgb, float* counts) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h)) return rc_;
   const size_t npx = (size_t)h->R * h->R;
-  // ordered behind the last all-reduce on its own stream (the march stream
-  // keeps running), into pinned memory
-  HIPCHK(h, hipMemcpyAsync(h->comp_host, h->comp[h->comp_last], npx * sizeof(float4),
-                           hipMemcpyDeviceToHost, h->comm_stream));
-  if (int rc = wait_stream(h, h->comm_stream, "comm_read_composite")) return rc;
-  const float4* buf = h->comp_host;
-  for (size_t i = 0; i < npx; i++) {
-    const float n = buf[i].w;
-    rgb[i * 3 + 0] = n > 0.0f ? buf[i].x / n : 0.0f;
-    rgb[i * 3 + 1] = n > 0.0f ? buf[i].y / n : 0.0f;
-    rgb[i * 3 + 2] = n > 0.0f ? buf[i].z / n : 0.0f;
-    if (counts) counts[i] = n;
+  if (h->grouped) {  // a device-list handle: over its replicas (N = 1 included)
+    if (h->grp_dirty || !h->grp_rgb32) {
+      if (!h->grp_rgb32) {  // one replica, PEER: the buffers of the composite on first use
+        const int32_t dev = h->device;
+        if (int rc = group_alloc(h, &dev, 1)) return rc;
+      }
+      if (int rc = group_composite(h)) return rc;
+    }
+    HIPCHK(h, hipSetDevice(h->device));
+    if (counts) {  // sum(n): the composite kernel again, counts only (cheap, same order)
+      CompositeSrc S;
+      memset(&S, 0, sizeof S);
+      if (h->group_transport == VPTMCM_GROUP_RCCL) {
+        S.n = 1;
+        S.p[0] = h->grp_gather;
+      } else {
+        S.n = 1u + (uint32_t)h->peers.size();
+        S.p[0] = h->grp_pack;
+        for (uint32_t k = 1; k < S.n; k++) S.p[k] = h->grp_gather + (size_t)(k - 1) * npx;
+      }
+      if (!h->comp_counts) HIPCHK(h, hipMalloc(&h->comp_counts, npx * sizeof(float)));
+      HIPCHK(h, launch_composite(S, (uint32_t)npx, nullptr, nullptr, h->comp_counts, h->stream));
+      HIPCHK(h, hipMemcpyAsync(counts, h->comp_counts, npx * sizeof(float), hipMemcpyDeviceToHost,
+                               h->stream));
+    }
+    if (rgba16f)
+      HIPCHK(h, hipMemcpyAsync(rgba16f, h->grp_rgba, npx * 8, hipMemcpyDeviceToHost, h->stream));
+    if (rgb)
+      HIPCHK(h, hipMemcpyAsync(rgb, h->grp_rgb32, npx * 3 * sizeof(float), hipMemcpyDeviceToHost,
+                               h->stream));
+    return wait_stream(h, h->stream, "read_composite");
   }
-  return VPTMCM_OK;
+  if (!h->comm || h->comp_last < 0)
+    FAIL(h, VPTMCM_ESTATE, "read_composite: no all-reduce issued (and not a device-list handle)");
+  HIPCHK(h, hipSetDevice(h->device));
+  // on the composite stream, behind the last all-reduce (the march stream keeps running)
+  if (!h->comp_rgb32) HIPCHK(h, hipMalloc(&h->comp_rgb32, npx * 3 * sizeof(float)));
+  if (!h->comp_rgba) HIPCHK(h, hipMalloc(&h->comp_rgba, npx * 4 * sizeof(uint16_t)));
+  if (!h->comp_counts) HIPCHK(h, hipMalloc(&h->comp_counts, npx * sizeof(float)));
+  CompositeSrc S;
+  memset(&S, 0, sizeof S);
+  S.n = 1;
+  S.p[0] = h->comp[h->comp_last];
+  HIPCHK(h, launch_composite(S, (uint32_t)npx, h->comp_rgb32, h->comp_rgba, h->comp_counts,
+                             h->comm_stream));
+  if (rgba16f)
+    HIPCHK(h, hipMemcpyAsync(rgba16f, h->comp_rgba, npx * 8, hipMemcpyDeviceToHost, h->comm_stream));
+  if (rgb)
+    HIPCHK(h, hipMemcpyAsync(rgb, h->comp_rgb32, npx * 3 * sizeof(float), hipMemcpyDeviceToHost,
+                             h->comm_stream));
+  if (counts)
+    HIPCHK(h, hipMemcpyAsync(counts, h->comp_counts, npx * sizeof(float), hipMemcpyDeviceToHost,
+                             h->comm_stream));
+  return wait_stream(h, h->comm_stream, "read_composite");
 }
 
 int vptmcm_comm_gather_bands(vptmcm* h, float* rgb) {
@@ -1575,6 +1874,110 @@ int vptmcm_debug_verify(vptmcm* h, int fn, uint32_t lo, uint64_t count, uint64_t
   (void)hipFree(dfirst);
   if (e != hipSuccess) FAIL(h, VPTMCM_EHIP, "debug_verify: %s", hipGetErrorString(e));
   *mismatches = nb;
+  return VPTMCM_OK;
+}
+
+// ------------------------------------------------ device-list entry points
+// Each input and each pass goes to every replica (replica 0 first, then the
+// peers in order); a pass's seed bits become each replica's own stream.
+
+int vptmcm_volume_begin(vptmcm* h, uint32_t width, uint32_t height, uint32_t depth) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  return for_replicas(h, [&](vptmcm* c) { return volume_begin_one(c, width, height, depth); });
+}
+
+int vptmcm_volume_write_block(vptmcm* h, const uint8_t* data, uint32_t x, uint32_t y, uint32_t z,
+                              uint32_t bw, uint32_t bh, uint32_t bd) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  return for_replicas(h, [&](vptmcm* c) { return volume_write_block_one(c, data, x, y, z, bw, bh, bd); });
+}
+
+int vptmcm_volume_end(vptmcm* h) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  return for_replicas(h, [&](vptmcm* c) { return volume_end_one(c); });
+}
+
+int vptmcm_set_material_tf(vptmcm* h, const uint8_t* rgba) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  return for_replicas(h, [&](vptmcm* c) { return set_material_tf_one(c, rgba); });
+}
+
+int vptmcm_set_light(vptmcm* h, const uint8_t* spd, const float dir[3]) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  return for_replicas(h, [&](vptmcm* c) { return set_light_one(c, spd, dir); });
+}
+
+int vptmcm_set_spectrum(vptmcm* h, const float* buf) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  return for_replicas(h, [&](vptmcm* c) { return set_spectrum_one(c, buf); });
+}
+
+int vptmcm_set_transfer_function(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  return for_replicas(h, [&](vptmcm* c) { return set_transfer_function_one(c, rgba, width, height); });
+}
+
+int vptmcm_set_environment(vptmcm* h, const uint8_t* rgba, uint32_t width, uint32_t height) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  return for_replicas(h, [&](vptmcm* c) { return set_environment_one(c, rgba, width, height); });
+}
+
+int vptmcm_set_band(vptmcm* h, uint32_t y0, uint32_t y1) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  return for_replicas(h, [&](vptmcm* c) { return set_band_one(c, y0, y1); });
+}
+
+int vptmcm_set_params(vptmcm* h, const vptmcm_params* p) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  return for_replicas(h, [&](vptmcm* c) { return set_params_one(c, p); });
+}
+
+int vptmcm_reset(vptmcm* h, const float* mvp, uint32_t seed_bits) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  return for_replicas(h, [&](vptmcm* c) { return reset_one(c, mvp, replica_seed(seed_bits, c->replica)); });
+}
+
+int vptmcm_render(vptmcm* h, const float* mvp, uint32_t seed_bits) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (h->peers.empty()) return render_one(h, mvp, seed_bits);  // the per-pass call: no closure
+  return for_replicas(h, [&](vptmcm* c) { return render_one(c, mvp, replica_seed(seed_bits, c->replica)); });
+}
+
+int vptmcm_render_passes(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (h->peers.empty()) return render_passes_one(h, mvp, seeds, n);
+  if (!seeds && n) FAIL(h, VPTMCM_EINVAL, "render_passes: null argument");
+  std::vector<uint32_t> rs(n);
+  return for_replicas(h, [&](vptmcm* c) {
+    for (uint32_t k = 0; k < n; k++) rs[k] = replica_seed(seeds[k], c->replica);
+    return render_passes_one(c, mvp, rs.data(), n);
+  });
+}
+
+int vptmcm_synchronize(vptmcm* h) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  return for_replicas(h, [&](vptmcm* c) { return synchronize_one(c); });
+}
+
+int vptmcm_enable_kernel_timing(vptmcm* h, int enable) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  return for_replicas(h, [&](vptmcm* c) { return enable_kernel_timing_one(c, enable); });
+}
+
+int vptmcm_composite(vptmcm* h) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!composited(h)) return VPTMCM_OK;
+  return group_composite(h);
+}
+
+int vptmcm_group_devices(vptmcm* h, int32_t* devices, uint32_t* n) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!n) FAIL(h, VPTMCM_EINVAL, "group_devices: null count");
+  *n = 1u + (uint32_t)h->peers.size();
+  if (devices) {
+    devices[0] = h->device;
+    for (size_t k = 0; k < h->peers.size(); k++) devices[k + 1] = h->peers[k]->device;
+  }
   return VPTMCM_OK;
 }
 

@@ -12,7 +12,8 @@
 //   setResolution(n)    -> base :71-77 (+ reset)
 //   setTransferFunction -> base :62-69 (kept for the surface; unused by the kernel)
 //   getTexture()        -> the rgba16float radiance image (host copy: a HIP
-//                          renderer cannot hand out a GPUTexture)
+//                          renderer cannot hand out a GPUTexture); with a
+//                          device list, the composite of every GPU's photons
 //   destroy()           -> js:207-211
 // DOM reads of the reference (#light-editor, #spectrum-representation,
 // #material-transfer-function) become explicit setters and change-event payloads.
@@ -36,6 +37,7 @@ function native() {
 }
 
 const LAYOUTS = { linear: 0, corner8: 1, brick8: 2 };
+const TRANSPORTS = { peer: 0, rccl: 1 };  // vptmcm_config::group_transport
 const RESET_ON = ['extinction', 'anisotropy', 'bounces', 'materialTransferFunction',
   'spectrumRepresentation', 'lightEditor'];  // js:116-125
 
@@ -45,7 +47,10 @@ function f32bits(x) {
 }
 
 class MCMSpectralComputeRenderer extends PropertyBag {
-  // device: { ordinal, layout } (or a device ordinal); volume: a Volume (readers.js)
+  // device: { ordinal, layout } (or a device ordinal), or { devices: [ordinals],
+  // layout, transport } for one renderer driving several GPUs (one
+  // photon-parallel replica per entry; options.devices works too; transport
+  // 'peer' (default, deterministic ordered composite) or 'rccl'); volume: a Volume (readers.js)
   // or an object with { data, width, height, depth }; camera: Camera.js or the
   // reference's camera node; environment: accepted and ignored, as the kernel's
   // environment sampling is dead code (wgsl:144-146).
@@ -53,7 +58,8 @@ class MCMSpectralComputeRenderer extends PropertyBag {
     super();
     this._resolution = options.resolution !== undefined ? options.resolution : 512;
     this._workgroup_size = options.workgroup_size || [8, 8];
-    this._device = typeof device === 'number' ? { ordinal: device } : (device || {});
+    this._device = typeof device === 'number' ? { ordinal: device } : Object.assign({}, device || {});
+    if (options.devices && !this._device.devices) this._device.devices = options.devices;
     this._volume = volume || null;
     this._camera = camera;
     this._environment = environment;
@@ -91,7 +97,16 @@ class MCMSpectralComputeRenderer extends PropertyBag {
     const layout = LAYOUTS[this._device.layout || 'corner8'];
     if (layout === undefined) throw new Error(`unknown volume layout '${this._device.layout}'`);
     const ordinal = this._device.ordinal !== undefined ? this._device.ordinal : -1;
-    this._h = native().create(this._resolution, ordinal, layout);
+    const devs = this._device.devices;
+    if (devs !== undefined) {
+      if (!Array.isArray(devs) || devs.length < 1 || devs.length > 8)
+        throw new Error('devices: an array of 1 to 8 device ordinals');
+      const transport = TRANSPORTS[this._device.transport || 'peer'];
+      if (transport === undefined) throw new Error(`unknown transport '${this._device.transport}'`);
+      this._h = native().create(this._resolution, ordinal, layout, 0, devs.map(d => d | 0), transport);
+    } else {
+      this._h = native().create(this._resolution, ordinal, layout);
+    }
     this._dirty = { light: true, tf: true, spectrum: true };
     this._volumeReady = false;
     if (this._volume) this._uploadVolume(this._volume);
@@ -231,6 +246,18 @@ class MCMSpectralComputeRenderer extends PropertyBag {
     const seeds = new Uint32Array(n);
     for (let k = 0; k < n; k++) seeds[k] = this._seedBits();
     native().renderPasses(this._h, m, seeds);
+  }
+
+  // The GPUs this renderer drives (its device list; one entry without one).
+  devices() {
+    return native().groupDevices(this._h);
+  }
+
+  // Enqueue the composite of the current frame over the GPUs (asynchronous;
+  // getTexture() makes it when it is missing). A progressive display calls it
+  // once per shown frame, right after that frame's render().
+  composite() {
+    native().composite(this._h);
   }
 
   // What the last march launch ran: { mode, tpl, spec, passes, launches }

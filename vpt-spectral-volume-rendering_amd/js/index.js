@@ -11,8 +11,12 @@ const spectrum = require('./spectrum');
 const ui = require('./ui');
 const mat4 = require('./mat4');
 
-// A HIP device descriptor in place of the reference's GPUDevice.
-function createDevice(ordinal = 0, layout = 'corner8') {
+// A HIP device descriptor in place of the reference's GPUDevice: one ordinal,
+// or a list of ordinals for one renderer driving several GPUs (a
+// photon-parallel replica per GPU, composited on the first; transport 'peer'
+// or 'rccl', include/vptmcm.h).
+function createDevice(ordinal = 0, layout = 'corner8', transport = 'peer') {
+  if (Array.isArray(ordinal)) return { devices: ordinal.slice(), layout, transport };
   return { ordinal, layout };
 }
 

@@ -155,11 +155,14 @@ static void finalize_box(napi_env env, void* data, void* hint) {
     free(box);
 }
 
-/* create(resolution, device, layout[, renderer]) -> handle */
+/* create(resolution, device, layout[, renderer[, devices[, transport]]]) -> handle;
+ * devices: an array of device ordinals (vptmcm_config::n_devices, one
+ * photon-parallel replica per entry, composited on devices[0]) */
 static napi_value js_create(napi_env env, napi_callback_info info) {
     napi_value argv[3];
     if (get_args(env, info, 3, argv)) return NULL;
     vptmcm_config cfg;
+    memset(&cfg, 0, sizeof cfg);
     cfg.resolution = get_u32(env, argv[0]);
     cfg.max_bins = VPTMCM_MAX_BINS;
     int32_t dev = -1;
@@ -167,13 +170,35 @@ static napi_value js_create(napi_env env, napi_callback_info info) {
     cfg.device = dev;
     cfg.volume_layout = get_u32(env, argv[2]);
     cfg.renderer = VPTMCM_RENDERER_SPECTRAL;
-    {   /* optional 4th argument: renderer kind */
-        size_t argc = 4;
-        napi_value all[4];
-        if (napi_get_cb_info(env, info, &argc, all, NULL, NULL) == napi_ok && argc >= 4) {
+    {   /* optional: renderer kind, device list, group transport */
+        size_t argc = 6;
+        napi_value all[6];
+        if (napi_get_cb_info(env, info, &argc, all, NULL, NULL) == napi_ok) {
             napi_valuetype t;
-            napi_typeof(env, all[3], &t);
-            if (t == napi_number) cfg.renderer = get_u32(env, all[3]);
+            if (argc >= 4 && napi_typeof(env, all[3], &t) == napi_ok && t == napi_number)
+                cfg.renderer = get_u32(env, all[3]);
+            bool is_arr = false;
+            if (argc >= 5 && napi_is_array(env, all[4], &is_arr) == napi_ok && is_arr) {
+                uint32_t n = 0;
+                napi_get_array_length(env, all[4], &n);
+                if (n < 1 || n > VPTMCM_MAX_DEVICES) {
+                    napi_throw_range_error(env, NULL, "devices: 1 to VPTMCM_MAX_DEVICES (8) ordinals");
+                    return NULL;
+                }
+                for (uint32_t k = 0; k < n; k++) {
+                    napi_value e;
+                    int32_t d = -1;
+                    napi_get_element(env, all[4], k, &e);
+                    if (napi_get_value_int32(env, e, &d) != napi_ok) {
+                        napi_throw_type_error(env, NULL, "devices: expected integer ordinals");
+                        return NULL;
+                    }
+                    cfg.devices[k] = d;
+                }
+                cfg.n_devices = n;
+            }
+            if (argc >= 6 && napi_typeof(env, all[5], &t) == napi_ok && t == napi_number)
+                cfg.group_transport = get_u32(env, all[5]);
         }
     }
     vptmcm* h = NULL;
@@ -513,6 +538,52 @@ static napi_value js_last_launch(napi_env env, napi_callback_info info) {
     return o;
 }
 
+/* composite(h): enqueue the replicas' composite of the current frame */
+static napi_value js_composite(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (get_args(env, info, 1, argv)) return NULL;
+    vptmcm* h = get_handle(env, argv[0]);
+    if (!h) return NULL;
+    return check(env, h, vptmcm_composite(h));
+}
+
+/* readComposite(h, Uint16Array(R*R*4) | null, Float32Array(R*R*3) | null, R) */
+static napi_value js_read_composite(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (get_args(env, info, 4, argv)) return NULL;
+    handle_box* box = get_box(env, argv[0]);
+    if (!box) return NULL;
+    napi_valuetype t1, t2;
+    napi_typeof(env, argv[1], &t1);
+    napi_typeof(env, argv[2], &t2);
+    uint16_t* q = NULL;
+    float* rgb = NULL;
+    if (t1 != napi_null && t1 != napi_undefined && !(q = get_frame_out(env, box, argv[1], argv[3], 2, 4)))
+        return NULL;
+    if (t2 != napi_null && t2 != napi_undefined && !(rgb = get_frame_out(env, box, argv[2], argv[3], 4, 3)))
+        return NULL;
+    return check(env, box->h, vptmcm_read_composite(box->h, q, rgb, NULL));
+}
+
+/* groupDevices(h) -> [ordinals] */
+static napi_value js_group_devices(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (get_args(env, info, 1, argv)) return NULL;
+    vptmcm* h = get_handle(env, argv[0]);
+    if (!h) return NULL;
+    int32_t d[VPTMCM_MAX_DEVICES];
+    uint32_t n = 0;
+    int rc = vptmcm_group_devices(h, d, &n);
+    if (rc) return throw_code(env, rc, vptmcm_last_error(h));
+    napi_value arr, x;
+    napi_create_array_with_length(env, n, &arr);
+    for (uint32_t k = 0; k < n; k++) {
+        napi_create_int32(env, d[k], &x);
+        napi_set_element(env, arr, k, x);
+    }
+    return arr;
+}
+
 static napi_value js_version(napi_env env, napi_callback_info info) {
     (void)info;
     napi_value s;
@@ -560,6 +631,9 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("setBand", js_set_band);
     EXPORT("commGatherBands", js_comm_gather_bands);
     EXPORT("lastLaunch", js_last_launch);
+    EXPORT("composite", js_composite);
+    EXPORT("readComposite", js_read_composite);
+    EXPORT("groupDevices", js_group_devices);
     EXPORT("version", js_version);
     return exports;
 }

@@ -35,12 +35,17 @@ EXPORTS = [
     "vptmcm_comm_init", "vptmcm_comm_allreduce_radiance", "vptmcm_comm_read_composite",
     "vptmcm_comm_barrier", "vptmcm_comm_allreduce_host", "vptmcm_debug_eval",
     "vptmcm_debug_verify", "vptmcm_debug_last_launch", "vptmcm_debug_schedule", "vptmcm_version",
+    "vptmcm_read_composite", "vptmcm_composite", "vptmcm_group_devices",
 ]
+MAX_DEVICES = 8
+GROUP_PEER, GROUP_RCCL = 0, 1
 
 
 class Config(C.Structure):
     _fields_ = [("resolution", C.c_uint32), ("max_bins", C.c_uint32), ("device", C.c_int32),
-                ("volume_layout", C.c_uint32), ("renderer", C.c_uint32)]
+                ("volume_layout", C.c_uint32), ("renderer", C.c_uint32),
+                ("n_devices", C.c_uint32), ("devices", C.c_int32 * MAX_DEVICES),
+                ("group_transport", C.c_uint32)]
 
 
 class Params(C.Structure):
@@ -120,6 +125,9 @@ def load() -> C.CDLL:
         "vptmcm_debug_last_launch": (C.c_int, [vp, u32p, C.POINTER(C.c_uint64)]),
         "vptmcm_debug_schedule": (C.c_int, [vp, u32p, C.c_uint32, u32p]),
         "vptmcm_version": (C.c_char_p, []),
+        "vptmcm_read_composite": (C.c_int, [vp, vp, vp, vp]),
+        "vptmcm_composite": (C.c_int, [vp]),
+        "vptmcm_group_devices": (C.c_int, [vp, C.POINTER(C.c_int32), u32p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -150,9 +158,19 @@ class Renderer:
     """Thin handle wrapper (one HIP device, one stream)."""
 
     def __init__(self, resolution: int = 512, device: int = -1, layout: int = LAYOUT_CORNER8,
-                 renderer: int = RENDERER_SPECTRAL):
+                 renderer: int = RENDERER_SPECTRAL, devices=None, transport: int = GROUP_PEER):
+        """devices: a device list (vptmcm_config::n_devices): one handle, one
+        photon-parallel replica per entry, composited on devices[0]."""
         self.L = load()
         cfg = Config(resolution, MAX_BINS, device, layout, renderer)
+        if devices is not None:
+            devices = list(devices)
+            if not 1 <= len(devices) <= MAX_DEVICES:
+                raise ValueError(f"1 to {MAX_DEVICES} devices, got {len(devices)}")
+            cfg.n_devices = len(devices)
+            for k, d in enumerate(devices):
+                cfg.devices[k] = int(d)
+            cfg.group_transport = int(transport)
         self.kind = renderer
         h = C.c_void_p()
         rc = self.L.vptmcm_create(C.byref(cfg), C.byref(h))
@@ -354,6 +372,23 @@ class Renderer:
         n = np.empty((self.R, self.R), np.float32)
         self._ck(self.L.vptmcm_comm_read_composite(self.h, _f32p(rgb), _f32p(n)))
         return rgb, n
+
+    def read_composite_all(self):
+        """vptmcm_read_composite: (rgba16f [R,R,4] u16, rgb [R,R,3] f32, counts [R,R] f32)."""
+        q = np.empty((self.R, self.R, 4), np.uint16)
+        rgb = np.empty((self.R, self.R, 3), np.float32)
+        n = np.empty((self.R, self.R), np.float32)
+        self._ck(self.L.vptmcm_read_composite(self.h, _ptr(q), _ptr(rgb), _ptr(n)))
+        return q, rgb, n
+
+    def composite(self) -> None:
+        self._ck(self.L.vptmcm_composite(self.h))
+
+    def group_devices(self) -> list:
+        n = np.zeros(1, np.uint32)
+        d = np.zeros(MAX_DEVICES, np.int32)
+        self._ck(self.L.vptmcm_group_devices(self.h, d.ctypes.data_as(C.POINTER(C.c_int32)), _u32p(n)))
+        return [int(x) for x in d[: int(n[0])]]
 
     def gather_bands(self) -> np.ndarray:
         """Mode B composite over the communicator: the fp32 image, bit-exact."""

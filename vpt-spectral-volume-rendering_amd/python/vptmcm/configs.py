@@ -106,16 +106,50 @@ def _synth_lib():
     return _synth
 
 
-def host_threads() -> int:
-    """CPU threads the CPU baselines use: the CPUs this process may run on
-    (its affinity mask), capped by OMP_NUM_THREADS when the job sets it."""
+def cgroup_cpu_quota(root: str = "/sys/fs/cgroup") -> float | None:
+    """CPUs' worth of time the process's cgroup may use (cpu.max quota / period,
+    cgroup v2; cpu.cfs_quota_us / cpu.cfs_period_us, v1), or None if unlimited
+    or unreadable. An affinity mask can list every CPU of the machine while the
+    quota grants a few of them."""
+    import math
     try:
-        n = len(os.sched_getaffinity(0))
+        q, p = Path(root, "cpu.max").read_text().split()[:2]
+        if q != "max" and int(p) > 0:
+            return int(q) / int(p)
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(Path(root, "cpu", "cpu.cfs_quota_us").read_text())
+        p = int(Path(root, "cpu", "cpu.cfs_period_us").read_text())
+        return q / p if q > 0 and p > 0 and math.isfinite(q / p) else None
+    except (OSError, ValueError):
+        return None
+
+
+def host_cpu_share() -> dict:
+    """The host CPUs this process may use, by each limit that applies."""
+    try:
+        aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        n = os.cpu_count() or 1
+        aff = os.cpu_count() or 1
     omp = os.environ.get("OMP_NUM_THREADS", "")
-    if omp.isdigit() and int(omp) > 0:
-        n = min(n, int(omp))
+    return {"affinity": aff, "cgroup_quota_cpus": cgroup_cpu_quota(),
+            "omp_num_threads": int(omp) if omp.isdigit() and int(omp) > 0 else None,
+            "os_cpu_count": os.cpu_count()}
+
+
+def host_threads() -> int:
+    """CPU threads the CPU baselines use: the CPUs this process may run on (its
+    affinity mask), capped by the cgroup's CPU quota (rounded up) and by
+    OMP_NUM_THREADS when the job sets them."""
+    import math
+    s = host_cpu_share()
+    n = s["affinity"]
+    if s["cgroup_quota_cpus"]:
+        n = min(n, max(1, math.ceil(s["cgroup_quota_cpus"])))
+    if s["omp_num_threads"]:
+        n = min(n, s["omp_num_threads"])
     return max(1, n)
 
 

@@ -2,7 +2,9 @@
 
 Under `torch.distributed.run` every local rank is a child of the same elastic
 agent, so (parent pid, MASTER_PORT, run id) names the job uniquely on the
-node. Rank 0 publishes the 128-byte ncclUniqueId through an atomically
+node. Every rank first publishes a join marker and waits, bounded, until all
+ranks have (join: no rank enters RCCL's bootstrap while a peer is missing).
+Rank 0 then publishes the 128-byte ncclUniqueId through an atomically
 renamed file in the temp dir; the other ranks poll for it. Everything after
 that (barriers, max-over-ranks timing) runs over RCCL itself, so the
 benchmark never loads a second HIP runtime (torch's) into the process.
@@ -14,6 +16,8 @@ import os
 import tempfile
 import time
 from pathlib import Path
+
+from ._lib import ECOMM, VptError
 
 
 def env_world() -> tuple[int, int, int]:
@@ -82,8 +86,59 @@ def exchange_unique_id(rank: int, make_uid, key: str | None = None,
     raise TimeoutError(f"rank {rank}: no unique id at {path} after {timeout_s}s")
 
 
-def cleanup(key: str | None = None) -> None:
+class RendezvousError(VptError):
+    """A peer rank never reached the rendezvous: raised before any RCCL call,
+    with the communicator error code (ECOMM), so callers handle it like a
+    failed communicator."""
+
+    def __init__(self, msg: str):
+        super().__init__(ECOMM, msg)
+
+
+def join_path(key: str, rank: int) -> Path:
+    return Path(tempfile.gettempdir()) / f"vptmcm-join-{key}-{rank}"
+
+
+def default_timeout_s() -> float:
+    """VPTMCM_COMM_TIMEOUT_MS (the library's communicator bound), default 120 s."""
     try:
-        uid_path(key or job_key()).unlink()
-    except FileNotFoundError:
-        pass
+        ms = int(os.environ.get("VPTMCM_COMM_TIMEOUT_MS", "120000"))
+    except ValueError:
+        ms = 120000
+    return (ms if ms > 0 else 120000) / 1e3
+
+
+def join(rank: int, world: int, key: str | None = None, timeout_s: float | None = None) -> None:
+    """All-ranks-present barrier ahead of RCCL: every rank publishes a join
+    marker, then waits until all `world` markers of this job key exist. RCCL's
+    bootstrap is entered only once every peer is known to be alive (a
+    communicator whose peer never arrives blocks inside RCCL's bootstrap, and
+    its abort can block too). A rank that does not arrive within
+    the bound ends every other rank here with RendezvousError (ECOMM)."""
+    key = key or job_key()
+    timeout_s = default_timeout_s() if timeout_s is None else timeout_s
+    mine = join_path(key, rank)
+    tmp = mine.with_name(mine.name + f".{os.getpid()}.tmp")
+    tmp.write_bytes(key.encode())
+    os.replace(tmp, mine)
+    deadline = time.monotonic() + timeout_s
+    missing = list(range(world))
+    while True:
+        missing = [r for r in missing if not join_path(key, r).exists()]
+        if not missing:
+            return
+        if time.monotonic() >= deadline:
+            raise RendezvousError(f"rendezvous: rank {rank} of {world}: rank(s) {missing} never joined "
+                                  f"within {timeout_s:g} s (job key {key}); no communicator was created")
+        time.sleep(0.01)
+
+
+def cleanup(key: str | None = None, world: int = 0) -> None:
+    """Remove the job's unique-id file and its join markers (rank 0, once every
+    rank has passed the communicator's first barrier)."""
+    key = key or job_key()
+    for p in [uid_path(key)] + [join_path(key, r) for r in range(world)]:
+        try:
+            p.unlink()
+        except FileNotFoundError:
+            pass
