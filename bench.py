@@ -251,7 +251,21 @@ def main():
         # a missing rank ends the job here with ECOMM)
         rendezvous.join(rank, world, key=key)
         uid = stdout_to_stderr(lambda: rendezvous.exchange_unique_id(rank, vptmcm.unique_id, key=key))
+        # RCCL's init cannot be bounded from inside the process (it does not
+        # return while a peer that joined and then died is missing): a
+        # watchdog ends the process instead, so the launcher tears the job down
+        import threading
+
+        def _init_hung():
+            sys.stderr.write(f"rank {rank}: RCCL communicator init did not return within "
+                             f"{rendezvous.default_timeout_s():g} s (a peer died after the rendezvous?)\n")
+            sys.stderr.flush()
+            os._exit(3)
+        dog = threading.Timer(rendezvous.default_timeout_s(), _init_hung)
+        dog.daemon = True
+        dog.start()
         stdout_to_stderr(lambda: r.comm_init(uid, world, rank))
+        dog.cancel()
         r.barrier()
         if rank == 0:
             rendezvous.cleanup(key, world)
@@ -278,6 +292,12 @@ def main():
         after the region's last pass (so every region ends with a composite
         the display could show). Returns the pass count of every march launch."""
         launches, done = [], 0
+        if not multi and F == 32:
+            # one call: the library launches it in 32-pass launches, the ones
+            # before the last balancing their tails across launch boundaries
+            # (DESIGN.md §5, cross-launch balancing); the last completes every tile
+            r.render_passes(mvp, seeds[first:first + count])
+            return [min(32, count - k) for k in range(0, count, 32)]
         while done < count:
             n = min(F, count - done)
             if multi:  # never fuse across a composite
@@ -312,10 +332,21 @@ def main():
 
     # ---- timed region: K passes (+ composites), bracketed by barrier + sync
     r.enable_kernel_timing(not a.no_timing)
+    stamps = os.environ.get("VPTMCM_BENCH_STAMPS")  # host clocks of the region (tools/wall_split.py)
+    if stamps:
+        clk = [(time.clock_gettime_ns(time.CLOCK_MONOTONIC), time.clock_gettime_ns(time.CLOCK_BOOTTIME))]
     t0 = time.perf_counter()
     launches = passes(1 + a.warmup, a.steps)
+    if stamps:
+        t_enq = time.perf_counter()
     r.synchronize()  # the march stream and (N > 1) the composite stream: the last all-reduce is done
     el = time.perf_counter() - t0
+    if stamps:
+        clk.append((time.clock_gettime_ns(time.CLOCK_MONOTONIC), time.clock_gettime_ns(time.CLOCK_BOOTTIME)))
+        Path(stamps).write_text(json.dumps({
+            "rank": rank, "t0_perf": t0, "t_enq_perf": t_enq, "t_end_perf": t0 + el, "el_s": el,
+            "monotonic_ns": [c[0] for c in clk], "boottime_ns": [c[1] for c in clk],
+            "launches": None}))
     if multi:
         # the composite is on every rank's device; reading it back to the host
         # is the display's cost, not the pass's (done outside the timed region)

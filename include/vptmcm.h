@@ -130,11 +130,12 @@ int vptmcm_set_volume(vptmcm* h, const uint8_t* voxels, uint32_t width,
 
 /* Block-wise volume ingest, mirroring WebGPUVolume.readModality's per-placement
  * writeTexture(origin=[x,y,z]) (WebGPUVolume.js:67-93): begin allocates the
- * volume (all zero, like a fresh texture), each block lands at its origin and
- * the cells / bricks it touches are re-laid out at once (they are resident in
- * HBM as soon as the placement arrives), end releases the staging copy. The
- * volume is renderable from begin on: blocks not yet written read as zero
- * density (the reference's renderers instead wait for Volume.ready). */
+ * volume (all zero, like a fresh texture), each block lands at its origin in
+ * HBM and the cells / bricks it touches are re-laid out before the next render
+ * reads them (placements arriving back to back are re-laid out together), end
+ * finishes the relayout and releases the staging copy. The volume is
+ * renderable from begin on: blocks not yet written read as zero density (the
+ * reference's renderers instead wait for Volume.ready). */
 int vptmcm_volume_begin(vptmcm* h, uint32_t width, uint32_t height, uint32_t depth);
 int vptmcm_volume_write_block(vptmcm* h, const uint8_t* data, uint32_t x, uint32_t y,
                               uint32_t z, uint32_t bw, uint32_t bh, uint32_t bd);
@@ -263,15 +264,17 @@ int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches);
 /* ncclGetUniqueId on rank 0; the caller ships the 128 bytes to other ranks. */
 int vptmcm_comm_unique_id(uint8_t* out /* 128 */);
 
-/* ncclCommInitRankConfig on the handle's device, run on a helper thread that
- * this call waits for at most VPTMCM_COMM_TIMEOUT_MS (environment, read here;
- * default 120000; an initialisation still blocked then — a peer that never
- * joined — is abandoned). Every later wait on the communicator (an RCCL
- * enqueue in progress, synchronize and the composite reads while RCCL work is
- * queued) polls ncclCommGetAsyncError under the same limit: on an
- * asynchronous error or the timeout the communicator is aborted
- * (ncclCommAbort, itself bounded to 2 s) and the call returns VPTMCM_ECOMM, so
- * a dead or hung peer ends every rank instead of hanging it. */
+/* ncclCommInitRank on the handle's device, in the calling thread. RCCL
+ * (2.27.7) does not return from it while its bootstrap waits for a rank that
+ * never arrives (a non-blocking config included), so the caller establishes
+ * that every rank is alive first (the torch-free rendezvous's join barrier,
+ * python/vptmcm/rendezvous.py, bounded by VPTMCM_COMM_TIMEOUT_MS). Every later
+ * wait on the communicator (an RCCL enqueue in progress, synchronize and the
+ * composite reads while RCCL work is queued) polls ncclCommGetAsyncError under
+ * VPTMCM_COMM_TIMEOUT_MS (environment, read here; default 120000): on an
+ * asynchronous error or the timeout the communicator is aborted and the call
+ * returns VPTMCM_ECOMM, so a rank that dies mid-run ends every rank instead of
+ * hanging it. A device-list handle (n_devices > 1) refuses (VPTMCM_ESTATE). */
 int vptmcm_comm_init(vptmcm* h, const uint8_t* unique_id, int nranks, int rank);
 
 /* Enqueue the cross-rank radiance composite of the current pass:
@@ -352,6 +355,13 @@ int vptmcm_debug_last_launch(vptmcm* h, uint32_t info[4], uint64_t* launches);
  * schedule (R <= 1024, not the raster variant) write it; a fresh handle reports
  * every slot idle. */
 int vptmcm_debug_schedule(vptmcm* h, uint32_t* out, uint32_t n_words, uint32_t* n_slots);
+
+/* Cross-launch balancing: per 8x8 tile (tile y/8 * ceil(R/8) +
+ * x/8) the passes it still owes after the launches so far, launching any
+ * queued render() passes first but NOT the owed ones (every other entry point
+ * runs every tile to the last queued pass first). *n_tiles receives the tile
+ * count; out (may be NULL) must hold n_words >= *n_tiles words. */
+int vptmcm_debug_owed(vptmcm* h, uint32_t* out, uint32_t n_words, uint32_t* n_tiles);
 
 /* Library version string. */
 const char* vptmcm_version(void);

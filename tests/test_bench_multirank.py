@@ -40,6 +40,8 @@ DRIVER = textwrap.dedent('''
         def set_params(self, **kw): pass
         def comm_init(self, uid, world, rank):
             LOG.append(["comm_init", bytes(uid).hex()[:16], world, rank])
+            if os.environ.get("FAKE_HANG_INIT") == os.environ["RANK"]:
+                time.sleep(3600)  # this rank's communicator init never returns
             os.write(1, ("RCCL version : (banner on fd 1, as RCCL writes it)" + chr(10)).encode())
             dist.init_process_group("gloo", rank=rank, world_size=world,
                                     timeout=__import__("datetime").timedelta(seconds=60))
@@ -136,7 +138,7 @@ def test_bench_rank_death_ends_the_job(tmp_path):
     others hanging: rank 0's next collective fails and bench.py exits non-zero
     within the timeout, printing no result line. (On the GPU the library's RCCL
     watchdog does the same: vptmcm_comm_* poll ncclCommGetAsyncError and abort
-    after VPTMCM_COMM_TIMEOUT_MS, test_comm_init_peer_never_joins.)"""
+    after VPTMCM_COMM_TIMEOUT_MS.)"""
     import time
     port = _free_port()
     argv = ["--gpus", "2", "--steps", "20", "--warmup", "5", "--volume", "16",
@@ -179,3 +181,30 @@ def test_bench_missing_rank_fails_in_the_rendezvous(tmp_path):
     assert "RCCL version" not in p.stderr  # the fake comm_init (and its banner) never ran
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert took < 60, took
+
+
+def test_bench_hung_comm_init_ends_every_rank(tmp_path):
+    """Both ranks pass the rendezvous, then rank 1's communicator init never
+    returns (a peer that dies inside RCCL's bootstrap): rank 0's init waits for
+    it and cannot be bounded from inside RCCL, so bench.py's init watchdog ends
+    each process with exit 3 after VPTMCM_COMM_TIMEOUT_MS."""
+    import time
+    port = _free_port()
+    argv = ["--gpus", "2", "--steps", "20", "--warmup", "5", "--volume", "16",
+            "--resolution", "16", "--cpu-seconds", "0"]
+    procs = []
+    t0 = time.monotonic()
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BENCH_ARGV=json.dumps(argv),
+                   BENCH_PATH=str(REPO / "bench.py"), LOG_OUT=str(tmp_path / f"log{rank}.json"),
+                   TORCHELASTIC_RUN_ID=f"h{port}", FAKE_HANG_INIT="1", VPTMCM_COMM_TIMEOUT_MS="4000")
+        procs.append(subprocess.Popen([sys.executable, "-c", DRIVER], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True, cwd=str(tmp_path)))
+    outs = [p.communicate(timeout=120) for p in procs]
+    took = time.monotonic() - t0
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 3, o + e
+        assert "did not return within 4 s" in e
+        assert not [ln for ln in o.splitlines() if ln.startswith("{")]
+    assert took < 90, took

@@ -453,29 +453,39 @@ def test_mode_b_gather_single_rank():
     gpu.close()
 
 
-def test_comm_init_peer_never_joins():
-    """The RCCL watchdog: a 2-rank communicator whose second rank never joins
-    fails with ECOMM after VPTMCM_COMM_TIMEOUT_MS instead of hanging; the
-    handle stays usable without a communicator."""
+def test_comm_peer_never_joins_fails_before_rccl():
+    """A two-rank job whose second rank never arrives: rank
+    0 fails in the all-ranks-present rendezvous with ECOMM after the bound,
+    before any RCCL call (RCCL 2.27.7's init cannot be bounded from outside:
+    it does not return while its bootstrap waits), so no RCCL
+    thread is started or left behind: the process's thread count is unchanged,
+    and the handle stays usable without a communicator."""
     import os
     import time
+
+    from vptmcm import rendezvous
+
+    def threads():
+        return len(os.listdir("/proc/self/task"))
+
     gpu, _ = make_pair(32, cf.sphere_in_cube(32), cf.tf_spectral())
-    os.environ["VPTMCM_COMM_TIMEOUT_MS"] = "3000"
-    try:
-        t0 = time.monotonic()
-        with pytest.raises(vptmcm.VptError, match="comm_init") as e:
-            gpu.comm_init(vptmcm.unique_id(), 2, 0)
-        took = time.monotonic() - t0
-    finally:
-        del os.environ["VPTMCM_COMM_TIMEOUT_MS"]
-    assert e.value.code == vptmcm.ECOMM and 2.5 < took < 60.0, (str(e.value), took)
-    print(f"comm_init failed after {took:.2f} s: {e.value}")
-    with pytest.raises(vptmcm.VptError, match="no communicator"):
-        gpu.barrier()
     mvp = cf.default_mvp_inverse()
     gpu.reset(mvp, 3)
+    gpu.synchronize()
+    before = threads()
+    key = f"never-joins-{os.getpid()}"
+    t0 = time.monotonic()
+    with pytest.raises(rendezvous.RendezvousError) as e:
+        rendezvous.join(0, 2, key=key, timeout_s=3.0)
+    took = time.monotonic() - t0
+    rendezvous.cleanup(key, 2)
+    assert e.value.code == vptmcm.ECOMM and 3.0 <= took < 30.0, (str(e.value), took)
+    assert threads() == before, (before, threads())
+    with pytest.raises(vptmcm.VptError, match="no communicator"):
+        gpu.barrier()
     gpu.render_passes(mvp, cf.seed_stream(2))
     gpu.synchronize()
+    assert threads() == before
     gpu.close()
 
 
@@ -942,4 +952,93 @@ def test_c3_driver_shaped_launch_bitexact():
     assert_photons_equal(gpu.read_photons(), cpu.photons, "C3 20-pass launch")
     assert_rgb32_equal(gpu.read_rgb(), rgb, "C3 20-pass launch")
     assert_rgba_equal(gpu.read_rgba16f(), want, "C3 20-pass launch")
+    gpu.close()
+
+
+def test_carry_owed_passes_bitexact_c3():
+    """Cross-launch balancing on C3 itself (512^3, R = 512): render() calls queue
+    32-pass launches that may end early, volume waves stopping at a pass
+    boundary once the lone SIMDs' waves reach the target and owing the rest;
+    the next launch deals the owing tiles first. After two full queues some
+    tiles owe passes (at most 32, a pass window); a read then runs every tile
+    to the last queued pass, and photons, fp32 and rgba16f images are bit-exact
+    against 72 oracle passes. render_passes(72) in one call (the bench's
+    region shape) is bit-exact too."""
+    R = 512
+    vol, tf, mvp = cf.fbm_volume(512, 512, nthreads=8), cf.tf_spectral(), cf.default_mvp_inverse()
+    gpu, cpu = make_pair(R, vol, tf, ext=32.0)
+    seeds = cf.seed_stream(73, start=0)
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0], nthreads=16)
+    for s in seeds[1:66]:
+        gpu.render(mvp, s)
+    owed = gpu.debug_owed()  # launches the 65th pass too, keeping what is owed
+    assert owed.max() <= 32 and (owed > 0).sum() > 100, (owed.max(), (owed > 0).sum())
+    for s in seeds[66:]:
+        gpu.render(mvp, s)
+    for s in seeds[1:]:
+        rgb, want = cpu.render(mvp, s, nthreads=16)
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "carry, 72 render() calls")
+    assert_rgb32_equal(gpu.read_rgb(), rgb, "carry, 72 render() calls")
+    assert_rgba_equal(gpu.read_rgba16f(), want, "carry, 72 render() calls")
+    assert (gpu.debug_owed() == 0).all()
+    gpu.reset(mvp, seeds[0])
+    gpu.render_passes(mvp, seeds[1:])
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "carry, render_passes(72)")
+    assert_rgba_equal(gpu.read_rgba16f(), want, "carry, render_passes(72)")
+    gpu.close()
+
+
+@pytest.mark.parametrize("layout", [vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_BRICK8])
+def test_carry_matrix_change_and_inputs_complete_owed_passes(layout):
+    """Owed passes run with their own matrix: a render() with another camera
+    first completes them (oracle: the same passes in order, old camera then
+    new); an input change (set_params) completes them with the old inputs; the
+    UI-like TF with uneven bins (MODE 6) carries too."""
+    R = 128
+    vol, mvp1, mvp2 = cf.fbm_volume(96, 17, nthreads=8), cf.golden_mvp("orbit"), cf.default_mvp_inverse()
+    for tf, spec in ((cf.tf_spectral(), "12"), (cf.tf_materials(True), "8_uneven")):
+        gpu, cpu = make_pair(R, vol, tf, spec=spec, ext=24.0, layout=layout)
+        seeds = cf.seed_stream(120, start=5)
+        gpu.reset(mvp1, seeds[0])
+        cpu.reset(mvp1, seeds[0], nthreads=16)
+        k = 1
+        for _ in range(40):  # one full queue with camera 1 (flushed with carry), 8 queued
+            gpu.render(mvp1, seeds[k])
+            cpu.render(mvp1, seeds[k], nthreads=16)
+            k += 1
+        owed = gpu.debug_owed()
+        assert owed.max() <= 32
+        for _ in range(40):  # camera 2: the owed camera-1 passes complete first
+            gpu.render(mvp2, seeds[k])
+            cpu.render(mvp2, seeds[k], nthreads=16)
+            k += 1
+        gpu.debug_owed()
+        gpu.set_params(extinction=12.0, bounces=8, steps=8)  # completes with extinction 24
+        cpu.params.update(extinction=12.0)
+        for _ in range(36):
+            gpu.render(mvp2, seeds[k])
+            rgb, want = cpu.render(mvp2, seeds[k], nthreads=16)
+            k += 1
+        assert_photons_equal(gpu.read_photons(), cpu.photons, f"carry, camera change, {spec}")
+        assert_rgba_equal(gpu.read_rgba16f(), want, f"carry, camera change, {spec}")
+        assert_rgb32_equal(gpu.read_rgb(), rgb, f"carry, camera change, {spec}")
+        gpu.close()
+
+
+def test_carry_off_matches(monkeypatch):
+    """VPTMCM_CARRY=0 (no early stops): the same bits, and nothing is ever owed."""
+    monkeypatch.setenv("VPTMCM_CARRY", "0")
+    R = 128
+    gpu, cpu = make_pair(R, cf.fbm_volume(96, 18, nthreads=8), cf.tf_spectral(), ext=24.0)
+    mvp = cf.default_mvp_inverse()
+    seeds = cf.seed_stream(70, start=9)
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0], nthreads=16)
+    for s in seeds[1:]:
+        gpu.render(mvp, s)
+        rgb, want = cpu.render(mvp, s, nthreads=16)
+    assert (gpu.debug_owed() == 0).all()
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "carry off")
+    assert_rgba_equal(gpu.read_rgba16f(), want, "carry off")
     gpu.close()

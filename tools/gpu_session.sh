@@ -59,6 +59,13 @@ for s in $STEPS; do
       NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,BOOTSTRAP timeout -k 10 90 tools/comm_diag $m > $OUT/comm_diag_$m.log 2>&1
       rc=$?; echo "commdiag $m rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
     done ;;
+  carryab)  # cross-launch balancing A/B on the default 1024-pass line (alternating, one box)
+    for c in 0 1 0 1; do
+      VPTMCM_CARRY=$c timeout -k 10 300 python bench.py --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 256 --unfused-steps 0 > $OUT/carry_$c.json 2>> $OUT/carry.err
+      rc=$?; [ $rc -ne 0 ] && { echo "carryab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      python3 -c "import json; d=json.load(open('$OUT/carry_$c.json')); print(json.dumps({'carry': $c, 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'render_api': d['render_api']['value']}))" >> $OUT/carryab.jsonl
+    done
+    echo "carryab rc=0" | tee -a $OUT/status.txt; cat $OUT/carryab.jsonl ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)

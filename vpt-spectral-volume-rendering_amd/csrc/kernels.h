@@ -35,18 +35,34 @@ struct TileSched {
   // launch (tile | flag << 31, 0xffffffff idle): a hot wave starts loading that
   // tile's photon state before its own schedule ends, and reloads on a change
   uint32_t* prev;
+  // Cross-launch balancing (MarchParams::carry): per tile the absolute index of
+  // its next pass; the completion counters of the early stop (this launch's,
+  // and the next launch's, which this launch zeroes).
+  uint32_t* tile_next;
+  uint32_t* stop_ctr;
+  uint32_t* stop_ctr_next;
 };
+// Flag byte of a tile (written by each launch for the next one's schedule):
+// bit 0 its wave entered the volume, bits 1-2 its lag bucket (passes it still
+// owes after the launch: 0, 1-3, 4-7, >= 8).
+constexpr uint32_t kFlagVolume = 1u, kLagShift = 1u;
 constexpr uint32_t kSchedChunk = 4 * kMarchBlock;  // tiles scanned per block-wide round
 constexpr uint32_t kSchedMaxTiles = 16384;         // larger frames use the raster mapping
 // Seeds of the passes one march launch runs back to back (render_passes): the
 // photon state stays in registers between them; every pass reseeds the RNG
-// from its own seed (wgsl:122) and stores its full image.
+// from its own seed (wgsl:122). A launch queues n <= kMaxFusedPasses new
+// passes; its window holds the seeds of the last kSeedWindow passes queued
+// since create (absolute pass indices [base, base + kSeedWindow), the launch's
+// target is base + kSeedWindow), so a tile that owes passes of earlier
+// launches (MarchParams::carry) finds their seeds too.
 constexpr uint32_t kMaxFusedPasses = 32;
+constexpr uint32_t kSeedWindow = 64;
 struct PassSeeds {
   uint32_t n;
-  uint32_t seed[kMaxFusedPasses];
+  uint32_t base;
+  uint32_t seed[kSeedWindow];
 };
-static_assert(offsetof(PassSeeds, seed) == 4, "pass_seed() reads seed[] at kernarg byte 4");
+static_assert(offsetof(PassSeeds, seed) == 8, "pass_seed() reads seed[] at kernarg byte 8");
 // k_march(PassSeeds, MarchParams, ...): MarchParams starts right after PassSeeds
 static_assert(sizeof(PassSeeds) % alignof(MarchParams) == 0, "MarchParams kernarg offset");
 static_assert(offsetof(MarchParams, yb) == offsetof(MarchParams, xb) + 4 * kMaxBins &&

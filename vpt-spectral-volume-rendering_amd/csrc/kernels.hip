@@ -250,8 +250,95 @@ __device__ __forceinline__ uint32_t wave_scan_small(uint32_t c, uint32_t& total)
 __device__ __forceinline__ uint32_t sched_flags_first(const uint8_t* __restrict__ flags) {
   return reinterpret_cast<const uint32_t*>(flags)[threadIdx.x];
 }
+// Deal one tile to a wave slot (see schedule_tile): the Latin square of the
+// slot's group, for the hardware block lb that owns the slot.
+__device__ __forceinline__ void deal_slot(uint32_t slot, uint32_t G, uint32_t lb, uint32_t packed,
+                                          uint32_t* s_tile) {
+  const uint32_t k = slot / (4u * G), rem = slot - k * 4u * G;
+  if ((rem >> 2) == lb) {
+    const uint32_t j = rem & 3u;
+    s_tile[4u * j + ((k + j) & 3u)] = packed;
+  }
+}
+
+// Cross-launch balancing (MarchParams::lag_sched, one chunk of tiles): the
+// volume tiles in four classes by the passes they still owe (most first, raster
+// order inside a class), then dealt so that the most owing ones get the lone
+// SIMD slots (the group-0 slots of the blocks whose group-1 slots are
+// background: slots [P, 4G) for P = nv - 4G pairs), the next ones the paired
+// group-0 slots, the least owing ones group 1. A SIMD with a single volume
+// wave then has work for the whole launch, and in a pair the owing wave leads
+// (it also takes the higher issue priority). Returns the slot's packed tile
+// (tile | volume << 31 | lag bucket << 29) and the launch's stop quota in *q
+// (the lone slot count, 0 without pairs).
+__device__ uint32_t schedule_tile_lag(uint32_t n, uint32_t f, uint32_t lb, uint32_t* s_red,
+                                      uint32_t* s_tile, uint32_t* q) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6, G = gridDim.x;
+  uint32_t cc = 0u;  // per class (k = 3 - bucket) the lane's count, 4 bits each
+#pragma unroll
+  for (uint32_t b = 0; b < 4u; b++) {
+    const uint32_t fb = (f >> (8u * b)) & 0xffu;
+    if (fb & kFlagVolume) cc += 1u << (4u * (3u - ((fb >> kLagShift) & 3u)));
+  }
+  uint32_t pre[4], wt[4];
+#pragma unroll
+  for (uint32_t k = 0; k < 4u; k++) pre[k] = wave_scan_small((cc >> (4u * k)) & 0xfu, wt[k]);
+  if (lane == 0u) {
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) s_red[4u * w + k] = wt[k];
+  }
+  __syncthreads();
+  uint32_t before[4] = {0u, 0u, 0u, 0u}, tot[4] = {0u, 0u, 0u, 0u};
+  for (uint32_t v = 0; v < 16u; v++) {
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) {
+      const uint32_t t = s_red[4u * v + k];
+      before[k] += (v < w) ? t : 0u;
+      tot[k] += t;
+    }
+  }
+  const uint32_t nv = tot[0] + tot[1] + tot[2] + tot[3];
+  const uint32_t pairs = nv > 4u * G ? nv - 4u * G : 0u, lone = 4u * G - pairs;
+  const bool remap = pairs > 0u && (tot[0] + tot[1] + tot[2]) > 0u;
+  if (q) *q = pairs > 0u ? lone : 0u;
+  // running rank inside each class, and the volume tiles before this lane's four
+  uint32_t seen[4];
+  uint32_t ones = 0u;
+#pragma unroll
+  for (uint32_t k = 0; k < 4u; k++) {
+    seen[k] = before[k] + pre[k];
+    ones += seen[k];
+  }
+  const uint32_t base1 = tot[0], base2 = tot[0] + tot[1], base3 = base2 + tot[2];
+#pragma unroll
+  for (uint32_t b = 0; b < 4u; b++) {
+    const uint32_t t = 4u * tid + b;
+    const uint32_t fb = (f >> (8u * b)) & 0xffu;
+    const uint32_t vol = fb & kFlagVolume, bucket = (fb >> kLagShift) & 3u, k = 3u - bucket;
+    if (t < n) {
+      uint32_t slot;
+      if (vol) {
+        const uint32_t r = (k == 0u ? seen[0] : k == 1u ? base1 + seen[1] : k == 2u ? base2 + seen[2]
+                                                                               : base3 + seen[3]);
+        slot = !remap ? r : (r < lone ? pairs + r : (r < 4u * G ? r - lone : r));
+      } else {
+        slot = nv + (t - ones);
+      }
+      deal_slot(slot, G, lb, t | (vol << 31) | (bucket << 29), s_tile);
+    }
+    if (vol) {
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; j++) seen[j] += (j == k) ? 1u : 0u;
+      ones++;
+    }
+  }
+  __syncthreads();  // s_tile complete
+  return s_tile[w];
+}
+
+template <bool LAG = false>
 __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8_t* __restrict__ flags,
-                                  uint32_t* s_red, uint32_t* s_tile) {
+                                  uint32_t* s_red, uint32_t* s_tile, uint32_t* stop_q = nullptr) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
   const uint32_t n = P.n_tiles, G = gridDim.x;
   // Consecutive slots go to consecutive hardware blocks, i.e. round-robin over
@@ -260,15 +347,16 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
   // a fully paired XCD runs its pairs ~4 % slower.
   // sched 2 keeps round 2's XCD-by-XCD order (the XCD-swizzled block).
   const uint32_t lb = P.sched == 2u ? xcd_swizzle(blockIdx.x, G) : blockIdx.x;
-  const uint32_t* f4 = reinterpret_cast<const uint32_t*>(flags);  // 0/1 bytes, padded to kSchedChunk
+  const uint32_t* f4 = reinterpret_cast<const uint32_t*>(flags);  // flag bytes, padded to kSchedChunk
   if (tid < 16u) s_tile[tid] = 0xffffffffu;  // idle unless a tile is dealt to it
+  if (LAG && P.lag_sched && n <= kSchedChunk) return schedule_tile_lag(n, f0, lb, s_red, s_tile, stop_q);
   uint32_t nv = 0u;  // number of volume tiles; one chunk (R <= 512): the scan's total
   if (n > kSchedChunk) {
     if (tid == 0u) s_red[16] = 0u;
     __syncthreads();
     uint32_t mine = 0u;
     for (uint32_t base = 0; base < n; base += kSchedChunk)
-      mine += __popc(f4[(base >> 2) + tid] & 0x01010101u);
+      mine += __popc(f4[(base >> 2) + tid] & 0x01010101u);  // the volume bits
     mine = wave_sum(mine);
     if (lane == 0u) atomicAdd(&s_red[16], mine);
     __syncthreads();
@@ -331,9 +419,9 @@ __device__ __forceinline__ void stage_lds_16(uint4* dst, const uint4* __restrict
 // from the kernarg segment (one scalar load per pass) instead of keeping all
 // kMaxFusedPasses seeds live in SGPRs.
 typedef const __attribute__((address_space(4))) uint32_t* karg_u32;
-__device__ __forceinline__ uint32_t pass_seed(uint32_t pass) {
+__device__ __forceinline__ uint32_t pass_seed(uint32_t widx) {  // widx: index in the seed window
   karg_u32 k = (karg_u32)__builtin_amdgcn_kernarg_segment_ptr();
-  return k[1u + pass];  // offsetof(PassSeeds, seed) == 4
+  return k[2u + widx];  // offsetof(PassSeeds, seed) == 8
 }
 // The CMF bin means of MarchParams (the second kernel argument), re-read from
 // the kernarg segment at every pass's radiance_to_rgb through a pointer the
@@ -357,7 +445,10 @@ __device__ __forceinline__ const __attribute__((address_space(4))) float* cmf_ta
 // 5: MODE 2's geometry and light with any bin layout and a TF of more than
 // kTfRowsMax distinct rows (u16 LDS TF; anisotropy from the row table or the
 // tf_b4 gather).
-template <uint32_t L, bool SPEC, uint32_t MODE>
+// CARRY: cross-launch balancing (MarchParams::carry; the per-tile pass window,
+// the early stop and the owing waves' priority); without it the kernel is the
+// plain n-pass launch.
+template <uint32_t L, bool SPEC, uint32_t MODE, bool CARRY>
 __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const MarchParams P,
                                                        const TileSched T, float* __restrict__ ph,
                                                        const uint8_t* __restrict__ vol,
@@ -386,7 +477,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __shared__ uint32_t s_rowmap[256];  // P.tf_dedup: density row -> first texel of its distinct row
   __shared__ uint32_t s_binlut[LUTB ? kBinLutCells + kBinLutCells / 4 : 1];  // MODE 6 / 7
 
-  __shared__ uint32_t s_red[17];
+  __shared__ uint32_t s_red[64];
   __shared__ uint32_t s_tile[16];
 
   TL_DECL();
@@ -426,10 +517,14 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   uint32_t tile;
   bool hot0;  // the tile entered the volume last launch (its wave is a long one)
   bool have = false;  // p already holds this tile's state (the slot's tile did not change)
+  bool owing = false;  // the tile owes passes of earlier launches (lag bucket > 0)
+  uint32_t stop_q = 0u;
+  if (CARRY && blockIdx.x == 0u && threadIdx.x == 0u) *T.stop_ctr_next = 0u;  // the next launch's counter
   if (P.sched != 1u) {
-    const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile(P, f0, T.flags_in, s_red, s_tile));
-    tile = s == 0xffffffffu ? s : s & 0x7fffffffu;
+    const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile<CARRY>(P, f0, T.flags_in, s_red, s_tile, &stop_q));
+    tile = s == 0xffffffffu ? s : s & 0x1fffffffu;
     hot0 = s != 0xffffffffu && (s >> 31) != 0u;
+    owing = CARRY && s != 0xffffffffu && ((s >> 29) & 3u) != 0u;
     have = hot0 && s == prev;
     if (lane == 0u && s != prev) T.prev[blockIdx.x * 16u + (threadIdx.x >> 6)] = s;
   } else {  // raster: the block's 16 consecutive tiles
@@ -438,6 +533,18 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     hot0 = true;
   }
   TL_MARK(1);
+  if (CARRY) stop_q = __builtin_amdgcn_readfirstlane(P.stop_q ? P.stop_q : stop_q);
+  // The tile's passes: from its own next pass (carry) or the launch's n new
+  // ones, up to the window's end (target); todo <= kSeedWindow always holds
+  // for a tile of this handle (the host keeps every tile within the window).
+  uint32_t todo = PS.n;
+  if (CARRY && tile < P.n_tiles) {
+    const auto tn = (const __attribute__((address_space(4))) uint32_t*)T.tile_next;  // scalar load
+    const uint32_t owed = PS.base + kSeedWindow - tn[tile];
+    todo = owed <= kSeedWindow ? owed : PS.n;
+  }
+  todo = __builtin_amdgcn_readfirstlane(todo);
+  const uint32_t first = kSeedWindow - todo;  // window index of the tile's first pass
   const uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
   const uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
   const size_t i = (size_t)tile * 64u + lane;
@@ -484,8 +591,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __syncthreads();
   if (live && !hot0) load_photon(ph, S, i, p);
   TL_MARK_WAIT(2);
-  if (!live) {
-    if (tile < P.n_tiles && lane == 0u) T.flags_out[tile] = 0u;  // an idle out-of-band tile
+  if (!live || todo == 0u) {
+    // an idle out-of-band tile; or a tile with no pass owed (a completion
+    // launch): its flag carries over
+    if (tile < P.n_tiles && lane == 0u) T.flags_out[tile] = (live && hot0) ? kFlagVolume : 0u;
     return;
   }
   const uint16_t* s_tf = reinterpret_cast<const uint16_t*>(s_tf4);
@@ -563,15 +672,32 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     p.bin = rc.bin;
     rb = rbpix;
   };
-  const uint32_t n_passes = PS.n;
+  const uint32_t n_passes = todo;
+  // early stop (MarchParams::allow_stop): a volume wave ends the launch at a
+  // pass boundary once stop_q volume waves have reached the target; the
+  // counter is read one pass ahead (lane 0, coherent across the XCDs) so its
+  // latency hides in the pass
+  const bool stop_ok = CARRY && P.allow_stop && hot0 && stop_q != 0u;
+  uint32_t ctr_v = 0u, done_passes = n_passes;
   for (uint32_t pass = 0; pass < n_passes; pass++) {
+  if (stop_ok) {
+    if (pass > 0u && __builtin_amdgcn_readfirstlane(ctr_v) >= stop_q && n_passes - pass <= kMaxFusedPasses) {
+      done_passes = pass;  // the pending sample is applied after the loop
+      break;
+    }
+    if (lane == 0u) ctr_v = __hip_atomic_load(T.stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 #if VPT_PRIO
   if (pass > 0u) hot = entered;
-  if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) __builtin_amdgcn_s_setprio(VPT_PRIO);
-  else __builtin_amdgcn_s_setprio(0);
+  if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) {
+    if (CARRY && owing) __builtin_amdgcn_s_setprio(VPT_PRIO + 1);  // the owing wave of a pair leads
+    else __builtin_amdgcn_s_setprio(VPT_PRIO);
+  } else {
+    __builtin_amdgcn_s_setprio(0);
+  }
   entered = false;
 #endif
-  uint32_t st = hash3(x, y, pass_seed(pass));  // wgsl:122 (state is not carried across passes)
+  uint32_t st = hash3(x, y, pass_seed(first + pass));  // wgsl:122 (state is not carried across passes)
 
   if constexpr (SPEC) {
     for (uint32_t step = 0; step < P.steps; step++) {
@@ -813,6 +939,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   }
   }  // pass
   TL_MARK(3);
+  if (CARRY && done_passes != n_passes) apply_pending();  // an early stop (the last pass applies its own)
 
   if (stale) p.pos = ray_start(from, p.dir);  // the last robust reset's start point
   store_state(ph, S, i, p);  // uPhotons[globalIndex] = p (wgsl:165), once per launch
@@ -820,7 +947,13 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   for (int b = 0; b < kMaxBins; b++)
     if (NBF || !VPT_NB_ZERO || (uint32_t)b < P.nb) ph[(kRad0 + b) * S + i] = p.rad[b];
 
-  if (lane == 0u) T.flags_out[tile] = entered ? 1u : 0u;  // the next pass's schedule
+  if (lane == 0u) {  // the next launch's schedule: volume flag and lag bucket
+    const uint32_t owe = n_passes - done_passes;
+    const uint32_t bucket = owe == 0u ? 0u : owe < 4u ? 1u : owe < 8u ? 2u : 3u;
+    T.flags_out[tile] = (entered ? kFlagVolume : 0u) | (bucket << kLagShift);
+    if (CARRY) T.tile_next[tile] = PS.base + first + done_passes;
+    if (stop_ok && owe == 0u) __hip_atomic_fetch_add(T.stop_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   STAMP_END(rgb32, tile, entered);
   TL_END(rgb32, tile, entered);
 }
@@ -890,7 +1023,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
                                                            uint16_t* __restrict__ rgba,
                                                            float* __restrict__ rgb32) {
   __shared__ float4 s_tf[kRgbTfMax];
-  __shared__ uint32_t s_red[17];
+  __shared__ uint32_t s_red[64];
   __shared__ uint32_t s_tile[16];
   // the SIMD-balanced tile schedule and volume-wave priority of k_march
   uint32_t tile;
@@ -950,7 +1083,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
     if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) __builtin_amdgcn_s_setprio(VPT_PRIO);
     else __builtin_amdgcn_s_setprio(0);
     entered = false;
-    uint32_t st = hash3(x, y, pass_seed(pass));  // MCMComputeRenderer.wgsl:112
+    uint32_t st = hash3(x, y, pass_seed(kSeedWindow - PS.n + pass));  // MCMComputeRenderer.wgsl:112
     for (uint32_t step = 0; step < P.steps; step++) {
       if (__builtin_amdgcn_ballot_w64(!rb) == 0ull) {
         // robust path: the exit and the reset of wgsl:126-139 without the
@@ -1255,9 +1388,14 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   if (info) *info = MarchLaunchInfo{mode, tpl, spec ? 1u : 0u, PS.n};
   // hipExtLaunchKernelGGL stamps the events from the dispatch packet itself
   // (no extra barrier/marker packets between back-to-back launches)
-#define VPT_LAUNCH(LAY, SP, MO)                                                                \
-  hipExtLaunchKernelGGL((k_march<LAY, SP, MO>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
+#define VPT_LAUNCH_C(LAY, SP, MO, CA)                                                              \
+  hipExtLaunchKernelGGL((k_march<LAY, SP, MO, CA>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
                         PS, Q, T, ph, vol, tf_lds, tf_b4, tf_brow, light, rgba, rgb32, rowmap, bin_lut)
+#define VPT_LAUNCH(LAY, SP, MO)                                   \
+  do {                                                            \
+    if (SP && Q.carry) VPT_LAUNCH_C(LAY, SP, MO, SP);             \
+    else VPT_LAUNCH_C(LAY, SP, MO, false);                        \
+  } while (0)
 #define VPT_LAUNCH_NB(LAY)                 \
   do {                                     \
     switch (spec ? mode : 8u + mode) {     \
@@ -1282,6 +1420,7 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   }
 #undef VPT_LAUNCH_NB
 #undef VPT_LAUNCH
+#undef VPT_LAUNCH_C
   return hipGetLastError();
 }
 

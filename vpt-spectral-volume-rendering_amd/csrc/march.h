@@ -105,6 +105,13 @@ struct MarchParams {
   // host-built and exact (kBinLutCells u32 thresholds, then as many bytes of
   // base | count << 4). Set when no cell holds two distinct thresholds.
   uint32_t bins_lut;
+  // Cross-launch balancing (vptmcm.cpp, "carry"): each tile runs from its own
+  // next pass (TileSched::tile_next) to the launch's target; with allow_stop a
+  // volume wave may end its launch at a pass boundary once stop_q volume waves
+  // (0: the lone SIMD slots of the deal) have reached the target, owing the
+  // rest to the next launch; lag_sched deals the owing tiles first (the
+  // previous launch allowed stops).
+  uint32_t carry, allow_stop, stop_q, lag_sched;
 };
 constexpr uint32_t kBinLutCells = 1024u;
 constexpr uint32_t kBinLutShift = 22u;

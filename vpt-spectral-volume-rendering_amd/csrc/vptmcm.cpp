@@ -55,6 +55,11 @@ struct vptmcm {
   uint32_t W = 0, H = 0, D = 0;
   bool volume_ready = false;   // renderable: from volume_begin on (unwritten blocks read zero)
   bool vol_done = false;       // LINEAR after volume_end (its staging copy is the volume)
+  // CORNER8 / BRICK8 cells [vol_c0, vol_c1) whose blocks arrived since the last
+  // relayout: re-laid out in one launch before the next march reads the cells
+  // (or at volume_end), so a slice-by-slice ingest relays each cell once
+  bool vol_dirty = false;
+  uint32_t vol_c0[3] = {0, 0, 0}, vol_c1[3] = {0, 0, 0};
   uint16_t* tf_rg = nullptr;   // 65536 (albedo | alpha << 8) texels
   uint32_t* tf_b4 = nullptr;   // 257*257 anisotropy corner cells
   uint8_t* tf_brow = nullptr;  // 256 anisotropy rows (valid when b_rows)
@@ -72,6 +77,24 @@ struct vptmcm {
   uint8_t* sched = nullptr;    // tile schedule flags: [2][sched_flag_bytes(n_tiles)]
   uint32_t* sched_prev = nullptr;  // each wave slot's last scheduled tile (TileSched::prev)
   uint32_t sched_cur = 0;      // which flag row the next march reads
+  // Cross-launch balancing ("carry", MarchParams::carry): a
+  // launch queued while more passes follow may end when the lone SIMDs' waves
+  // reach its target, the other volume waves stopping at a pass boundary and
+  // owing the rest (per tile: tile_next, the absolute index of its next pass);
+  // the next launch deals the owing tiles first and runs each tile from its
+  // own next pass. Every photon's passes and seeds are unchanged, so the bits
+  // are; any observation or input change first runs every tile to the last
+  // queued pass (flush_renders).
+  bool carry_on = false;       // spectral, one schedule chunk, not disabled (VPTMCM_CARRY=0)
+  bool carry_pending = false;  // a launch with early stops ran since all tiles were complete
+  bool tile_next_stale = false;  // tile_next lags the launches (every tile is at pass_target)
+  float carry_mvp[16] = {};    // the matrix of the owed passes
+  uint32_t* tile_next = nullptr;
+  uint32_t* stop_ctr = nullptr;  // two completion counters, alternating per launch
+  uint32_t ctr_parity = 0;
+  uint32_t stop_q = 0;         // VPTMCM_STOP_Q: the early-stop quota (0: the lone SIMD slots)
+  uint32_t pass_target = 0;    // absolute index of the next pass to queue
+  uint32_t seed_ring[kSeedWindow] = {};  // seeds of the last kSeedWindow passes queued
 
   float spectrum[VPTMCM_SPECTRUM_FLOATS] = {};
   uint8_t light_host[256];
@@ -111,6 +134,7 @@ struct vptmcm {
   // call returns VPTMCM_ECOMM, so a dead or hung peer ends the job instead of
   // hanging every rank.
   int64_t comm_timeout_ms = 120000;
+  bool comm_failed = false;  // the communicator was aborted (comm_fail): waits stay bounded
   uint32_t* band_cover = nullptr;  // Mode B: one counter per 8-row tile, all-reduced
   hipStream_t comm_stream = nullptr;
   float4* comp[2] = {nullptr, nullptr};
@@ -468,21 +492,55 @@ int time_close(vptmcm* h) {
   return VPTMCM_OK;
 }
 
-// One march launch running n <= kMaxFusedPasses passes back to back.
-int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
+// Re-lay out the cells of the blocks that arrived since the last relayout
+// (vptmcm::vol_dirty) from the staging copy, on the handle's stream.
+int flush_relayout(vptmcm* h) {
+  if (!h->vol_dirty) return VPTMCM_OK;
+  h->vol_dirty = false;
+  const bool brick = h->layout == kLayoutBrick8;
+  const uint32_t n[3] = {h->vol_c1[0] - h->vol_c0[0], h->vol_c1[1] - h->vol_c0[1], h->vol_c1[2] - h->vol_c0[2]};
+  HIPCHK(h, launch_corner8(h->vol_lin, h->W, h->H, h->D, brick ? (h->W + kBrickCells) / kBrickCells : 0u,
+                           brick ? (h->H + kBrickCells) / kBrickCells : 0u, h->vol_c8, h->stream,
+                           h->vol_c0, n));
+  return VPTMCM_OK;
+}
+
+// One march launch queueing n <= kMaxFusedPasses new passes (seeds) with
+// matrix mvp. allow_stop: more passes follow, so volume waves may stop early
+// and owe passes to the next launch (carry); otherwise every tile reaches the
+// new target. A launch with another matrix first completes the owed passes
+// with theirs.
+int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n, bool allow_stop = false) {
   if (!h->volume_ready) FAIL(h, VPTMCM_ESTATE, "render: no volume set (setVolume first)");
-  MarchParams P = make_params(h, mvp, seeds[0]);
+  if (h->carry_pending && memcmp(mvp, h->carry_mvp, sizeof h->carry_mvp) != 0) {
+    if (int rc = do_march(h, h->carry_mvp, nullptr, 0, false)) return rc;
+  }
+  if (int rc = flush_relayout(h)) return rc;
+  MarchParams P = make_params(h, mvp, n ? seeds[0] : 0u);
+  const bool carry = h->carry_on && (allow_stop || h->carry_pending);
+  if (carry && h->tile_next_stale) {  // every tile is at the last target: the one this launch starts from
+    HIPCHK(h, hipMemsetD32Async(h->tile_next, (int)h->pass_target, h->n_tiles, h->stream));
+    h->tile_next_stale = false;
+  }
+  for (uint32_t k = 0; k < n; k++) h->seed_ring[(h->pass_target + k) % kSeedWindow] = seeds[k];
+  h->pass_target += n;
   PassSeeds PS;
   memset(&PS, 0, sizeof PS);
   PS.n = n;
-  memcpy(PS.seed, seeds, n * sizeof(uint32_t));
+  PS.base = h->pass_target - kSeedWindow;
+  for (uint32_t k = 0; k < kSeedWindow; k++) PS.seed[k] = h->seed_ring[(PS.base + k) % kSeedWindow];
+  P.carry = carry ? 1u : 0u;
+  P.allow_stop = (carry && allow_stop) ? 1u : 0u;
+  P.lag_sched = (carry && h->carry_pending) ? 1u : 0u;
+  P.stop_q = h->stop_q;
   hipEvent_t eb = nullptr, ee = nullptr;
   int rc = time_slot(h, &eb);
   if (rc) return rc;
   if (h->timing && h->time_stop) ee = h->region.end;
   const uint8_t* vol = h->layout != kLayoutLinear ? (const uint8_t*)h->vol_c8 : h->vol_lin;
   const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
-  TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev};
+  TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev, h->tile_next,
+              h->stop_ctr + h->ctr_parity, h->stop_ctr + (h->ctr_parity ^ 1u)};
   // variant bit 1: raster mapping; bit 7: round 2's XCD-by-XCD slot order
   P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : (h->variant & 128u) ? 2u : 0u;
   if (h->kind == VPTMCM_RENDERER_RGB)
@@ -495,16 +553,24 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   h->march_launches++;
   h->sched_cur = c ^ 1u;
   h->grp_dirty = true;
+  if (carry) h->ctr_parity ^= 1u;
+  else h->tile_next_stale = true;
+  h->carry_pending = P.allow_stop != 0u;
+  if (h->carry_pending) memcpy(h->carry_mvp, mvp, sizeof h->carry_mvp);
   return VPTMCM_OK;
 }
 
-// Launch the queued render() passes (see vptmcm::pend_n).
-int flush_renders(vptmcm* h) {
-  if (h->pend_n == 0) return VPTMCM_OK;
+// Launch the queued render() passes (see vptmcm::pend_n). keep_lag: more
+// passes follow (the queue is full), so the launch may leave owed passes;
+// otherwise (an observation, an input change, another matrix) every tile is
+// run to the last queued pass, with a completion launch if nothing is queued.
+int flush_renders(vptmcm* h, bool keep_lag = false) {
+  if (h->pend_n == 0 && (keep_lag || !h->carry_pending)) return VPTMCM_OK;
+  HIPCHK(h, hipSetDevice(h->device));
+  if (h->pend_n == 0) return do_march(h, h->carry_mvp, nullptr, 0, false);
   const uint32_t n = h->pend_n;
   h->pend_n = 0;
-  HIPCHK(h, hipSetDevice(h->device));
-  return do_march(h, h->pend_mvp, h->pend_seeds, n);
+  return do_march(h, h->pend_mvp, h->pend_seeds, n, keep_lag);
 }
 
 // ---- communicator waits (see vptmcm::comm_timeout_ms)
@@ -513,8 +579,6 @@ int64_t now_ms() {
   return std::chrono::duration_cast<std::chrono::milliseconds>(
              std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-
-constexpr int64_t kAbortWaitMs = 2000;  // longest wait for ncclCommAbort (comm_abort_bounded)
 
 // VPTMCM_COMM_TRACE=1: timestamped lines on stderr at each stage of the
 // communicator's setup and failure handling (diagnostics of RCCL hangs).
@@ -535,33 +599,17 @@ void comm_trace(const char* fmt, ...) {
 
 // Abort the communicator after an error or a timeout: RCCL kernels still
 // waiting for a peer observe the abort flag and exit, so the handle's streams
-// drain. Every later communicator call returns VPTMCM_ECOMM.
-// ncclCommAbort of a communicator whose initialisation still waits for a peer
-// in the bootstrap can block far past any timeout (seen on the GPU pool: more
-// than 120 s, in one of several runs of test_comm_init_peer_never_joins). The
-// abort runs on a detached helper thread; the caller waits for it at most
-// wait_ms and otherwise leaves it (the communicator is never used again, and
-// the helper ends with the process).
-bool comm_abort_bounded(ncclComm_t c, int64_t wait_ms) {
-  if (!c) return true;
-  auto done = std::make_shared<std::atomic<bool>>(false);
-  comm_trace("abort: start");
-  std::thread([c, done] {
-    (void)ncclCommAbort(c);
-    done->store(true, std::memory_order_release);
-    comm_trace("abort: returned");
-  }).detach();
-  const int64_t t0 = now_ms();
-  while (!done->load(std::memory_order_acquire) && now_ms() - t0 < wait_ms)
-    std::this_thread::sleep_for(std::chrono::milliseconds(1));
-  return done->load(std::memory_order_acquire);
-}
-
+// drain. The communicator exists only once its initialisation has returned
+// (vptmcm_comm_init), i.e. past RCCL's bootstrap, so the abort does not wait
+// for a peer. Every later communicator call returns VPTMCM_ECOMM, and the
+// handle's stream waits stay bounded (vptmcm::comm_failed).
 int comm_fail(vptmcm* h, const char* what, const char* why) {
-  const bool aborted = comm_abort_bounded(h->comm, kAbortWaitMs);
+  comm_trace("abort: start (%s)", what);
+  if (h->comm) (void)ncclCommAbort(h->comm);
+  comm_trace("abort: returned");
   h->comm = nullptr;
-  FAIL(h, VPTMCM_ECOMM, "%s: %s (communicator %s; rank %d of %d)", what, why,
-       aborted ? "aborted" : "abandoned: its abort had not returned after 2 s", h->rank, h->nranks);
+  h->comm_failed = true;
+  FAIL(h, VPTMCM_ECOMM, "%s: %s (communicator aborted; rank %d of %d)", what, why, h->rank, h->nranks);
 }
 
 // The communicator's asynchronous state: OK, 1 (still in progress) or the
@@ -617,7 +665,7 @@ int64_t now_us() {
 }
 
 int wait_stream(vptmcm* h, hipStream_t s, const char* what) {
-  if (!h->comm) {
+  if (!h->comm && !h->comm_failed) {
     if (h->sync_spin_us > 0) {  // spin, then block
       const int64_t t0 = now_us();
       for (;;) {
@@ -636,9 +684,12 @@ int wait_stream(vptmcm* h, hipStream_t s, const char* what) {
     if (e == hipSuccess) return VPTMCM_OK;
     if (e != hipErrorNotReady) FAIL(h, VPTMCM_EHIP, "%s: %s", what, hipGetErrorString(e));
     if ((spin & 255u) == 0u) {
-      const int rc = comm_state(h, what);
+      const int rc = h->comm ? comm_state(h, what) : VPTMCM_OK;
       if (rc < 0) return rc;
       if (now_ms() - t0 > h->comm_timeout_ms) {
+        if (!h->comm)
+          FAIL(h, VPTMCM_ECOMM, "%s: stream not drained %lld ms after the communicator's abort", what,
+               (long long)h->comm_timeout_ms);
         char b[96];
         snprintf(b, sizeof b, "stream not drained after %lld ms (a peer rank died or hangs?)",
                  (long long)h->comm_timeout_ms);
@@ -693,6 +744,7 @@ void free_volume(vptmcm* h) {
   h->vol_c8 = nullptr;
   h->volume_ready = false;
   h->vol_done = false;
+  h->vol_dirty = false;
   h->W = h->H = h->D = 0;
 }
 
@@ -966,6 +1018,15 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   CK(hipMemsetAsync(h->sched, 0, 2 * (size_t)sched_flag_bytes(h->n_tiles), h->stream));
   CK(hipMalloc(&h->sched_prev, sched_slot_words(h->n_tiles) * sizeof(uint32_t)));
   CK(hipMemsetAsync(h->sched_prev, 0xff, sched_slot_words(h->n_tiles) * sizeof(uint32_t), h->stream));
+  CK(hipMalloc(&h->tile_next, h->n_tiles * sizeof(uint32_t)));
+  CK(hipMemsetAsync(h->tile_next, 0, h->n_tiles * sizeof(uint32_t), h->stream));
+  CK(hipMalloc(&h->stop_ctr, 2 * sizeof(uint32_t)));
+  CK(hipMemsetAsync(h->stop_ctr, 0, 2 * sizeof(uint32_t), h->stream));
+  // carry: the spectral march with the balanced schedule in one chunk (R <= 512)
+  h->carry_on = h->kind == VPTMCM_RENDERER_SPECTRAL && h->n_tiles <= kSchedChunk &&
+                (h->variant & (1u | 2u | 128u)) == 0u;
+  if (const char* v = getenv("VPTMCM_CARRY")) h->carry_on = h->carry_on && v[0] != '0';
+  if (const char* v = getenv("VPTMCM_STOP_Q")) h->stop_q = (uint32_t)strtoul(v, nullptr, 10);
   if (h->kind == VPTMCM_RENDERER_RGB) {  // WebGPUAbstractComputeRenderer.js:23-28
     static const uint8_t kDefaultTf[8] = {255, 0, 0, 0, 255, 0, 0, 255};
     if (vptmcm_set_transfer_function(h, kDefaultTf, 2, 1)) return fail(VPTMCM_EHIP);
@@ -1002,11 +1063,19 @@ void vptmcm_destroy(vptmcm* h) {
   if (h->comp_rgb32) (void)hipFree(h->comp_rgb32);
   if (h->comp_rgba) (void)hipFree(h->comp_rgba);
   if (h->comp_counts) (void)hipFree(h->comp_counts);
-  // bounded waits while a communicator exists (a failed one is aborted)
-  if (h->comm_stream) (void)wait_stream(h, h->comm_stream, "destroy");
-  if (h->stream) (void)wait_stream(h, h->stream, "destroy");
+  // bounded waits while a communicator exists or after its abort; streams that
+  // did not drain may still touch the handle's buffers, which are then left
+  // allocated (a deliberate leak) rather than freed under running work
+  bool drained = true;
+  if (h->comm_stream) drained = wait_stream(h, h->comm_stream, "destroy") == VPTMCM_OK && drained;
+  if (h->stream) drained = wait_stream(h, h->stream, "destroy") == VPTMCM_OK && drained;
   if (h->comm && comm_call(h, ncclCommFinalize(h->comm), "destroy: ncclCommFinalize") == VPTMCM_OK)
     (void)ncclCommDestroy(h->comm);
+  if (!drained) {
+    comm_trace("destroy: streams not drained; device buffers left allocated");
+    delete h;
+    return;
+  }
   if (h->band_cover) (void)hipFree(h->band_cover);
   for (int k = 0; k < 2; k++) {
     if (h->comp[k]) (void)hipFree(h->comp[k]);
@@ -1031,6 +1100,8 @@ void vptmcm_destroy(vptmcm* h) {
   if (h->light) (void)hipFree(h->light);
   if (h->sched) (void)hipFree(h->sched);
   if (h->sched_prev) (void)hipFree(h->sched_prev);
+  if (h->tile_next) (void)hipFree(h->tile_next);
+  if (h->stop_ctr) (void)hipFree(h->stop_ctr);
   if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -1041,9 +1112,11 @@ void vptmcm_destroy(vptmcm* h) {
 // Block-wise ingest. begin allocates the staging copy (x-fastest u8, zero like
 // a fresh texture) and, for CORNER8 / BRICK8, the cell array (zero cells = a
 // zero volume); every block is copied into the staging copy and the cells it
-// touches are re-laid out at once, so its bricks are resident in HBM as soon
-// as its placement arrives and the volume is renderable throughout (blocks
-// not yet written read as zero density); end frees the staging copy.
+// touches join a box that is re-laid out in one launch before the next march
+// reads the cells or at end (consecutive placements are batched: a
+// slice-by-slice ingest relays each cell once, not twice), so the volume is
+// renderable throughout (blocks not yet written read as zero density); end
+// frees the staging copy.
 static int volume_begin_one(vptmcm* h, uint32_t width, uint32_t height, uint32_t depth) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
@@ -1115,14 +1188,16 @@ static int volume_write_block_one(vptmcm* h, const uint8_t* data, uint32_t x, ui
     HIPCHK(h, hipMemcpy3DAsync(&p, h->stream));
   }
   if (h->layout != kLayoutLinear) {
-    // the cells whose 8 corners include a voxel of the block: x .. x + bw per axis
-    const bool brick = h->layout == kLayoutBrick8;
-    const uint32_t c0[3] = {x, y, z}, n[3] = {bw + 1u, bh + 1u, bd + 1u};
-    HIPCHK(h, launch_corner8(h->vol_lin, h->W, h->H, h->D,
-                             brick ? (h->W + kBrickCells) / kBrickCells : 0u,
-                             brick ? (h->H + kBrickCells) / kBrickCells : 0u, h->vol_c8, h->stream, c0, n));
+    // the cells whose 8 corners include a voxel of the block, x .. x + bw per
+    // axis, join the box re-laid out before the next march (flush_relayout)
+    const uint32_t c0[3] = {x, y, z}, c1[3] = {x + bw + 1u, y + bh + 1u, z + bd + 1u};
+    for (int k = 0; k < 3; k++) {
+      h->vol_c0[k] = h->vol_dirty ? std::min(h->vol_c0[k], c0[k]) : c0[k];
+      h->vol_c1[k] = h->vol_dirty ? std::max(h->vol_c1[k], c1[k]) : c1[k];
+    }
+    h->vol_dirty = true;
   }
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));  // the caller keeps the block buffer
   return VPTMCM_OK;
 }
 
@@ -1131,6 +1206,7 @@ static int volume_end_one(vptmcm* h) {
   if (int rc_ = flush_renders(h)) return rc_;
   if (!h->vol_lin || h->vol_done) FAIL(h, VPTMCM_ESTATE, "volume_end without volume_begin");
   HIPCHK(h, hipSetDevice(h->device));
+  if (int rc = flush_relayout(h)) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->layout != kLayoutLinear) {  // every cell is current: the staging copy goes
     HIPCHK(h, hipFree(h->vol_lin));
@@ -1312,6 +1388,7 @@ static int reset_one(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   if (!mvp) FAIL(h, VPTMCM_EINVAL, "reset: null matrix");
   HIPCHK(h, hipSetDevice(h->device));
   MarchParams P = make_params(h, mvp, seed_bits);
+  h->tile_next_stale = true;  // no pass is owed after a reset (flush_renders ran them)
   if (h->kind == VPTMCM_RENDERER_RGB)
     HIPCHK(h, launch_reset_rgb(P, h->photons, h->stream));
   else
@@ -1327,7 +1404,9 @@ static int render_one(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   // queue the pass; a different matrix or a full queue launches the queue
   // first (the launch order, and so every result, is unchanged)
   if (h->pend_n == kMaxFusedPasses || (h->pend_n && memcmp(h->pend_mvp, mvp, sizeof h->pend_mvp))) {
-    int rc = flush_renders(h);
+    // a full queue: more passes follow, owed passes may carry; another matrix:
+    // the queued ones complete first
+    int rc = flush_renders(h, h->pend_n == kMaxFusedPasses && !memcmp(h->pend_mvp, mvp, sizeof h->pend_mvp));
     if (rc) return rc;
   }
   if (h->pend_n == 0) memcpy(h->pend_mvp, mvp, sizeof h->pend_mvp);
@@ -1342,7 +1421,9 @@ static int render_passes_one(vptmcm* h, const float* mvp, const uint32_t* seeds,
   HIPCHK(h, hipSetDevice(h->device));
   const uint32_t fuse = (h->variant & 4u) ? 1u : kMaxFusedPasses;  // variant bit 2: one pass per launch
   for (uint32_t k = 0; k < n; k += fuse) {
-    int rc = do_march(h, mvp, seeds + k, n - k < fuse ? n - k : fuse);
+    // every launch but the call's last may leave owed passes (carry); the last
+    // one completes every tile
+    int rc = do_march(h, mvp, seeds + k, n - k < fuse ? n - k : fuse, k + fuse < n);
     if (rc) return rc;
   }
   return VPTMCM_OK;
@@ -1581,54 +1662,28 @@ int vptmcm_comm_init(vptmcm* h, const uint8_t* uid, int nranks, int rank) {
   }
   ncclUniqueId id;
   memcpy(&id, uid, sizeof id);
-  // Bounded: a peer that never joins ends in VPTMCM_ECOMM after the timeout.
-  // The initialisation runs on a helper thread that the handle waits for at
-  // most comm_timeout_ms and otherwise abandons: a non-blocking config
-  // (blocking = 0, round 3's first version) still blocked inside
-  // ncclCommInitRankConfig for the first communicator of a process whose peer
-  // never joined (tools/comm_abort_repeat.py), and its asynchronous group job
-  // lives in the calling thread's thread-local storage, so the helper runs the
-  // blocking form (the whole initialisation inside the call, nothing left
-  // behind in its TLS when it exits). Collectives on the communicator are
-  // watched as before (comm_state / wait_stream: ncclCommGetAsyncError, bounded
-  // waits, ncclCommAbort).
-  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-  cfg.blocking = 1;
+  // RCCL 2.27.7 does not return from ncclCommInitRankConfig while its bootstrap
+  // waits for a rank that never arrives, with blocking = 0 too: the calling
+  // thread sleep-polls inside the call while the init job spins on the
+  // bootstrap sockets and the root thread waits in accept()
+  // (tools/comm_diag.cpp, profiles/r04/s1/comm_diag_nb.log), and no
+  // communicator handle exists to abort until the call returns. Peer liveness
+  // is therefore established before this call (rendezvous.join: every rank
+  // present, bounded by VPTMCM_COMM_TIMEOUT_MS, ECOMM otherwise), and the call
+  // runs in the caller's thread: no helper thread is left behind.
+  comm_trace("comm_init: ncclCommInitRank nranks=%d rank=%d", nranks, rank);
+  ncclComm_t c = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&c, nranks, id, rank);
+  comm_trace("comm_init: ncclCommInitRank returned %d", (int)r);
+  if (r != ncclSuccess) {
+    if (c) (void)ncclCommAbort(c);
+    FAIL(h, VPTMCM_ECOMM, "ncclCommInitRank (rank %d of %d): %s", rank, nranks, ncclGetErrorString(r));
+  }
+  h->comm = c;
+  h->comm_failed = false;
   h->nranks = nranks;
   h->rank = rank;
-  struct InitJob {
-    ncclComm_t comm = nullptr;
-    ncclResult_t r = ncclInternalError;
-    std::atomic<bool> done{false};
-  };
-  auto job = std::make_shared<InitJob>();
-  comm_trace("comm_init: ncclCommInitRankConfig nranks=%d rank=%d", nranks, rank);
-  std::thread([job, nranks, id, rank, cfg, dev = h->device]() mutable {
-    (void)hipSetDevice(dev);  // RCCL binds the communicator to the calling thread's device
-    ncclComm_t c = nullptr;
-    const ncclResult_t res = ncclCommInitRankConfig(&c, nranks, id, rank, &cfg);
-    job->comm = c;
-    job->r = res;
-    job->done.store(true, std::memory_order_release);
-  }).detach();
-  const int64_t t0 = now_ms();
-  for (uint32_t spin = 0; !job->done.load(std::memory_order_acquire); spin++) {
-    if (now_ms() - t0 > h->comm_timeout_ms)
-      FAIL(h, VPTMCM_ECOMM,
-           "comm_init: ncclCommInitRankConfig had not returned after %lld ms (a peer rank never "
-           "joined?); the initialisation is abandoned (rank %d of %d)",
-           (long long)h->comm_timeout_ms, rank, nranks);
-    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(200));
-  }
-  h->comm = job->comm;
-  const ncclResult_t r = job->r;
-  comm_trace("comm_init: ncclCommInitRankConfig returned %d", (int)r);
-  if (r != ncclSuccess && r != ncclInProgress) {
-    comm_abort_bounded(h->comm, kAbortWaitMs);
-    h->comm = nullptr;
-    FAIL(h, VPTMCM_ECOMM, "ncclCommInitRankConfig: %s", ncclGetErrorString(r));
-  }
-  if (int rc = comm_settle(h, "comm_init")) return rc;
+
   HIPCHK(h, hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking));
   size_t bytes = (size_t)h->R * h->R * sizeof(float4);
   for (int k = 0; k < 2; k++) {
@@ -1804,6 +1859,25 @@ int vptmcm_debug_last_launch(vptmcm* h, uint32_t info[4], uint64_t* launches) {
   info[2] = h->last_launch.spec;
   info[3] = h->last_launch.passes;
   if (launches) *launches = h->march_launches;
+  return VPTMCM_OK;
+}
+
+int vptmcm_debug_owed(vptmcm* h, uint32_t* out, uint32_t n_words, uint32_t* n_tiles) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (int rc_ = flush_renders(h, true)) return rc_;  // queued passes launch; owed ones stay owed
+  if (!n_tiles) FAIL(h, VPTMCM_EINVAL, "debug_owed: null tile count");
+  *n_tiles = h->n_tiles;
+  if (!out) return VPTMCM_OK;
+  if (n_words < h->n_tiles) FAIL(h, VPTMCM_EINVAL, "debug_owed: output holds fewer words than tiles");
+  HIPCHK(h, hipSetDevice(h->device));
+  if (h->tile_next_stale || !h->carry_on) {
+    for (uint32_t t = 0; t < h->n_tiles; t++) out[t] = 0u;
+    return VPTMCM_OK;
+  }
+  HIPCHK(h, hipMemcpyAsync(out, h->tile_next, h->n_tiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  for (uint32_t t = 0; t < h->n_tiles; t++) out[t] = h->pass_target - out[t];
   return VPTMCM_OK;
 }
 
