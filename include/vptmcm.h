@@ -349,7 +349,8 @@ int vptmcm_debug_last_launch(vptmcm* h, uint32_t info[4], uint64_t* launches);
 /* The tile schedule of the last spectral march launch (after launching any
  * queued render() passes): per wave slot (block * 16 + wave of the march grid)
  * the tile it ran, with bit 31 set when the tile entered the volume in the
- * launch before (the schedule's volume class), 0xffffffff for an idle slot.
+ * launch before (the schedule's volume class) and bits 29-30 its lag bucket in
+ * a cross-launch-balanced launch (0 otherwise), 0xffffffff for an idle slot.
  * *n_slots receives the slot count; out (may be NULL to query the count)
  * must hold n_words >= *n_slots words. Only launches with the balanced
  * schedule (R <= 1024, not the raster variant) write it; a fresh handle reports

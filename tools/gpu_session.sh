@@ -12,7 +12,7 @@ STEPS=${STEPS:-tests bench prof}
 for s in $STEPS; do
   case $s in
   tests)
-    timeout -k 10 ${TEST_T:-900} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
+    timeout -k 10 ${TEST_T:-900} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_gpu.log 2>&1
     rc=$?; echo "pytest rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc ;;
   smoke)
     timeout -k 10 300 python __graft_entry__.py smoke > $OUT/smoke.log 2>&1
@@ -60,12 +60,36 @@ for s in $STEPS; do
       rc=$?; echo "commdiag $m rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
     done ;;
   carryab)  # cross-launch balancing A/B on the default 1024-pass line (alternating, one box)
-    for c in 0 1 0 1; do
-      VPTMCM_CARRY=$c timeout -k 10 300 python bench.py --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 256 --unfused-steps 0 > $OUT/carry_$c.json 2>> $OUT/carry.err
+    for c in ${CARRY_CASES:-0 1 0 1}; do  # 0 off, 1 on (quota: lone slots), q<N>: on with VPTMCM_STOP_Q=N
+      case $c in q*) cv=1; q=${c#q};; *) cv=$c; q=0;; esac
+      VPTMCM_CARRY=$cv VPTMCM_STOP_Q=$q timeout -k 10 300 python bench.py --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 256 --unfused-steps 0 > $OUT/carry_$c.json 2>> $OUT/carry.err
       rc=$?; [ $rc -ne 0 ] && { echo "carryab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
-      python3 -c "import json; d=json.load(open('$OUT/carry_$c.json')); print(json.dumps({'carry': $c, 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'render_api': d['render_api']['value']}))" >> $OUT/carryab.jsonl
+      python3 -c "import json; d=json.load(open('$OUT/carry_$c.json')); print(json.dumps({'carry': '$c', 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'render_api': d['render_api']['value']}))" >> $OUT/carryab.jsonl
     done
     echo "carryab rc=0" | tee -a $OUT/status.txt; cat $OUT/carryab.jsonl ;;
+  wallsplit)  # the driver's exact command under a kernel trace + host clocks of its timed region
+    (cd /tmp && export TMPDIR=/tmp VPTMCM_BENCH_STAMPS="$GRAFT_REPO_ROOT/$OUT/stamps.json" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/drvprof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 > "$GRAFT_REPO_ROOT/$OUT/drvprof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/drvprof.err")
+    rc=$?; echo "wallsplit rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
+    python3 tools/wall_split.py $OUT/stamps.json $OUT/drvprof/run_kernel_trace.csv > $OUT/wall_split.json 2>&1; cat $OUT/wall_split.json ;;
+  ingest)  # block-wise volume ingest time (tools/ingest_time.py)
+    timeout -k 10 300 python tools/ingest_time.py > $OUT/ingest.jsonl 2> $OUT/ingest.err
+    rc=$?; echo "ingest rc=$rc" | tee -a $OUT/status.txt; cat $OUT/ingest.jsonl; fault $rc && exit $rc ;;
+  drvab)  # the driver's command, alternating the round-3 library (VPTMCM_LIB=r03) and the current one
+    for lib in ${DRV_LIBS:-r03 cur r03 cur r03 cur r03 cur}; do
+      if [ $lib = cur ]; then unset VPTMCM_LIB; else export VPTMCM_LIB=$lib; fi
+      timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 > $OUT/drv_$lib.json 2>> $OUT/drvab.err
+      rc=$?; unset VPTMCM_LIB; [ $rc -ne 0 ] && { echo "drvab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      python3 -c "import json; d=json.load(open('$OUT/drv_$lib.json')); r=d['roofline']; print(json.dumps({'lib': '$lib', 'value': d['value'], 'wall_us': round(d['ms_per_step']*20e3, 1), 'kernel_us': r['kernel_avg_us'], 'wall_minus_kernel_us': round(d['ms_per_step']*20e3 - r['kernel_avg_us'], 1)}))" >> $OUT/drvab.jsonl
+    done
+    echo "drvab rc=0" | tee -a $OUT/status.txt; cat $OUT/drvab.jsonl ;;
+  ingest_r03)
+    VPTMCM_LIB=r03 timeout -k 10 300 python tools/ingest_time.py > $OUT/ingest_r03.jsonl 2> $OUT/ingest_r03.err
+    rc=$?; echo "ingest_r03 rc=$rc" | tee -a $OUT/status.txt; cat $OUT/ingest_r03.jsonl; fault $rc && exit $rc ;;
+  carryprobe)  # launch-by-launch owed passes and kernel-trace durations, carry on and off
+    for c in 1 0; do
+      (cd /tmp && export TMPDIR=/tmp VPTMCM_CARRY=$c && timeout -k 10 300 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$OUT/cprobe_$c" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/carry_probe.py" > "$GRAFT_REPO_ROOT/$OUT/cprobe_$c.jsonl" 2> "$GRAFT_REPO_ROOT/$OUT/cprobe_$c.err")
+      rc=$?; echo "carryprobe $c rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
+    done ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)

@@ -400,6 +400,8 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
 // s_waitcnt immediate (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8]
 // | vmcnt_hi[15:14]) for vmcnt(0) with expcnt and lgkmcnt left unconstrained.
 constexpr uint32_t kWaitVmcnt0 = 0x0F70u;
+// The tile of a packed schedule slot word (TileSched::prev, s_tile).
+constexpr uint32_t kSlotTileMask = 0x1fffffffu;
 
 // Copies CHUNKS * kMarchBlock uint4 from global memory into LDS with
 // global_load_lds_dwordx4: each wave's instruction writes 64 consecutive
@@ -497,8 +499,9 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   if (P.sched != 1u) {  // a scalar load (lgkmcnt): its use does not wait for the TF copy
     const auto pt = (const __attribute__((address_space(4))) uint32_t*)T.prev;
     prev = pt[blockIdx.x * 16u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
-    if (prev != 0xffffffffu && (prev >> 31) != 0u && (prev & 0x7fffffffu) < P.n_tiles)
-      load_photon(ph, S, (size_t)(prev & 0x7fffffffu) * 64u + lane, p);
+    // (the packed slot word: tile | volume << 31 | lag bucket << 29)
+    if (prev != 0xffffffffu && (prev >> 31) != 0u && (prev & kSlotTileMask) < P.n_tiles)
+      load_photon(ph, S, (size_t)(prev & kSlotTileMask) * 64u + lane, p);
   }
   // (raw bytes here, converted at their LDS store: a conversion here would
   // wait for the TF copy before the schedule starts)
@@ -522,7 +525,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   if (CARRY && blockIdx.x == 0u && threadIdx.x == 0u) *T.stop_ctr_next = 0u;  // the next launch's counter
   if (P.sched != 1u) {
     const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile<CARRY>(P, f0, T.flags_in, s_red, s_tile, &stop_q));
-    tile = s == 0xffffffffu ? s : s & 0x1fffffffu;
+    tile = s == 0xffffffffu ? s : s & kSlotTileMask;
     hot0 = s != 0xffffffffu && (s >> 31) != 0u;
     owing = CARRY && s != 0xffffffffu && ((s >> 29) & 3u) != 0u;
     have = hot0 && s == prev;

@@ -130,7 +130,10 @@ def load() -> C.CDLL:
         "vptmcm_group_devices": (C.c_int, [vp, C.POINTER(C.c_int32), u32p]),
         "vptmcm_debug_owed": (C.c_int, [vp, u32p, C.c_uint32, u32p]),
     }
+    variant = bool(os.environ.get("VPTMCM_LIB"))
     for name, (res, args) in sig.items():
+        if variant and not hasattr(L, name):
+            continue  # an A/B variant built from an older revision lacks newer entry points
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
