@@ -562,6 +562,11 @@ def main():
                                           if traffic and not a.no_timing else None),
                          "issue": issue,
                          "kernel": "k_march", "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
+                         # host wall time of the timed region minus its march GPU time (launch
+                         # enqueue, dispatch, completion wake-up)
+                         "region_wall_us": round(el_max * 1e6, 1),
+                         "wall_minus_kernel_us": (round(el_max * 1e6 - kern_ms_max * 1e3, 1)
+                                                  if not a.no_timing else None),
                          "passes_per_launch": ppl,
                          "kernel_us_per_pass": round(kern_ms_max * 1e3 / a.steps, 3),
                          "algorithmic_bytes_per_launch": bytes_per_launch,

@@ -13,6 +13,12 @@
 #ifndef VPT_NB_ZERO
 #define VPT_NB_ZERO 1  // nb < 12: unguarded 12-bin loops over zeroed unused bins
 #endif
+#ifndef VPT_CTR_EARLY
+#define VPT_CTR_EARLY 0  // 1: read the carry stop counter at the top of each pass (one pass stale)
+#endif
+#ifndef VPT_OWE_PRIO
+#define VPT_OWE_PRIO 1  // carry: the owing wave of a pair takes the higher issue priority
+#endif
 #ifndef VPT_PRIO
 #define VPT_PRIO 1  // s_setprio level of volume waves (0 = off); 11 % faster passes
 #endif
@@ -688,12 +694,14 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       done_passes = pass;  // the pending sample is applied after the loop
       break;
     }
+#if VPT_CTR_EARLY
     if (lane == 0u) ctr_v = __hip_atomic_load(T.stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
   }
 #if VPT_PRIO
   if (pass > 0u) hot = entered;
   if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) {
-    if (CARRY && owing) __builtin_amdgcn_s_setprio(VPT_PRIO + 1);  // the owing wave of a pair leads
+    if (CARRY && VPT_OWE_PRIO && owing) __builtin_amdgcn_s_setprio(VPT_PRIO + 1);  // the owing wave of a pair leads
     else __builtin_amdgcn_s_setprio(VPT_PRIO);
   } else {
     __builtin_amdgcn_s_setprio(0);
@@ -705,6 +713,13 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   if constexpr (SPEC) {
     for (uint32_t step = 0; step < P.steps; step++) {
       STAMP_RESTART();
+#if !VPT_CTR_EARLY
+      // the stop counter, read during the pass's last step (lane 0, coherent
+      // across the XCDs): it lands with that step's gather and is at most one
+      // step old at the pass boundary
+      if (stop_ok && step + 1u == P.steps && lane == 0u)
+        ctr_v = __hip_atomic_load(T.stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
       // The previous step's deferred add_radiance, once, ahead of every path:
       // one definition of the bins for the loop's back edge (per-path updates
       // left 12 + 14 register copies in the volume and all-exit latches), and
@@ -958,7 +973,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     if (stop_ok && owe == 0u) __hip_atomic_fetch_add(T.stop_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   STAMP_END(rgb32, tile, entered);
-  TL_END(rgb32, tile, entered);
+  TL_END(rgb32, tile, entered, CARRY ? ((n_passes << 16) | (done_passes << 8) | (owing ? 1u : 0u)) : 0u);
 }
 
 

@@ -26,14 +26,16 @@
     __builtin_amdgcn_s_waitcnt(0x0F70);   \
     TL_MARK(k);                           \
   } while (0)
-#define TL_END(out, tile, entered)                                                       \
+// extra (non-zero): word 6 instead of the probe time (carry launches: the
+// tile's passes to do << 16 | passes done << 8 | owing)
+#define TL_END(out, tile, entered, extra)                                                \
   do {                                                                                   \
     TL_MARK_WAIT(4);                                                                     \
     if (lane == 0u) {                                                                    \
       uint32_t* _o = reinterpret_cast<uint32_t*>(out) + (size_t)(tile) * 8u;             \
       for (int _k = 0; _k < 5; _k++) _o[_k] = tl[_k];                                    \
       _o[5] = ((entered) ? 1u : 0u) | ((__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xffu) << 8); \
-      _o[6] = tl[5];                                                                     \
+      _o[6] = (extra) ? (uint32_t)(extra) : tl[5];                                       \
       _o[7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);                                 \
     }                                                                                    \
   } while (0)
@@ -59,8 +61,8 @@
 #define TL_MARK_WAIT(k) \
   do {                  \
   } while (0)
-#define TL_END(out, tile, entered) \
-  do {                             \
+#define TL_END(out, tile, entered, extra) \
+  do {                                    \
   } while (0)
 #endif
 

@@ -517,7 +517,12 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n, boo
   }
   if (int rc = flush_relayout(h)) return rc;
   MarchParams P = make_params(h, mvp, n ? seeds[0] : 0u);
-  const bool carry = h->carry_on && (allow_stop || h->carry_pending);
+  // VPTMCM_CARRY_FORCE=1 (measurement): the carry kernel for every launch, stops or not
+  static const bool force = [] {
+    const char* v = getenv("VPTMCM_CARRY_FORCE");
+    return v && v[0] == '1';
+  }();
+  const bool carry = h->carry_on && (allow_stop || h->carry_pending || force);
   if (carry && h->tile_next_stale) {  // every tile is at the last target: the one this launch starts from
     HIPCHK(h, hipMemsetD32Async(h->tile_next, (int)h->pass_target, h->n_tiles, h->stream));
     h->tile_next_stale = false;
@@ -565,6 +570,13 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n, boo
 // otherwise (an observation, an input change, another matrix) every tile is
 // run to the last queued pass, with a completion launch if nothing is queued.
 int flush_renders(vptmcm* h, bool keep_lag = false) {
+  // VPTMCM_CARRY_NOFINAL=1 (timeline diagnostics only; results then wrong): no
+  // completion launch, so a read sees the stamps of the last early-stop launch
+  static const bool nofinal = [] {
+    const char* v = getenv("VPTMCM_CARRY_NOFINAL");
+    return v && v[0] == '1';
+  }();
+  if (nofinal) keep_lag = true;
   if (h->pend_n == 0 && (keep_lag || !h->carry_pending)) return VPTMCM_OK;
   HIPCHK(h, hipSetDevice(h->device));
   if (h->pend_n == 0) return do_march(h, h->carry_mvp, nullptr, 0, false);
