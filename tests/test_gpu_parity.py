@@ -955,8 +955,8 @@ def test_c3_driver_shaped_launch_bitexact():
     gpu.close()
 
 
-def test_carry_owed_passes_bitexact_c3():
-    """Cross-launch balancing on C3 itself (512^3, R = 512): render() calls queue
+def test_carry_owed_passes_bitexact_c3(monkeypatch):
+    """Cross-launch balancing (VPTMCM_CARRY=1) on C3 itself (512^3, R = 512): render() calls queue
     32-pass launches that may end early, volume waves stopping at a pass
     boundary once the lone SIMDs' waves reach the target and owing the rest;
     the next launch deals the owing tiles first. After two full queues some
@@ -964,6 +964,7 @@ def test_carry_owed_passes_bitexact_c3():
     to the last queued pass, and photons, fp32 and rgba16f images are bit-exact
     against 72 oracle passes. render_passes(72) in one call (the bench's
     region shape) is bit-exact too."""
+    monkeypatch.setenv("VPTMCM_CARRY", "1")
     R = 512
     vol, tf, mvp = cf.fbm_volume(512, 512, nthreads=8), cf.tf_spectral(), cf.default_mvp_inverse()
     gpu, cpu = make_pair(R, vol, tf, ext=32.0)
@@ -990,11 +991,12 @@ def test_carry_owed_passes_bitexact_c3():
 
 
 @pytest.mark.parametrize("layout", [vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_BRICK8])
-def test_carry_matrix_change_and_inputs_complete_owed_passes(layout):
+def test_carry_matrix_change_and_inputs_complete_owed_passes(layout, monkeypatch):
     """Owed passes run with their own matrix: a render() with another camera
     first completes them (oracle: the same passes in order, old camera then
     new); an input change (set_params) completes them with the old inputs; the
     UI-like TF with uneven bins (MODE 6) carries too."""
+    monkeypatch.setenv("VPTMCM_CARRY", "1")
     R = 128
     vol, mvp1, mvp2 = cf.fbm_volume(96, 17, nthreads=8), cf.golden_mvp("orbit"), cf.default_mvp_inverse()
     for tf, spec in ((cf.tf_spectral(), "12"), (cf.tf_materials(True), "8_uneven")):
@@ -1027,7 +1029,7 @@ def test_carry_matrix_change_and_inputs_complete_owed_passes(layout):
 
 
 def test_carry_off_matches(monkeypatch):
-    """VPTMCM_CARRY=0 (no early stops): the same bits, and nothing is ever owed."""
+    """VPTMCM_CARRY=0 (the default; no early stops): the same bits, and nothing is ever owed."""
     monkeypatch.setenv("VPTMCM_CARRY", "0")
     R = 128
     gpu, cpu = make_pair(R, cf.fbm_volume(96, 18, nthreads=8), cf.tf_spectral(), ext=24.0)

@@ -46,6 +46,9 @@ struct TileSched {
 // bit 0 its wave entered the volume, bits 1-2 its lag bucket (passes it still
 // owes after the launch: 0, 1-3, 4-7, >= 8).
 constexpr uint32_t kFlagVolume = 1u, kLagShift = 1u;
+// A launch's stop block (TileSched::stop_ctr): counter line + flag lines.
+constexpr uint32_t kStopFlagLines = 64u, kStopLineWords = 32u;
+constexpr uint32_t kStopBlockWords = (1u + kStopFlagLines) * kStopLineWords;
 constexpr uint32_t kSchedChunk = 4 * kMarchBlock;  // tiles scanned per block-wide round
 constexpr uint32_t kSchedMaxTiles = 16384;         // larger frames use the raster mapping
 // Seeds of the passes one march launch runs back to back (render_passes): the

@@ -406,6 +406,16 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
 // s_waitcnt immediate (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8]
 // | vmcnt_hi[15:14]) for vmcnt(0) with expcnt and lgkmcnt left unconstrained.
 constexpr uint32_t kWaitVmcnt0 = 0x0F70u;
+// Early stop of a carry launch (TileSched::stop_ctr): the completion counter in
+// word 0, then kStopFlagLines flag lines, one 128-B line each, raised together
+// when the counter reaches the quota; a wave polls the line of its tile (one
+// load per pass, second half of its passes only), so the 1600 pollers spread
+// over 64 lines instead of queueing on the counter's (round 4: polling the
+// counter itself every pass cost 8 % per pass).
+__device__ __forceinline__ uint32_t stop_flag_load(const TileSched& T, uint32_t tile) {
+  return __hip_atomic_load(T.stop_ctr + kStopLineWords * (1u + (tile & (kStopFlagLines - 1u))),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // The tile of a packed schedule slot word (TileSched::prev, s_tile).
 constexpr uint32_t kSlotTileMask = 0x1fffffffu;
 
@@ -528,7 +538,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   bool have = false;  // p already holds this tile's state (the slot's tile did not change)
   bool owing = false;  // the tile owes passes of earlier launches (lag bucket > 0)
   uint32_t stop_q = 0u;
-  if (CARRY && blockIdx.x == 0u && threadIdx.x == 0u) *T.stop_ctr_next = 0u;  // the next launch's counter
+  // the next launch's stop block: its counter (word 0) and its 64 flag lines
+  if (CARRY && blockIdx.x == 0u && threadIdx.x <= kStopFlagLines) T.stop_ctr_next[kStopLineWords * threadIdx.x] = 0u;
   if (P.sched != 1u) {
     const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile<CARRY>(P, f0, T.flags_in, s_red, s_tile, &stop_q));
     tile = s == 0xffffffffu ? s : s & kSlotTileMask;
@@ -690,12 +701,12 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   uint32_t ctr_v = 0u, done_passes = n_passes;
   for (uint32_t pass = 0; pass < n_passes; pass++) {
   if (stop_ok) {
-    if (pass > 0u && __builtin_amdgcn_readfirstlane(ctr_v) >= stop_q && n_passes - pass <= kMaxFusedPasses) {
+    if (pass > 0u && __builtin_amdgcn_readfirstlane(ctr_v) != 0u && n_passes - pass <= kMaxFusedPasses) {
       done_passes = pass;  // the pending sample is applied after the loop
       break;
     }
 #if VPT_CTR_EARLY
-    if (lane == 0u) ctr_v = __hip_atomic_load(T.stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0u && 2u * pass >= n_passes) ctr_v = stop_flag_load(T, tile);
 #endif
   }
 #if VPT_PRIO
@@ -717,8 +728,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       // the stop counter, read during the pass's last step (lane 0, coherent
       // across the XCDs): it lands with that step's gather and is at most one
       // step old at the pass boundary
-      if (stop_ok && step + 1u == P.steps && lane == 0u)
-        ctr_v = __hip_atomic_load(T.stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (stop_ok && step + 1u == P.steps && lane == 0u && 2u * pass >= n_passes)
+        ctr_v = stop_flag_load(T, tile);
 #endif
       // The previous step's deferred add_radiance, once, ahead of every path:
       // one definition of the bins for the loop's back edge (per-path updates
@@ -970,7 +981,13 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     const uint32_t bucket = owe == 0u ? 0u : owe < 4u ? 1u : owe < 8u ? 2u : 3u;
     T.flags_out[tile] = (entered ? kFlagVolume : 0u) | (bucket << kLagShift);
     if (CARRY) T.tile_next[tile] = PS.base + first + done_passes;
-    if (stop_ok && owe == 0u) __hip_atomic_fetch_add(T.stop_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (stop_ok && n_passes == done_passes) {
+    // count the completion; the one that reaches the quota raises the 64 flag lines
+    uint32_t old = 0u;
+    if (lane == 0u) old = __hip_atomic_fetch_add(T.stop_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__builtin_amdgcn_readfirstlane(old) + 1u == stop_q)
+      __hip_atomic_store(T.stop_ctr + kStopLineWords * (1u + lane), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   STAMP_END(rgb32, tile, entered);
   TL_END(rgb32, tile, entered, CARRY ? ((n_passes << 16) | (done_passes << 8) | (owing ? 1u : 0u)) : 0u);

@@ -90,7 +90,7 @@ struct vptmcm {
   bool tile_next_stale = false;  // tile_next lags the launches (every tile is at pass_target)
   float carry_mvp[16] = {};    // the matrix of the owed passes
   uint32_t* tile_next = nullptr;
-  uint32_t* stop_ctr = nullptr;  // two completion counters, alternating per launch
+  uint32_t* stop_ctr = nullptr;  // two stop blocks (counter + flag lines), alternating per launch
   uint32_t ctr_parity = 0;
   uint32_t stop_q = 0;         // VPTMCM_STOP_Q: the early-stop quota (0: the lone SIMD slots)
   uint32_t pass_target = 0;    // absolute index of the next pass to queue
@@ -545,7 +545,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n, boo
   const uint8_t* vol = h->layout != kLayoutLinear ? (const uint8_t*)h->vol_c8 : h->vol_lin;
   const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
   TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev, h->tile_next,
-              h->stop_ctr + h->ctr_parity, h->stop_ctr + (h->ctr_parity ^ 1u)};
+              h->stop_ctr + h->ctr_parity * kStopBlockWords, h->stop_ctr + (h->ctr_parity ^ 1u) * kStopBlockWords};
   // variant bit 1: raster mapping; bit 7: round 2's XCD-by-XCD slot order
   P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : (h->variant & 128u) ? 2u : 0u;
   if (h->kind == VPTMCM_RENDERER_RGB)
@@ -1032,12 +1032,15 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   CK(hipMemsetAsync(h->sched_prev, 0xff, sched_slot_words(h->n_tiles) * sizeof(uint32_t), h->stream));
   CK(hipMalloc(&h->tile_next, h->n_tiles * sizeof(uint32_t)));
   CK(hipMemsetAsync(h->tile_next, 0, h->n_tiles * sizeof(uint32_t), h->stream));
-  CK(hipMalloc(&h->stop_ctr, 2 * sizeof(uint32_t)));
-  CK(hipMemsetAsync(h->stop_ctr, 0, 2 * sizeof(uint32_t), h->stream));
-  // carry: the spectral march with the balanced schedule in one chunk (R <= 512)
-  h->carry_on = h->kind == VPTMCM_RENDERER_SPECTRAL && h->n_tiles <= kSchedChunk &&
-                (h->variant & (1u | 2u | 128u)) == 0u;
-  if (const char* v = getenv("VPTMCM_CARRY")) h->carry_on = h->carry_on && v[0] != '0';
+  CK(hipMalloc(&h->stop_ctr, 2 * kStopBlockWords * sizeof(uint32_t)));
+  CK(hipMemsetAsync(h->stop_ctr, 0, 2 * kStopBlockWords * sizeof(uint32_t), h->stream));
+  // carry (VPTMCM_CARRY=1): the spectral march with the balanced schedule in one
+  // chunk (R <= 512). Off by default: bit-exact, but measured no faster — the
+  // background waves' work fills the tail it removes
+  h->carry_on = false;
+  if (const char* v = getenv("VPTMCM_CARRY"))
+    h->carry_on = v[0] == '1' && h->kind == VPTMCM_RENDERER_SPECTRAL && h->n_tiles <= kSchedChunk &&
+                  (h->variant & (1u | 2u | 128u)) == 0u;
   if (const char* v = getenv("VPTMCM_STOP_Q")) h->stop_q = (uint32_t)strtoul(v, nullptr, 10);
   if (h->kind == VPTMCM_RENDERER_RGB) {  // WebGPUAbstractComputeRenderer.js:23-28
     static const uint8_t kDefaultTf[8] = {255, 0, 0, 0, 255, 0, 0, 255};
