@@ -183,3 +183,37 @@ def test_group_argument_errors():
     with pytest.raises(vptmcm.VptError, match="no volume"):
         g.render(cf.default_mvp_inverse(), 1)
     g.close()
+
+
+def test_group_rgb_sibling_composites():
+    """The RGB sibling ('mcm-compute') behind a device list: two replicas on one
+    GPU, composited like the spectral renderer's; its fp32 image is the photon's
+    radiance (MCMComputeRenderer.wgsl:161), so the oracle composite is built
+    from the oracle photons."""
+    from test_gpu_rgb import tf_rgb
+    R, vol, mvp = 64, cf.fbm_volume(48, 13, nthreads=8), cf.default_mvp_inverse()
+    tf, env = tf_rgb("ramp"), (255, 230, 200, 255)
+    g = vptmcm.Renderer(R, devices=[0, 0], renderer=vptmcm.RENDERER_RGB)
+    g.set_transfer_function(tf)
+    g.set_environment(env)
+    g.set_volume(vol)
+    g.set_params(extinction=24.0, anisotropy=0.6, bounces=8, steps=8)
+    base = cf.seed_stream(6, start=40)
+    g.reset(mvp, base[0])
+    g.render_passes(mvp, base[1:])
+    reps = []
+    for k in (0, 1):
+        o = orc.OracleRGB(R)
+        o.volume, o.tf, o.env = vol, tf, np.array(env, np.uint8)
+        o.params.update(extinction=24.0, anisotropy=0.6, bounces=8, steps=8)
+        s = cf.seed_stream(6, start=40, rank=k)
+        o.reset(mvp, s[0])
+        for x in s[1:]:
+            o.render(mvp, x)
+        rgb = o.photons.reshape(R, R, -1)[..., 12:15].copy().view(np.float32)
+        reps.append((o, rgb))
+    assert (g.read_photons() == reps[0][0].photons).all()
+    want_rgb, want_rgba, _ = _composite(reps)
+    assert_rgb32_equal(g.read_rgb(), want_rgb, "RGB sibling composite")
+    assert_rgba_equal(g.read_rgba16f(), want_rgba, "RGB sibling composite")
+    g.close()
