@@ -1044,3 +1044,30 @@ def test_carry_off_matches(monkeypatch):
     assert_photons_equal(gpu.read_photons(), cpu.photons, "carry off")
     assert_rgba_equal(gpu.read_rgba16f(), want, "carry off")
     gpu.close()
+
+
+def test_carry_screen_filling_volume(monkeypatch):
+    """Carry with every tile in the volume (the 'near' camera fills the screen:
+    256 volume tiles on 64 SIMDs, so no SIMD holds a lone volume wave): the
+    lag deal keeps the plain order, no launch stops early, every tile has
+    exactly one wave slot, and photons and images stay bit-exact. (Before the
+    fix the lone-slot count underflowed here and two tiles could share a slot.)"""
+    monkeypatch.setenv("VPTMCM_CARRY", "1")
+    R = 128
+    gpu, cpu = make_pair(R, cf.fbm_volume(96, 19, nthreads=8), cf.tf_spectral(), ext=24.0)
+    mvp = cf.golden_mvp("near")
+    seeds = cf.seed_stream(70, start=11)
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0], nthreads=16)
+    for s in seeds[1:]:
+        gpu.render(mvp, s)
+        rgb, want = cpu.render(mvp, s, nthreads=16)
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "carry, screen-filling volume")
+    assert_rgba_equal(gpu.read_rgba16f(), want, "carry, screen-filling volume")
+    assert_rgb32_equal(gpu.read_rgb(), rgb, "carry, screen-filling volume")
+    slots = gpu.debug_schedule()
+    dealt = slots[slots != 0xFFFFFFFF]
+    tiles = dealt & 0x1FFFFFFF
+    assert len(tiles) == (R // 8) ** 2 and len(np.unique(tiles)) == len(tiles), "one slot per tile"
+    assert ((dealt >> 31) == 1).all(), "every tile entered the volume"
+    gpu.close()

@@ -87,12 +87,16 @@ def main():
             "paired_not_owing_complete": q(end[hot & (nl == 2) & (owing == 0) & ~stopped]),
             "paired_stopped": q(end[hot & (nl >= 2) & stopped]),
             "lone_stopped": q(end[hot & (nl == 1) & stopped]),
-            "background": q(end[~hot])}
+            "background": q(end[~hot]),
+            "background_beside_pairs": q(end[~hot & (nl >= 2)]),
+            "background_beside_lone": q(end[~hot & (nl == 1)])}
         out["passes_done"] = {"lone": q(done[hot & (nl == 1)]), "paired": q(done[hot & (nl == 2)])}
         out["simd_load"] = {int(v): int((np.array(list(load.values())) == v).sum()) for v in set(load.values())}
     else:
         out["loop_end"] = {"lone": q(end[vol & (nl == 1)]), "paired": q(end[vol & (nl == 2)]),
-                           "background": q(end[~vol])}
+                           "background": q(end[~vol]),
+                           "background_beside_pairs": q(end[~vol & (nl >= 2)]),
+                           "background_beside_lone": q(end[~vol & (nl == 1)])}
     print(json.dumps(out))
 
 

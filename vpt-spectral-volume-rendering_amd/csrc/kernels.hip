@@ -19,6 +19,9 @@
 #ifndef VPT_OWE_PRIO
 #define VPT_OWE_PRIO 1  // carry: the owing wave of a pair takes the higher issue priority
 #endif
+#ifndef VPT_KO_BG
+#define VPT_KO_BG 0  // experiment only (wrong images): background waves of paired CUs skip their passes
+#endif
 #ifndef VPT_PRIO
 #define VPT_PRIO 1  // s_setprio level of volume waves (0 = off); 11 % faster passes
 #endif
@@ -277,6 +280,12 @@ __device__ __forceinline__ void deal_slot(uint32_t slot, uint32_t G, uint32_t lb
 // (it also takes the higher issue priority). Returns the slot's packed tile
 // (tile | volume << 31 | lag bucket << 29) and the launch's stop quota in *q
 // (the lone slot count, 0 without pairs).
+#if VPT_KO_BG
+#define KO_NV(v) \
+  if (threadIdx.x == 0u) s_tile[16] = (v)
+#else
+#define KO_NV(v)
+#endif
 __device__ uint32_t schedule_tile_lag(uint32_t n, uint32_t f, uint32_t lb, uint32_t* s_red,
                                       uint32_t* s_tile, uint32_t* q) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6, G = gridDim.x;
@@ -304,9 +313,12 @@ __device__ uint32_t schedule_tile_lag(uint32_t n, uint32_t f, uint32_t lb, uint3
     }
   }
   const uint32_t nv = tot[0] + tot[1] + tot[2] + tot[3];
-  const uint32_t pairs = nv > 4u * G ? nv - 4u * G : 0u, lone = 4u * G - pairs;
-  const bool remap = pairs > 0u && (tot[0] + tot[1] + tot[2]) > 0u;
-  if (q) *q = pairs > 0u ? lone : 0u;
+  // pairs >= 4G (two or more volume waves on every SIMD): no lone SIMDs, no
+  // remap and no early stop
+  const uint32_t pairs = nv > 4u * G ? nv - 4u * G : 0u, lone = pairs < 4u * G ? 4u * G - pairs : 0u;
+  const bool remap = pairs > 0u && lone > 0u && (tot[0] + tot[1] + tot[2]) > 0u;
+  if (q) *q = (pairs > 0u && lone > 0u) ? lone : 0u;
+  KO_NV(nv);
   // running rank inside each class, and the volume tiles before this lane's four
   uint32_t seen[4];
   uint32_t ones = 0u;
@@ -382,6 +394,7 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
       total += t;
     }
     if (n <= kSchedChunk) nv = total;
+    KO_NV(nv);
     uint32_t ones = before + pre;  // volume tiles before tile base + 4*tid
 #pragma unroll
     for (uint32_t q = 0; q < 4u; q++) {
@@ -496,7 +509,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __shared__ uint32_t s_binlut[LUTB ? kBinLutCells + kBinLutCells / 4 : 1];  // MODE 6 / 7
 
   __shared__ uint32_t s_red[64];
-  __shared__ uint32_t s_tile[16];
+  __shared__ uint32_t s_tile[VPT_KO_BG ? 17 : 16];
 
   TL_DECL();
   TL_MARK(0);
@@ -563,6 +576,12 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     const uint32_t owed = PS.base + kSeedWindow - tn[tile];
     todo = owed <= kSeedWindow ? owed : PS.n;
   }
+#if VPT_KO_BG
+  if (P.sched != 1u && !hot0) {  // a CU whose four SIMDs all hold two volume waves
+    const uint32_t nv = s_tile[16], pairs = nv > 4u * gridDim.x ? nv - 4u * gridDim.x : 0u;
+    if (blockIdx.x * 4u + 4u <= pairs) todo = 0u;
+  }
+#endif
   todo = __builtin_amdgcn_readfirstlane(todo);
   const uint32_t first = kSeedWindow - todo;  // window index of the tile's first pass
   const uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
