@@ -955,7 +955,8 @@ def test_c3_driver_shaped_launch_bitexact():
     gpu.close()
 
 
-def test_carry_owed_passes_bitexact_c3(monkeypatch):
+@pytest.mark.parametrize("bg", ["0", "1"])
+def test_carry_owed_passes_bitexact_c3(bg, monkeypatch):
     """Cross-launch balancing (VPTMCM_CARRY=1) on C3 itself (512^3, R = 512): render() calls queue
     32-pass launches that may end early, volume waves stopping at a pass
     boundary once the lone SIMDs' waves reach the target and owing the rest;
@@ -963,8 +964,11 @@ def test_carry_owed_passes_bitexact_c3(monkeypatch):
     tiles owe passes (at most 32, a pass window); a read then runs every tile
     to the last queued pass, and photons, fp32 and rgba16f images are bit-exact
     against 72 oracle passes. render_passes(72) in one call (the bench's
-    region shape) is bit-exact too."""
+    region shape) is bit-exact too. bg = 1 (VPTMCM_CARRY_BG): background waves
+    stop at the same signal and background tiles owe passes as well, dealt by
+    what they owe (most owing to the CUs without SIMD pairs)."""
     monkeypatch.setenv("VPTMCM_CARRY", "1")
+    monkeypatch.setenv("VPTMCM_CARRY_BG", bg)
     R = 512
     vol, tf, mvp = cf.fbm_volume(512, 512, nthreads=8), cf.tf_spectral(), cf.default_mvp_inverse()
     gpu, cpu = make_pair(R, vol, tf, ext=32.0)
@@ -975,6 +979,12 @@ def test_carry_owed_passes_bitexact_c3(monkeypatch):
         gpu.render(mvp, s)
     owed = gpu.debug_owed()  # launches the 65th pass too, keeping what is owed
     assert owed.max() <= 32 and (owed > 0).sum() > 100, (owed.max(), (owed > 0).sum())
+    if bg == "1":  # the tiles dealt as background (the schedule of that launch) owe passes too
+        slots = gpu.debug_schedule()  # (completes the owed passes)
+        dealt = slots[slots != 0xFFFFFFFF]
+        background = np.zeros(owed.size, bool)
+        background[dealt[(dealt >> 31) == 0] & 0x1FFFFFFF] = True
+        assert (owed[background] > 0).sum() > 100, (owed[background] > 0).sum()
     for s in seeds[66:]:
         gpu.render(mvp, s)
     for s in seeds[1:]:

@@ -90,12 +90,13 @@ for s in $STEPS; do
       (cd /tmp && export TMPDIR=/tmp VPTMCM_CARRY=$c && timeout -k 10 300 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$OUT/cprobe_$c" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/carry_probe.py" > "$GRAFT_REPO_ROOT/$OUT/cprobe_$c.jsonl" 2> "$GRAFT_REPO_ROOT/$OUT/cprobe_$c.err")
       rc=$?; echo "carryprobe $c rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
     done ;;
-  carrysweep)  # lib:carry cases (lib 'cur' = the product library; carry 0, 1, q<N> = VPTMCM_STOP_Q)
+  carrysweep)  # lib:carry cases (lib 'cur' = the product library; carry 0, 1, q<N> = VPTMCM_STOP_Q, b = 1 with VPTMCM_CARRY_BG=1)
     for cs in ${SWEEP_CASES:-cur:0 cur:1}; do
       lib=${cs%%:*}; c=${cs#*:}
-      case $c in q*) cv=1; q=${c#q}; f=0;; f) cv=1; q=1000000; f=1;; *) cv=$c; q=0; f=0;; esac
+      bgv=0
+      case $c in q*) cv=1; q=${c#q}; f=0;; f) cv=1; q=1000000; f=1;; b) cv=1; q=0; f=0; bgv=1;; *) cv=$c; q=0; f=0;; esac
       if [ $lib = cur ]; then unset VPTMCM_LIB; else export VPTMCM_LIB=$lib; fi
-      VPTMCM_CARRY=$cv VPTMCM_STOP_Q=$q VPTMCM_CARRY_FORCE=$f timeout -k 10 300 python bench.py --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 256 --unfused-steps 0 > $OUT/cs.json 2>> $OUT/carrysweep.err
+      VPTMCM_CARRY=$cv VPTMCM_CARRY_BG=$bgv VPTMCM_STOP_Q=$q VPTMCM_CARRY_FORCE=$f timeout -k 10 300 python bench.py --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 256 --unfused-steps 0 > $OUT/cs.json 2>> $OUT/carrysweep.err
       rc=$?; unset VPTMCM_LIB; [ $rc -ne 0 ] && { echo "carrysweep rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
       python3 -c "import json; d=json.load(open('$OUT/cs.json')); print(json.dumps({'case': '$cs', 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'render_api': d['render_api']['value']}))" >> $OUT/carrysweep.jsonl
     done

@@ -286,30 +286,55 @@ __device__ __forceinline__ void deal_slot(uint32_t slot, uint32_t G, uint32_t lb
 #else
 #define KO_NV(v)
 #endif
+// With bg (MarchParams::bg_lag) the background tiles are classed the same way
+// and dealt most owing first to the background slots of the CUs without pairs
+// (group 1-3 slots at positions >= pairs), the least owing to the paired CUs'
+// group 2-3 slots (positions < pairs): those SIMDs already run two volume waves.
 __device__ uint32_t schedule_tile_lag(uint32_t n, uint32_t f, uint32_t lb, uint32_t* s_red,
-                                      uint32_t* s_tile, uint32_t* q) {
+                                      uint32_t* s_tile, uint32_t* q, bool bg) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6, G = gridDim.x;
-  uint32_t cc = 0u;  // per class (k = 3 - bucket) the lane's count, 4 bits each
+  uint32_t cc = 0u, cb = 0u;  // per class (k = 3 - bucket) the lane's count, 4 bits each
 #pragma unroll
   for (uint32_t b = 0; b < 4u; b++) {
     const uint32_t fb = (f >> (8u * b)) & 0xffu;
-    if (fb & kFlagVolume) cc += 1u << (4u * (3u - ((fb >> kLagShift) & 3u)));
+    const uint32_t one = 1u << (4u * (3u - ((fb >> kLagShift) & 3u)));
+    if (fb & kFlagVolume) cc += one;
+    else if (4u * tid + b < n) cb += one;
   }
-  uint32_t pre[4], wt[4];
+  uint32_t pre[4], wt[4], preb[4] = {0u, 0u, 0u, 0u}, wtb[4];
 #pragma unroll
   for (uint32_t k = 0; k < 4u; k++) pre[k] = wave_scan_small((cc >> (4u * k)) & 0xfu, wt[k]);
+  if (bg) {
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) preb[k] = wave_scan_small((cb >> (4u * k)) & 0xfu, wtb[k]);
+  }
   if (lane == 0u) {
 #pragma unroll
     for (uint32_t k = 0; k < 4u; k++) s_red[4u * w + k] = wt[k];
+    if (bg) {
+#pragma unroll
+      for (uint32_t k = 0; k < 4u; k++) s_red[64u + 4u * w + k] = wtb[k];
+    }
   }
   __syncthreads();
   uint32_t before[4] = {0u, 0u, 0u, 0u}, tot[4] = {0u, 0u, 0u, 0u};
+  uint32_t beforeb[4] = {0u, 0u, 0u, 0u}, totb[4] = {0u, 0u, 0u, 0u};
   for (uint32_t v = 0; v < 16u; v++) {
 #pragma unroll
     for (uint32_t k = 0; k < 4u; k++) {
       const uint32_t t = s_red[4u * v + k];
       before[k] += (v < w) ? t : 0u;
       tot[k] += t;
+    }
+  }
+  if (bg) {
+    for (uint32_t v = 0; v < 16u; v++) {
+#pragma unroll
+      for (uint32_t k = 0; k < 4u; k++) {
+        const uint32_t t = s_red[64u + 4u * v + k];
+        beforeb[k] += (v < w) ? t : 0u;
+        totb[k] += t;
+      }
     }
   }
   const uint32_t nv = tot[0] + tot[1] + tot[2] + tot[3];
@@ -320,14 +345,17 @@ __device__ uint32_t schedule_tile_lag(uint32_t n, uint32_t f, uint32_t lb, uint3
   if (q) *q = (pairs > 0u && lone > 0u) ? lone : 0u;
   KO_NV(nv);
   // running rank inside each class, and the volume tiles before this lane's four
-  uint32_t seen[4];
+  uint32_t seen[4], seenb[4];
   uint32_t ones = 0u;
 #pragma unroll
   for (uint32_t k = 0; k < 4u; k++) {
     seen[k] = before[k] + pre[k];
+    seenb[k] = beforeb[k] + preb[k];
     ones += seen[k];
   }
   const uint32_t base1 = tot[0], base2 = tot[0] + tot[1], base3 = base2 + tot[2];
+  const uint32_t bb1 = totb[0], bb2 = totb[0] + totb[1], bb3 = bb2 + totb[2];
+  const bool bgdeal = bg && pairs > 0u && lone > 0u;
 #pragma unroll
   for (uint32_t b = 0; b < 4u; b++) {
     const uint32_t t = 4u * tid + b;
@@ -339,6 +367,16 @@ __device__ uint32_t schedule_tile_lag(uint32_t n, uint32_t f, uint32_t lb, uint3
         const uint32_t r = (k == 0u ? seen[0] : k == 1u ? base1 + seen[1] : k == 2u ? base2 + seen[2]
                                                                                : base3 + seen[3]);
         slot = !remap ? r : (r < lone ? pairs + r : (r < 4u * G ? r - lone : r));
+      } else if (bgdeal) {
+        const uint32_t r = (k == 0u ? seenb[0] : k == 1u ? bb1 + seenb[1] : k == 2u ? bb2 + seenb[2]
+                                                                         : bb3 + seenb[3]);
+        if (r < 3u * lone) {  // group 1..3, positions [pairs, 4G)
+          const uint32_t g = r / lone;
+          slot = (1u + g) * 4u * G + pairs + (r - g * lone);
+        } else {  // group 2..3, positions [0, pairs)
+          const uint32_t r2 = r - 3u * lone, g = r2 / pairs;
+          slot = (2u + g) * 4u * G + (r2 - g * pairs);
+        }
       } else {
         slot = nv + (t - ones);
       }
@@ -348,6 +386,9 @@ __device__ uint32_t schedule_tile_lag(uint32_t n, uint32_t f, uint32_t lb, uint3
 #pragma unroll
       for (uint32_t j = 0; j < 4u; j++) seen[j] += (j == k) ? 1u : 0u;
       ones++;
+    } else if (t < n) {
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; j++) seenb[j] += (j == k) ? 1u : 0u;
     }
   }
   __syncthreads();  // s_tile complete
@@ -367,7 +408,8 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
   const uint32_t lb = P.sched == 2u ? xcd_swizzle(blockIdx.x, G) : blockIdx.x;
   const uint32_t* f4 = reinterpret_cast<const uint32_t*>(flags);  // flag bytes, padded to kSchedChunk
   if (tid < 16u) s_tile[tid] = 0xffffffffu;  // idle unless a tile is dealt to it
-  if (LAG && P.lag_sched && n <= kSchedChunk) return schedule_tile_lag(n, f0, lb, s_red, s_tile, stop_q);
+  if (LAG && P.lag_sched && n <= kSchedChunk)
+    return schedule_tile_lag(n, f0, lb, s_red, s_tile, stop_q, P.bg_lag != 0u);
   uint32_t nv = 0u;  // number of volume tiles; one chunk (R <= 512): the scan's total
   if (n > kSchedChunk) {
     if (tid == 0u) s_red[16] = 0u;
@@ -508,7 +550,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __shared__ uint32_t s_rowmap[256];  // P.tf_dedup: density row -> first texel of its distinct row
   __shared__ uint32_t s_binlut[LUTB ? kBinLutCells + kBinLutCells / 4 : 1];  // MODE 6 / 7
 
-  __shared__ uint32_t s_red[64];
+  __shared__ uint32_t s_red[CARRY ? 128 : 64];
   __shared__ uint32_t s_tile[VPT_KO_BG ? 17 : 16];
 
   TL_DECL();
@@ -712,11 +754,11 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     rb = rbpix;
   };
   const uint32_t n_passes = todo;
-  // early stop (MarchParams::allow_stop): a volume wave ends the launch at a
-  // pass boundary once stop_q volume waves have reached the target; the
-  // counter is read one pass ahead (lane 0, coherent across the XCDs) so its
-  // latency hides in the pass
-  const bool stop_ok = CARRY && P.allow_stop && hot0 && stop_q != 0u;
+  // early stop (MarchParams::allow_stop): a volume wave (with bg_lag any wave)
+  // ends the launch at a pass boundary once stop_q volume waves have reached
+  // the target; the counter is read one pass ahead (lane 0, coherent across
+  // the XCDs) so its latency hides in the pass
+  const bool stop_ok = CARRY && P.allow_stop && (hot0 || P.bg_lag) && stop_q != 0u;
   uint32_t ctr_v = 0u, done_passes = n_passes;
   for (uint32_t pass = 0; pass < n_passes; pass++) {
   if (stop_ok) {
@@ -1001,7 +1043,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     T.flags_out[tile] = (entered ? kFlagVolume : 0u) | (bucket << kLagShift);
     if (CARRY) T.tile_next[tile] = PS.base + first + done_passes;
   }
-  if (stop_ok && n_passes == done_passes) {
+  if (stop_ok && hot0 && n_passes == done_passes) {
     // count the completion; the one that reaches the quota raises the 64 flag lines
     uint32_t old = 0u;
     if (lane == 0u) old = __hip_atomic_fetch_add(T.stop_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -110,8 +110,10 @@ struct MarchParams {
   // volume wave may end its launch at a pass boundary once stop_q volume waves
   // (0: the lone SIMD slots of the deal) have reached the target, owing the
   // rest to the next launch; lag_sched deals the owing tiles first (the
-  // previous launch allowed stops).
-  uint32_t carry, allow_stop, stop_q, lag_sched;
+  // previous launch allowed stops). bg_lag: background waves stop at the same
+  // signal, and the background tiles are dealt by what they owe too, the most
+  // owing to the CUs without SIMD pairs.
+  uint32_t carry, allow_stop, stop_q, lag_sched, bg_lag;
 };
 constexpr uint32_t kBinLutCells = 1024u;
 constexpr uint32_t kBinLutShift = 22u;
