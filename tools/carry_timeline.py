@@ -12,6 +12,7 @@ volume-wave count. Reports the loop-end times by class.
     VPTMCM_LIB=tl VPTMCM_CARRY_NOFINAL=1 VPTMCM_CARRY=1 python tools/carry_timeline.py
 """
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -76,7 +77,7 @@ def main():
     load = dict(zip(ids.tolist(), cnt.tolist()))
     nl = np.array([load.get(int(s), 0) for s in simd])
     end = tt[:, 3]
-    out = {"carry": carry, "launches": L, "waves": int(len(w)), "span_us": round(float(tt[:, 4].max()), 1),
+    out = {"carry": carry, "carry_bg": os.environ.get("VPTMCM_CARRY_BG", "0"), "launches": L, "waves": int(len(w)), "span_us": round(float(tt[:, 4].max()), 1),
            "owed_after": {"tiles": int((owed > 0).sum()), "total": int(owed.sum())}}
     if carry:
         stopped = hot & (done < todo)

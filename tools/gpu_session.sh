@@ -102,8 +102,9 @@ for s in $STEPS; do
     done
     echo "carrysweep rc=0" | tee -a $OUT/status.txt; cat $OUT/carrysweep.jsonl ;;
   ctl)  # per-wave timeline of the last carry launch vs a plain one (VPT_STAMP=2 build 'tl')
-    for c in 1 0; do
-      VPTMCM_LIB=tl VPTMCM_CARRY_NOFINAL=1 VPTMCM_CARRY=$c timeout -k 10 300 python tools/carry_timeline.py 12 >> $OUT/ctl.jsonl 2>> $OUT/ctl.err
+    for c in ${CTL_CASES:-1 0 b}; do  # b: carry with VPTMCM_CARRY_BG=1
+      case $c in b) cv=1; bgv=1;; *) cv=$c; bgv=0;; esac
+      VPTMCM_LIB=tl VPTMCM_CARRY_NOFINAL=1 VPTMCM_CARRY=$cv VPTMCM_CARRY_BG=$bgv timeout -k 10 300 python tools/carry_timeline.py 12 >> $OUT/ctl.jsonl 2>> $OUT/ctl.err
       rc=$?; echo "ctl $c rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
     done; cat $OUT/ctl.jsonl ;;
   counters)
