@@ -91,7 +91,10 @@ def main():
             "background": q(end[~hot]),
             "background_beside_pairs": q(end[~hot & (nl >= 2)]),
             "background_beside_lone": q(end[~hot & (nl == 1)])}
-        out["passes_done"] = {"lone": q(done[hot & (nl == 1)]), "paired": q(done[hot & (nl == 2)])}
+        out["passes_done"] = {"lone": q(done[hot & (nl == 1)]), "paired": q(done[hot & (nl == 2)]),
+                              "background_beside_pairs": q(done[~vol & (nl >= 2)]),
+                              "background_beside_lone": q(done[~vol & (nl == 1)])}
+        out["background_stopped"] = int((~vol & (todo > 0) & (done < todo)).sum())
         out["simd_load"] = {int(v): int((np.array(list(load.values())) == v).sum()) for v in set(load.values())}
     else:
         out["loop_end"] = {"lone": q(end[vol & (nl == 1)]), "paired": q(end[vol & (nl == 2)]),
