@@ -107,6 +107,14 @@ for s in $STEPS; do
       VPTMCM_LIB=tl VPTMCM_CARRY_NOFINAL=1 VPTMCM_CARRY=$cv VPTMCM_CARRY_BG=$bgv timeout -k 10 300 python tools/carry_timeline.py 12 >> $OUT/ctl.jsonl 2>> $OUT/ctl.err
       rc=$?; echo "ctl $c rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
     done; cat $OUT/ctl.jsonl ;;
+  hullab)  # robust-miss pixels by the projected hull vs the box only (VPTMCM_LIB=nohull), orbit camera
+    for lib in ${HULL_LIBS:-nohull cur nohull cur}; do
+      if [ $lib = cur ]; then unset VPTMCM_LIB; else export VPTMCM_LIB=$lib; fi
+      timeout -k 10 300 python bench.py --camera ${HULL_CAMERA:-orbit} --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 0 --unfused-steps 0 > $OUT/hull_$lib.json 2>> $OUT/hullab.err
+      rc=$?; unset VPTMCM_LIB; [ $rc -ne 0 ] && { echo "hullab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      python3 -c "import json; d=json.load(open('$OUT/hull_$lib.json')); print(json.dumps({'lib': '$lib', 'camera': '${HULL_CAMERA:-orbit}', 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass']}))" >> $OUT/hullab.jsonl
+    done
+    echo "hullab rc=0" | tee -a $OUT/status.txt; cat $OUT/hullab.jsonl ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)

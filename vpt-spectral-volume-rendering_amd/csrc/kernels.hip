@@ -19,6 +19,9 @@
 #ifndef VPT_OWE_PRIO
 #define VPT_OWE_PRIO 1  // carry: the owing wave of a pair takes the higher issue priority
 #endif
+#ifndef VPT_RB_HULL
+#define VPT_RB_HULL 1  // robust-miss pixels beyond the projected hull's edges too (0: the box only)
+#endif
 #ifndef VPT_KO_BG
 #define VPT_KO_BG 0  // experiment only (wrong images): background waves of paired CUs skip their passes
 #endif
@@ -507,6 +510,17 @@ __device__ __forceinline__ const __attribute__((address_space(4))) float* cmf_ta
                                                                offsetof(MarchParams, xb)) / 4);
 }
 
+// A pixel centre outside the robust-miss box or beyond one of the hull edges
+// (MarchParams::rb_edge; unused edges never qualify).
+__device__ __forceinline__ bool robust_pixel(const MarchParams& P, float sx, float sy) {
+  bool out = sx < P.rb_x0 || sx > P.rb_x1 || sy < P.rb_y0 || sy > P.rb_y1;
+  if (VPT_RB_HULL) {
+#pragma unroll
+    for (int e = 0; e < kRbEdges; e++) out = out || fmaf(P.rb_edge[e][0], sx, P.rb_edge[e][1] * sy) > P.rb_edge[e][2];
+  }
+  return out;
+}
+
 // MODE: 0 generic; 1 every radiance bin in use (nb >= 12); 2 (FAST, the
 // benchmark configuration) additionally equal-width bins (bin_of's arithmetic
 // path), a wavelength-invariant TF blue channel (LDS row table), blur == 0 with
@@ -702,8 +716,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   // whose lanes are all in that state (background tiles) skips the distance
   // log, the advance, the bounds test and the ray-start slab test, and
   // materialises the start point once, at the end of the launch.
-  const bool rbpix = P.robust != 0u && fixed &&
-                     (sx < P.rb_x0 || sx > P.rb_x1 || sy < P.rb_y0 || sy > P.rb_y1);
+  const bool rbpix = P.robust != 0u && fixed && robust_pixel(P, sx, sy);
   bool rb = false, stale = false;
   // add_radiance of a termination is deferred to the start of the next step
   // (it only touches the radiance bins, applied in the same order),
@@ -1170,8 +1183,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
   bool entered = false;
   // robust-miss pixels, as in k_march: once reset with this launch's matrix
   // their rays miss the cube by a margin, so every later step is an exit
-  const bool rbpix = P.robust != 0u && fixed &&
-                     (sx < P.rb_x0 || sx > P.rb_x1 || sy < P.rb_y0 || sy > P.rb_y1);
+  const bool rbpix = P.robust != 0u && fixed && robust_pixel(P, sx, sy);
   bool rb = false, stale = false;
 
   for (uint32_t pass = 0; pass < PS.n; pass++) {

@@ -49,6 +49,8 @@ enum Plane : uint32_t {
 enum RgbPlane : uint32_t { kTr0 = 8, kRgbRad0 = 11, kRgbPlanes = 14 };
 constexpr uint32_t kRgbTfMax = 4096;  // TF texels staged in LDS (row 0, decoded float4)
 
+constexpr int kRbEdges = 8;  // MarchParams::rb_edge (a projected box has at most 6 hull edges)
+
 struct MarchParams {
   float m[16];           // mvpInverse, column-major
   float inv_res[2];      // 1/R as f32 (js:297)
@@ -79,10 +81,14 @@ struct MarchParams {
                          // the XCDs), 1 raster, 2 scheduled XCD by XCD (round 2's order)
   // Robust-miss screen region (NDC, host-derived from the forward matrix):
   // with blur 0, every ray of a pixel whose centre lies outside
-  // [rb_x0, rb_x1] x [rb_y0, rb_y1] misses the unit cube by a margin, so each
-  // of its steps is an exit (see k_march's robust path).
+  // [rb_x0, rb_x1] x [rb_y0, rb_y1], or beyond one of the rb_edge lines
+  // (a * sx + b * sy > c: the edges of the convex hull of the expanded cube's
+  // projected corners, padded; unused edges have c = FLT_MAX), misses the unit
+  // cube by a margin, so each of its steps is an exit (see k_march's robust
+  // path; robust_pixel).
   uint32_t robust;
   float rb_x0, rb_x1, rb_y0, rb_y1;
+  float rb_edge[kRbEdges][3];
   uint32_t R, tiles_x, n_tiles, npad;
   uint32_t band_y0, band_y1;  // pixel rows [band_y0, band_y1) this renderer owns (Mode B)
   uint32_t W, H, D;

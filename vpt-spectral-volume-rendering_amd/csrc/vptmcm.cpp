@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -213,7 +214,10 @@ float srgb_to_linear(uint8_t b) {
 // computed photon position on the ray is outside [0,1]^3: each step is an
 // exit. Computed in double from the f32 matrix; returns the screen bounds
 // outside of which pixel centres qualify, or false (no robust pixels).
-bool robust_region(const float* m32, float ir, float rb[4]) {
+// edge[kRbEdges][3] receives the hull lines of the same expanded corners'
+// projections (counter-clockwise, outward normal (a, b) with |a| + |b| = 1):
+// a * sx + b * sy > c qualifies a pixel centre too, c padded like the box.
+bool robust_region(const float* m32, float ir, float rb[4], float (*edge)[3]) {
   double M[16], F[16];
   for (int i = 0; i < 16; i++) M[i] = m32[i];  // column-major: M[col * 4 + row]
   auto mul = [](const double* A, double x, double y, double z, double o[4]) {
@@ -254,7 +258,7 @@ bool robust_region(const float* m32, float ir, float rb[4]) {
   for (int r = 0; r < 4; r++)
     for (int c = 0; c < 4; c++) F[c * 4 + r] = A[r][4 + c];
   const double delta = 1e-3 * (1.0 + maxnear) + 1e-6 * maxfar;
-  double x0 = 1e300, x1 = -1e300, y0 = 1e300, y1 = -1e300;
+  double x0 = 1e300, x1 = -1e300, y0 = 1e300, y1 = -1e300, px[8], py[8];
   for (int c = 0; c < 8; c++) {
     mul(F, (c & 1) ? 1.0 + delta : -delta, (c & 2) ? 1.0 + delta : -delta,
         (c & 4) ? 1.0 + delta : -delta, o);
@@ -265,12 +269,47 @@ bool robust_region(const float* m32, float ir, float rb[4]) {
     x1 = nx > x1 ? nx : x1;
     y0 = ny < y0 ? ny : y0;
     y1 = ny > y1 ? ny : y1;
+    px[c] = nx;
+    py[c] = ny;
   }
   const double pad = (double)ir + 1e-4;
   rb[0] = std::nextafter((float)(x0 - pad), -INFINITY);
   rb[1] = std::nextafter((float)(x1 + pad), INFINITY);
   rb[2] = std::nextafter((float)(y0 - pad), -INFINITY);
   rb[3] = std::nextafter((float)(y1 + pad), INFINITY);
+  for (int e = 0; e < kRbEdges; e++) edge[e][0] = edge[e][1] = 0.0f, edge[e][2] = FLT_MAX;
+  // convex hull of the eight projections (monotone chain, counter-clockwise)
+  int idx[8], hull[16], nh = 0;
+  for (int k = 0; k < 8; k++) idx[k] = k;
+  std::sort(idx, idx + 8, [&](int a, int b) { return px[a] < px[b] || (px[a] == px[b] && py[a] < py[b]); });
+  auto cross = [&](int o_, int a, int b) {
+    return (px[a] - px[o_]) * (py[b] - py[o_]) - (py[a] - py[o_]) * (px[b] - px[o_]);
+  };
+  for (int k = 0; k < 8; k++) {  // lower chain
+    while (nh >= 2 && cross(hull[nh - 2], hull[nh - 1], idx[k]) <= 0.0) nh--;
+    hull[nh++] = idx[k];
+  }
+  for (int k = 6, lo = nh + 1; k >= 0; k--) {  // upper chain
+    while (nh >= lo && cross(hull[nh - 2], hull[nh - 1], idx[k]) <= 0.0) nh--;
+    hull[nh++] = idx[k];
+  }
+  nh--;  // the last point repeats the first
+  if (nh < 3 || nh > kRbEdges) return true;  // degenerate: the box alone
+  for (int e = 0; e < nh; e++) {
+    const int a = hull[e], b = hull[(e + 1) % nh];
+    double nx = py[b] - py[a], ny = px[a] - px[b];  // outward for a counter-clockwise hull
+    const double l1 = std::fabs(nx) + std::fabs(ny);
+    if (!(l1 > 0.0)) return true;
+    nx /= l1;
+    ny /= l1;
+    double cmax = -1e300;  // the support of every corner (rounding of the hull)
+    for (int k = 0; k < 8; k++) cmax = std::max(cmax, nx * px[k] + ny * py[k]);
+    // the kernel's f32 evaluation of a * sx + b * sy (|sx|, |sy| <= 1, a and b
+    // rounded to f32) errs by < 1e-6: far inside the 1e-4 of the pad
+    edge[e][0] = (float)nx;
+    edge[e][1] = (float)ny;
+    edge[e][2] = std::nextafter((float)(cmax + pad), INFINITY);
+  }
   return true;
 }
 
@@ -356,7 +395,9 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
   for (int k = 0; k < 4; k++) P.env[k] = h->env[k];
   float rb[4];
   P.robust = (P.blur == 0.0f && P.rcp_extinction > 0.0f && std::isfinite(P.rcp_extinction) &&
-              robust_region(mvp, P.inv_res[0], rb)) ? 1u : 0u;
+              robust_region(mvp, P.inv_res[0], rb, P.rb_edge)) ? 1u : 0u;
+  if (!P.robust)
+    for (int e = 0; e < kRbEdges; e++) P.rb_edge[e][0] = P.rb_edge[e][1] = 0.0f, P.rb_edge[e][2] = FLT_MAX;
   if (P.robust) {
     P.rb_x0 = rb[0];
     P.rb_x1 = rb[1];
