@@ -930,19 +930,13 @@ def test_c5_1024_volume_streamed_rows_against_oracle():
     gpu.close()
 
 
-@pytest.mark.parametrize("bg_ratio", [None, "2.6", "5"])
-def test_c3_driver_shaped_launch_bitexact(bg_ratio, monkeypatch):
+def test_c3_driver_shaped_launch_bitexact():
     """The benchmarked launch shape itself: BASELINE C3
     (512^3 fBm seed 512, spectral TF, R = 512, S = 8, 12 bins, extinction 32,
     default camera) from a reset, the driver's 5 warm-up passes as one launch,
     then its timed `--steps 20` region as ONE 20-pass fused launch (the FAST
     MODE 2 kernel on CORNER8), with the bench's own seed stream: photons, the
-    fp32 image and the rgba16f image bit-exact against the oracle. bg_ratio
-    (VPTMCM_BG_RATIO): background doubling, some waves of the CUs without SIMD
-    pairs marching a second background tile (C3 has 576 pairs: ~400 second
-    tiles at 2.6, ~1000 of the paired CUs' 1152 background tiles at 5)."""
-    if bg_ratio is not None:
-        monkeypatch.setenv("VPTMCM_BG_RATIO", bg_ratio)
+    fp32 image and the rgba16f image bit-exact against the oracle."""
     R, S = 512, 8
     vol, tf, mvp = cf.fbm_volume(512, 512, nthreads=8), cf.tf_spectral(), cf.default_mvp_inverse()
     gpu, cpu = make_pair(R, vol, tf, ext=32.0, steps=S)

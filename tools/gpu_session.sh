@@ -115,16 +115,6 @@ for s in $STEPS; do
       python3 -c "import json; d=json.load(open('$OUT/hull_$lib.json')); print(json.dumps({'lib': '$lib', 'camera': '${HULL_CAMERA:-orbit}', 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass']}))" >> $OUT/hullab.jsonl
     done
     echo "hullab rc=0" | tee -a $OUT/status.txt; cat $OUT/hullab.jsonl ;;
-  dblab)  # background doubling (VPTMCM_BG_RATIO) on the default line and the driver's line, alternating
-    for r in ${DBL_RATIOS:-0 2.6 4 0 2.6 4}; do
-      if [ $r = 0 ]; then unset VPTMCM_BG_RATIO; else export VPTMCM_BG_RATIO=$r; fi
-      timeout -k 10 300 python bench.py --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 0 --unfused-steps 0 > $OUT/dbl_$r.json 2>> $OUT/dblab.err
-      rc=$?; [ $rc -ne 0 ] && { echo "dblab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
-      timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 > $OUT/dbld_$r.json 2>> $OUT/dblab.err
-      rc=$?; unset VPTMCM_BG_RATIO; [ $rc -ne 0 ] && { echo "dblab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
-      python3 -c "import json; d=json.load(open('$OUT/dbl_$r.json')); e=json.load(open('$OUT/dbld_$r.json')); print(json.dumps({'bg_ratio': '$r', 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'drv_value': e['value'], 'drv_kernel_us': e['roofline']['kernel_avg_us']}))" >> $OUT/dblab.jsonl
-    done
-    echo "dblab rc=0" | tee -a $OUT/status.txt; cat $OUT/dblab.jsonl ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)

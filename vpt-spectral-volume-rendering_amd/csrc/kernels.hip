@@ -398,17 +398,9 @@ __device__ uint32_t schedule_tile_lag(uint32_t n, uint32_t f, uint32_t lb, uint3
   return s_tile[w];
 }
 
-// Background doubling (MarchParams::bg_ratio > 0, one chunk, plain deal): with
-// SIMD pairs, the background tiles go first to the background slots of the
-// CUs without pairs (three per SIMD), then M of them as a second tile of those
-// slots (s_tile2: the wave marches it after its first), the rest to the paired
-// CUs' group 2-3 slots. M balances the issue work of a paired SIMD (two volume
-// waves + x background tiles) against a lone one (one volume wave + y): with
-// a = bg_ratio the work of a volume tile in background tiles, y - x = a.
 template <bool LAG = false>
 __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8_t* __restrict__ flags,
-                                  uint32_t* s_red, uint32_t* s_tile, uint32_t* stop_q = nullptr,
-                                  uint32_t* s_tile2 = nullptr) {
+                                  uint32_t* s_red, uint32_t* s_tile, uint32_t* stop_q = nullptr) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
   const uint32_t n = P.n_tiles, G = gridDim.x;
   // Consecutive slots go to consecutive hardware blocks, i.e. round-robin over
@@ -419,7 +411,6 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
   const uint32_t lb = P.sched == 2u ? xcd_swizzle(blockIdx.x, G) : blockIdx.x;
   const uint32_t* f4 = reinterpret_cast<const uint32_t*>(flags);  // flag bytes, padded to kSchedChunk
   if (tid < 16u) s_tile[tid] = 0xffffffffu;  // idle unless a tile is dealt to it
-  if (s_tile2 && tid < 16u) s_tile2[tid] = 0xffffffffu;
   if (LAG && P.lag_sched && n <= kSchedChunk)
     return schedule_tile_lag(n, f0, lb, s_red, s_tile, stop_q, P.bg_lag != 0u);
   uint32_t nv = 0u;  // number of volume tiles; one chunk (R <= 512): the scan's total
@@ -449,43 +440,17 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
     }
     if (n <= kSchedChunk) nv = total;
     KO_NV(nv);
-    // background doubling (see above): M second tiles on the lone CUs' slots
-    const uint32_t pairs = nv > 4u * G ? nv - 4u * G : 0u, lone = pairs < 4u * G ? 4u * G - pairs : 0u;
-    const uint32_t nb = n - nv;
-    uint32_t M = 0u;
-    if (s_tile2 && P.bg_ratio > 0.0f && n <= kSchedChunk && pairs > 0u && lone > 0u && nb > 3u * lone) {
-      const float mf = (P.bg_ratio - 3.0f + (float)(nb - 3u * lone) / (float)pairs) /
-                       (1.0f / (float)lone + 1.0f / (float)pairs);
-      const uint32_t cap = min(3u * lone, nb - 3u * lone);
-      M = mf <= 0.0f ? 0u : min((uint32_t)mf, cap);
-    }
     uint32_t ones = before + pre;  // volume tiles before tile base + 4*tid
 #pragma unroll
     for (uint32_t q = 0; q < 4u; q++) {
       const uint32_t t = base + 4u * tid + q;
       const uint32_t fl = (f >> (8u * q)) & 1u;
       if (t < n) {
-        uint32_t slot = fl ? ones : nv + (t - ones);
-        uint32_t* dst = s_tile;
-        if (!fl && M != 0u) {
-          const uint32_t r = t - ones;  // background rank
-          uint32_t j = r;               // lone-CU background slot (group 1..3, positions [pairs, 4G))
-          if (r >= 3u * lone + M) {     // the paired CUs' group 2-3 slots
-            const uint32_t r2 = r - 3u * lone - M, g = r2 / pairs;
-            slot = (2u + g) * 4u * G + (r2 - g * pairs);
-          } else {
-            if (r >= 3u * lone) {  // the second tile of lone-CU slot j
-              j = r - 3u * lone;
-              dst = s_tile2;
-            }
-            const uint32_t g = j / lone;
-            slot = (1u + g) * 4u * G + pairs + (j - g * lone);
-          }
-        }
+        const uint32_t slot = fl ? ones : nv + (t - ones);
         const uint32_t k = slot / (4u * G), rem = slot - k * 4u * G;
         if ((rem >> 2) == lb) {
           const uint32_t j = rem & 3u;
-          dst[4u * j + ((k + j) & 3u)] = t | (fl << 31);
+          s_tile[4u * j + ((k + j) & 3u)] = t | (fl << 31);
         }
       }
       ones += fl;
@@ -569,9 +534,8 @@ __device__ __forceinline__ bool robust_pixel(const MarchParams& P, float sx, flo
 // tf_b4 gather).
 // CARRY: cross-launch balancing (MarchParams::carry; the per-tile pass window,
 // the early stop and the owing waves' priority); without it the kernel is the
-// plain n-pass launch. DBL: background doubling (MarchParams::bg_ratio; a wave
-// may march a second, background tile after its first).
-template <uint32_t L, bool SPEC, uint32_t MODE, bool CARRY, bool DBL = false>
+// plain n-pass launch.
+template <uint32_t L, bool SPEC, uint32_t MODE, bool CARRY>
 __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const MarchParams P,
                                                        const TileSched T, float* __restrict__ ph,
                                                        const uint8_t* __restrict__ vol,
@@ -602,7 +566,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 
   __shared__ uint32_t s_red[CARRY ? 128 : 64];
   __shared__ uint32_t s_tile[VPT_KO_BG ? 17 : 16];
-  __shared__ uint32_t s_tile2[DBL ? 16 : 1];  // background doubling: the slot's second tile
 
   TL_DECL();
   TL_MARK(0);
@@ -644,13 +607,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   bool have = false;  // p already holds this tile's state (the slot's tile did not change)
   bool owing = false;  // the tile owes passes of earlier launches (lag bucket > 0)
   uint32_t stop_q = 0u;
-  uint32_t tile2 = 0xffffffffu;  // background doubling: a second (background) tile after the first
   // the next launch's stop block: its counter (word 0) and its 64 flag lines
   if (CARRY && blockIdx.x == 0u && threadIdx.x <= kStopFlagLines) T.stop_ctr_next[kStopLineWords * threadIdx.x] = 0u;
   if (P.sched != 1u) {
-    const uint32_t s = __builtin_amdgcn_readfirstlane(
-        schedule_tile<CARRY>(P, f0, T.flags_in, s_red, s_tile, &stop_q, DBL ? s_tile2 : nullptr));
-    if (DBL) tile2 = __builtin_amdgcn_readfirstlane(s_tile2[threadIdx.x >> 6]);
+    const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile<CARRY>(P, f0, T.flags_in, s_red, s_tile, &stop_q));
     tile = s == 0xffffffffu ? s : s & kSlotTileMask;
     hot0 = s != 0xffffffffu && (s >> 31) != 0u;
     owing = CARRY && s != 0xffffffffu && ((s >> 29) & 3u) != 0u;
@@ -679,12 +639,12 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   }
 #endif
   todo = __builtin_amdgcn_readfirstlane(todo);
-  uint32_t first = kSeedWindow - todo;  // window index of the tile's first pass
-  uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
-  uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
-  size_t i = (size_t)tile * 64u + lane;
+  const uint32_t first = kSeedWindow - todo;  // window index of the tile's first pass
+  const uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
+  const uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
+  const size_t i = (size_t)tile * 64u + lane;
   // tiles outside the band (whole tiles: band rows are multiples of 8) are idle
-  bool live = tile != 0xffffffffu && x < P.R && y < P.R && y >= P.band_y0 && y < P.band_y1;
+  const bool live = tile != 0xffffffffu && x < P.R && y < P.R && y >= P.band_y0 && y < P.band_y1;
   bool entered = false;  // wave-uniform: some lane of this wave was inside the volume
   STAMP_BEGIN();
   // The TF copy into LDS (global_load_lds, issued at entry) is complete for
@@ -724,18 +684,13 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       if (threadIdx.x + k * kMarchBlock < kLutWords) s_binlut[threadIdx.x + k * kMarchBlock] = binlut_v[k];
   }
   __syncthreads();
-  // per tile: the slot's tile, then (DBL) its second, background tile; without
-  // DBL there is no back edge (a loop here costs the plain kernel 15 VGPRs)
-  bool second = false;
-tile_body:
-  {
   if (live && !hot0) load_photon(ph, S, i, p);
   TL_MARK_WAIT(2);
   if (!live || todo == 0u) {
     // an idle out-of-band tile; or a tile with no pass owed (a completion
     // launch): its flag carries over
     if (tile < P.n_tiles && lane == 0u) T.flags_out[tile] = (live && hot0) ? kFlagVolume : 0u;
-    goto tile_done;
+    return;
   }
   const uint16_t* s_tf = reinterpret_cast<const uint16_t*>(s_tf4);
 
@@ -1110,21 +1065,6 @@ tile_body:
   }
   STAMP_END(rgb32, tile, entered);
   TL_END(rgb32, tile, entered, CARRY ? ((n_passes << 16) | (done_passes << 8) | (owing ? 1u : 0u)) : 0u);
-  }  // tile
-tile_done:
-  if (DBL && !second && tile2 != 0xffffffffu) {
-    second = true;
-    tile = tile2 & kSlotTileMask;  // a background tile: no state in flight, the launch's n passes
-    hot0 = have = owing = false;
-    todo = PS.n;
-    first = kSeedWindow - todo;
-    x = (tile % P.tiles_x) * 8u + (lane & 7u);
-    y = (tile / P.tiles_x) * 8u + (lane >> 3);
-    i = (size_t)tile * 64u + lane;
-    live = x < P.R && y < P.R && y >= P.band_y0 && y < P.band_y1;
-    entered = false;
-    goto tile_body;
-  }
 }
 
 
@@ -1516,10 +1456,6 @@ hipError_t launch_reset(const MarchParams& P, float* ph, hipStream_t s) {
   return hipGetLastError();
 }
 
-// The march instances that carry a background-doubling variant (DBL): the
-// FAST spectral configuration only.
-constexpr bool dbl_mode(bool spec, uint32_t mode) { return spec && mode == 2u; }
-
 hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P, const PassSeeds& PS,
                         const TileSched& T, float* ph, const uint8_t* vol, const uint16_t* tf_rg, const uint32_t* tf_b4,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba, float* rgb32,
@@ -1560,14 +1496,13 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   if (info) *info = MarchLaunchInfo{mode, tpl, spec ? 1u : 0u, PS.n};
   // hipExtLaunchKernelGGL stamps the events from the dispatch packet itself
   // (no extra barrier/marker packets between back-to-back launches)
-#define VPT_LAUNCH_C(LAY, SP, MO, CA, DB)                                                              \
-  hipExtLaunchKernelGGL((k_march<LAY, SP, MO, CA, DB>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
+#define VPT_LAUNCH_C(LAY, SP, MO, CA)                                                              \
+  hipExtLaunchKernelGGL((k_march<LAY, SP, MO, CA>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
                         PS, Q, T, ph, vol, tf_lds, tf_b4, tf_brow, light, rgba, rgb32, rowmap, bin_lut)
-#define VPT_LAUNCH(LAY, SP, MO)                                                      \
-  do {                                                                               \
-    if (SP && Q.carry) VPT_LAUNCH_C(LAY, SP, MO, SP, false);                         \
-    else if (dbl_mode(SP, MO) && Q.bg_ratio > 0.0f) VPT_LAUNCH_C(LAY, SP, MO, false, dbl_mode(SP, MO)); \
-    else VPT_LAUNCH_C(LAY, SP, MO, false, false);                                    \
+#define VPT_LAUNCH(LAY, SP, MO)                                   \
+  do {                                                            \
+    if (SP && Q.carry) VPT_LAUNCH_C(LAY, SP, MO, SP);             \
+    else VPT_LAUNCH_C(LAY, SP, MO, false);                        \
   } while (0)
 #define VPT_LAUNCH_NB(LAY)                 \
   do {                                     \

@@ -120,10 +120,6 @@ struct MarchParams {
   // signal, and the background tiles are dealt by what they owe too, the most
   // owing to the CUs without SIMD pairs.
   uint32_t carry, allow_stop, stop_q, lag_sched, bg_lag;
-  // Background doubling (plain scheduled launches, one chunk; 0 = off): the
-  // issue work of a volume tile in background tiles, from which the schedule
-  // sizes the second tiles it gives the lone CUs' background waves.
-  float bg_ratio;
 };
 constexpr uint32_t kBinLutCells = 1024u;
 constexpr uint32_t kBinLutShift = 22u;
