@@ -930,13 +930,18 @@ def test_c5_1024_volume_streamed_rows_against_oracle():
     gpu.close()
 
 
-def test_c3_driver_shaped_launch_bitexact():
+@pytest.mark.parametrize("dark", [None, "1"])
+def test_c3_driver_shaped_launch_bitexact(dark, monkeypatch):
     """The benchmarked launch shape itself: BASELINE C3
     (512^3 fBm seed 512, spectral TF, R = 512, S = 8, 12 bins, extinction 32,
     default camera) from a reset, the driver's 5 warm-up passes as one launch,
     then its timed `--steps 20` region as ONE 20-pass fused launch (the FAST
     MODE 2 kernel on CORNER8), with the bench's own seed stream: photons, the
-    fp32 image and the rgba16f image bit-exact against the oracle."""
+    fp32 image and the rgba16f image bit-exact against the oracle. dark = 1
+    (VPTMCM_DARK): the background waves the light never reaches run the draw
+    chain alone."""
+    if dark is not None:
+        monkeypatch.setenv("VPTMCM_DARK", dark)
     R, S = 512, 8
     vol, tf, mvp = cf.fbm_volume(512, 512, nthreads=8), cf.tf_spectral(), cf.default_mvp_inverse()
     gpu, cpu = make_pair(R, vol, tf, ext=32.0, steps=S)
@@ -1080,4 +1085,36 @@ def test_carry_screen_filling_volume(monkeypatch):
     tiles = dealt & 0x1FFFFFFF
     assert len(tiles) == (R // 8) ** 2 and len(np.unique(tiles)) == len(tiles), "one slot per tile"
     assert ((dealt >> 31) == 1).all(), "every tile entered the volume"
+    gpu.close()
+
+
+def test_dark_background_light_and_camera_changes(monkeypatch):
+    """VPTMCM_DARK=1 where its conditions change between launches without a
+    reset: the light flips from +x to -x (lit pixels' bins are no longer zero,
+    dark ones become lit), then the camera moves (the stored photons come from
+    the old camera: the launch's first step decides). Every launch bit-exact
+    against the oracle, photons and both images."""
+    monkeypatch.setenv("VPTMCM_DARK", "1")
+    R = 128
+    vol, tf = cf.fbm_volume(96, 21, nthreads=8), cf.tf_spectral()
+    gpu, cpu = make_pair(R, vol, tf, ext=24.0)
+    spd = np.full(256, 100, np.uint8)
+    seeds = cf.seed_stream(60, start=3)
+    mvp1, mvp2 = cf.default_mvp_inverse(), cf.golden_mvp("orbit")
+    gpu.reset(mvp1, seeds[0])
+    cpu.reset(mvp1, seeds[0], nthreads=16)
+    k = 1
+    for light, mvp, n in (((1, 0, 0), mvp1, 12), ((-1, 0, 0), mvp1, 12), ((-1, 0, 0), mvp2, 12),
+                          ((0.6, 0.0, -0.8), mvp2, 12)):
+        ld = np.asarray(light, np.float32)
+        gpu.set_light(spd, ld)
+        cpu.light, cpu.light_dir = spd, ld
+        gpu.render_passes(mvp, seeds[k:k + n])
+        for s in seeds[k:k + n]:
+            rgb, want = cpu.render(mvp, s, nthreads=16)
+        k += n
+        what = f"dark, light {light}"
+        assert_photons_equal(gpu.read_photons(), cpu.photons, what)
+        assert_rgb32_equal(gpu.read_rgb(), rgb, what)
+        assert_rgba_equal(gpu.read_rgba16f(), want, what)
     gpu.close()

@@ -115,6 +115,16 @@ for s in $STEPS; do
       python3 -c "import json; d=json.load(open('$OUT/hull_$lib.json')); print(json.dumps({'lib': '$lib', 'camera': '${HULL_CAMERA:-orbit}', 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass']}))" >> $OUT/hullab.jsonl
     done
     echo "hullab rc=0" | tee -a $OUT/status.txt; cat $OUT/hullab.jsonl ;;
+  darkab)  # dark-background chain (VPTMCM_DARK=1) on the default line and the driver's line, alternating
+    for d in ${DARK_CASES:-0 1 0 1 0 1}; do
+      if [ $d = 1 ]; then export VPTMCM_DARK=1; else unset VPTMCM_DARK; fi
+      timeout -k 10 300 python bench.py --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 0 --unfused-steps 64 > $OUT/dark_$d.json 2>> $OUT/darkab.err
+      rc=$?; [ $rc -ne 0 ] && { echo "darkab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 > $OUT/darkd_$d.json 2>> $OUT/darkab.err
+      rc=$?; unset VPTMCM_DARK; [ $rc -ne 0 ] && { echo "darkab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      python3 -c "import json; d=json.load(open('$OUT/dark_$d.json')); e=json.load(open('$OUT/darkd_$d.json')); print(json.dumps({'dark': '$d', 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'unfused_us': d['unfused']['kernel_avg_us'], 'drv_value': e['value'], 'drv_kernel_us': e['roofline']['kernel_avg_us']}))" >> $OUT/darkab.jsonl
+    done
+    echo "darkab rc=0" | tee -a $OUT/status.txt; cat $OUT/darkab.jsonl ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)

@@ -773,6 +773,89 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   // the XCDs) so its latency hides in the pass
   const bool stop_ok = CARRY && P.allow_stop && (hot0 || P.bg_lag) && stop_q != 0u;
   uint32_t ctr_v = 0u, done_passes = n_passes;
+  auto write_image = [&]() {
+    float X = 0.0f, Y = 0.0f, Z = 0.0f;
+    {
+      const auto cmf = cmf_table();  // xb[12], yb[12], zb[12]
+#pragma unroll
+      for (int b = 0; b < kMaxBins; b++) {
+        if (NBF || VPT_NB_ZERO || (uint32_t)b < P.nb) {
+          X = fmaf(p.rad[b], cmf[b], X);
+          Y = fmaf(p.rad[b], cmf[kMaxBins + b], Y);
+          Z = fmaf(p.rad[b], cmf[2 * kMaxBins + b], Z);
+        }
+      }
+    }
+    float r = fmaf(-0.498536f, Z, fmaf(-1.537150f, Y, 3.240479f * X));
+    float g = fmaf(0.041556f, Z, fmaf(1.875990f, Y, -0.969255f * X));
+    float bl = fmaf(1.057311f, Z, fmaf(-0.204041f, Y, 0.055647f * X));
+    uint2 px;
+    px.x = (uint32_t)f2h(r) | ((uint32_t)f2h(g) << 16);
+    px.y = (uint32_t)f2h(bl) | (0x3c00u << 16);
+    reinterpret_cast<uint2*>(rgba)[(size_t)y * P.R + x] = px;
+    if (!VPT_STAMP) {  // fp32 before the f16 store (read_rgb, k_pack)
+      float* o = rgb32 + ((size_t)y * P.R + x) * 3u;
+      o[0] = r;
+      o[1] = g;
+      o[2] = bl;
+    }
+  };
+  // Dark background (MarchParams::dark, FAST geometry): a wave whose every
+  // lane (a) is a robust-miss pixel, (b) has all radiance bins +0, (c) exits
+  // at the launch's first step with zero radiance and (d) sees the directional
+  // light from behind for every ray of its pixel (cos < -1e-3 at the four
+  // corners of the jitter square: the sign of (far - near) . L is affine over
+  // it) adds only +0 samples all launch, and a +0 sample leaves +0 bins +0
+  // (fma(fma(oh, +-0, -0), inv, +0) = +0). Such a wave runs the draw chain
+  // alone: each step is the robust path's exit and reset, of which only the
+  // sample count and the last reset's direction, wavelength and bin are
+  // observable.
+  bool dark = false;
+  if constexpr (GEO && !CARRY) {
+    if (P.dark != 0u && __builtin_amdgcn_ballot_w64(!rbpix) == 0ull && n_passes != 0u && P.steps != 0u) {
+      bool ok = true;
+#pragma unroll
+      for (int b = 0; b < kMaxBins; b++) ok = ok && __float_as_uint(p.rad[b]) == 0u;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const float u = (c & 1) ? 1.0f : -1.0f, v = (c & 2) ? 1.0f : -1.0f;
+        const f3 to = unproject(P.m, fmaf(u, P.inv_res[0], sx), fmaf(v, P.inv_res[1], sy), 1.0f);
+        const float dx = to.x - from.x, dy = to.y - from.y, dz = to.z - from.z;
+        const float cl = fmaf(dz, P.light_dir[2], fmaf(dy, P.light_dir[1], dx * P.light_dir[0]));
+        ok = ok && cl < -1e-3f * (__builtin_fabsf(dx) + __builtin_fabsf(dy) + __builtin_fabsf(dz));
+      }
+      {  // the launch's first step, as the general path computes it
+        const uint32_t s1 = pcg_hash(hash3(x, y, pass_seed(first)));
+        const float dist = -spec_log_unit(s1) * P.rcp_extinction;
+        const float qx = fmaf(dist, p.dir.x, p.pos.x), qy = fmaf(dist, p.dir.y, p.pos.y),
+                    qz = fmaf(dist, p.dir.z, p.pos.z);
+        const float qmax = __builtin_fmaxf(__builtin_fmaxf(qx, qy), qz);
+        const float qmin = __builtin_fminf(__builtin_fminf(qx, qy), qz);
+        ok = ok && (qmax > 1.0f || qmin < 0.0f) && exit_radiance<GEO>(P, p.dir, wc) == 0.0f;
+      }
+      dark = __builtin_amdgcn_ballot_w64(!ok) == 0ull;
+    }
+  }
+  if (dark) {
+    uint32_t h3 = 0u, h4 = 0u, h5 = 0u;
+    for (uint32_t pass = 0; pass < n_passes; pass++) {
+      uint32_t st = hash3(x, y, pass_seed(first + pass));
+      for (uint32_t step = 0; step < P.steps; step++) {
+        const uint32_t s1 = pcg_hash(st), sw = pcg_hash(s1), h1 = pcg_hash(sw), h2 = pcg_hash(h1);
+        h3 = pcg_hash(h2);
+        h4 = pcg_hash(h3);
+        h5 = pcg_hash(h4);
+        st = h5;
+      }
+      p.samples += P.steps;
+    }
+    p.dir = ray_dir_from_draws(P, sx, sy, from, h3, h4);
+    p.bounces = 0u;
+    p.lambda = lambda_of(P, h5);
+    p.bin = bin_of_draw<UNIB, LUTB>(P, p.lambda, h5, s_binlut);
+    stale = true;
+    write_image();
+  } else {
   for (uint32_t pass = 0; pass < n_passes; pass++) {
   if (stop_ok) {
     if (pass > 0u && __builtin_amdgcn_readfirstlane(ctr_v) != 0u && n_passes - pass <= kMaxFusedPasses) {
@@ -1013,34 +1096,9 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   // for the launch's last pass only: the passes of one launch are queued
   // render() calls with no read between them, so only the last image is
   // observable (2.3 % per pass at 32 passes per launch).
-  if (pass + 1u == n_passes) {
-  float X = 0.0f, Y = 0.0f, Z = 0.0f;
-  {
-    const auto cmf = cmf_table();  // xb[12], yb[12], zb[12]
-#pragma unroll
-    for (int b = 0; b < kMaxBins; b++) {
-      if (NBF || VPT_NB_ZERO || (uint32_t)b < P.nb) {
-        X = fmaf(p.rad[b], cmf[b], X);
-        Y = fmaf(p.rad[b], cmf[kMaxBins + b], Y);
-        Z = fmaf(p.rad[b], cmf[2 * kMaxBins + b], Z);
-      }
-    }
-  }
-  float r = fmaf(-0.498536f, Z, fmaf(-1.537150f, Y, 3.240479f * X));
-  float g = fmaf(0.041556f, Z, fmaf(1.875990f, Y, -0.969255f * X));
-  float bl = fmaf(1.057311f, Z, fmaf(-0.204041f, Y, 0.055647f * X));
-  uint2 px;
-  px.x = (uint32_t)f2h(r) | ((uint32_t)f2h(g) << 16);
-  px.y = (uint32_t)f2h(bl) | (0x3c00u << 16);
-  reinterpret_cast<uint2*>(rgba)[(size_t)y * P.R + x] = px;
-  if (!VPT_STAMP) {  // fp32 before the f16 store (read_rgb, k_pack)
-    float* o = rgb32 + ((size_t)y * P.R + x) * 3u;
-    o[0] = r;
-    o[1] = g;
-    o[2] = bl;
-  }
-  }
+  if (pass + 1u == n_passes) write_image();
   }  // pass
+  }  // not dark
   TL_MARK(3);
   if (CARRY && done_passes != n_passes) apply_pending();  // an early stop (the last pass applies its own)
 

@@ -120,6 +120,9 @@ struct MarchParams {
   // signal, and the background tiles are dealt by what they owe too, the most
   // owing to the CUs without SIMD pairs.
   uint32_t carry, allow_stop, stop_q, lag_sched, bg_lag;
+  // Dark background (k_march, FAST geometry, plain launches): waves whose every
+  // sample is provably +0 run the draw chain alone (VPTMCM_DARK).
+  uint32_t dark;
 };
 constexpr uint32_t kBinLutCells = 1024u;
 constexpr uint32_t kBinLutShift = 22u;
