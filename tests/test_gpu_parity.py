@@ -930,18 +930,17 @@ def test_c5_1024_volume_streamed_rows_against_oracle():
     gpu.close()
 
 
-@pytest.mark.parametrize("dark", [None, "1"])
+@pytest.mark.parametrize("dark", ["0", "1"])
 def test_c3_driver_shaped_launch_bitexact(dark, monkeypatch):
     """The benchmarked launch shape itself: BASELINE C3
     (512^3 fBm seed 512, spectral TF, R = 512, S = 8, 12 bins, extinction 32,
     default camera) from a reset, the driver's 5 warm-up passes as one launch,
     then its timed `--steps 20` region as ONE 20-pass fused launch (the FAST
     MODE 2 kernel on CORNER8), with the bench's own seed stream: photons, the
-    fp32 image and the rgba16f image bit-exact against the oracle. dark = 1
-    (VPTMCM_DARK): the background waves the light never reaches run the draw
-    chain alone."""
-    if dark is not None:
-        monkeypatch.setenv("VPTMCM_DARK", dark)
+    fp32 image and the rgba16f image bit-exact against the oracle, with the
+    dark-background chain (the default: background waves the light never
+    reaches run the draw chain alone) and without it (VPTMCM_DARK=0)."""
+    monkeypatch.setenv("VPTMCM_DARK", dark)
     R, S = 512, 8
     vol, tf, mvp = cf.fbm_volume(512, 512, nthreads=8), cf.tf_spectral(), cf.default_mvp_inverse()
     gpu, cpu = make_pair(R, vol, tf, ext=32.0, steps=S)
@@ -1089,7 +1088,7 @@ def test_carry_screen_filling_volume(monkeypatch):
 
 
 def test_dark_background_light_and_camera_changes(monkeypatch):
-    """VPTMCM_DARK=1 where its conditions change between launches without a
+    """The dark-background chain where its conditions change between launches without a
     reset: the light flips from +x to -x (lit pixels' bins are no longer zero,
     dark ones become lit), then the camera moves (the stored photons come from
     the old camera: the launch's first step decides). Every launch bit-exact

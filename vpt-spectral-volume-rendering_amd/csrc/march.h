@@ -121,7 +121,7 @@ struct MarchParams {
   // owing to the CUs without SIMD pairs.
   uint32_t carry, allow_stop, stop_q, lag_sched, bg_lag;
   // Dark background (k_march, FAST geometry, plain launches): waves whose every
-  // sample is provably +0 run the draw chain alone (VPTMCM_DARK).
+  // sample is provably +0 run the draw chain alone (on by default; VPTMCM_DARK=0).
   uint32_t dark;
 };
 constexpr uint32_t kBinLutCells = 1024u;
