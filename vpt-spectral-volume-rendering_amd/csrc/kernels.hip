@@ -811,8 +811,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   // sample count and the last reset's direction, wavelength and bin are
   // observable.
   bool dark = false;
-  if constexpr (GEO && !CARRY) {
-    if (P.dark != 0u && __builtin_amdgcn_ballot_w64(!rbpix) == 0ull && n_passes != 0u && P.steps != 0u) {
+  if constexpr (GEO) {
+    // (carry: not when background waves may stop early, MarchParams::bg_lag)
+    if (P.dark != 0u && !(CARRY && P.bg_lag) && __builtin_amdgcn_ballot_w64(!rbpix) == 0ull &&
+        n_passes != 0u && P.steps != 0u) {
       bool ok = true;
 #pragma unroll
       for (int b = 0; b < kMaxBins; b++) ok = ok && __float_as_uint(p.rad[b]) == 0u;
