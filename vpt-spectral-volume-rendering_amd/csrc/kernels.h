@@ -46,6 +46,12 @@ struct TileSched {
 // bit 0 its wave entered the volume, bits 1-2 its lag bucket (passes it still
 // owes after the launch: 0, 1-3, 4-7, >= 8).
 constexpr uint32_t kFlagVolume = 1u, kLagShift = 1u;
+// The tile's wave took the dark-background chain (k_march): the next plain
+// deal gives such tiles the background slots beside SIMD pairs first.
+constexpr uint32_t kFlagDark = 8u;
+// Packed schedule word of a background tile in the plain deal with the dark
+// chain on: the tile was dark last launch.
+constexpr uint32_t kSlotDarkBit = 29u;
 // A launch's stop block (TileSched::stop_ctr): counter line + flag lines.
 constexpr uint32_t kStopFlagLines = 64u, kStopLineWords = 32u;
 constexpr uint32_t kStopBlockWords = (1u + kStopFlagLines) * kStopLineWords;

@@ -425,35 +425,70 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
     __syncthreads();
     nv = s_red[16];
   }
+  // Dark-first deal (plain launches with the dark chain, one chunk): the
+  // background tiles whose waves took the dark chain last launch (kFlagDark,
+  // ~70 instead of ~240 instructions per step) go first to the background
+  // slots beside SIMD pairs (group 2-3, positions < pairs), the others first
+  // to the CUs without pairs, so the paired SIMDs carry the cheap background.
+  const bool dk = !LAG && P.dark == 1u && n <= kSchedChunk;
   uint32_t run = 0u;  // volume tiles before this chunk
   for (uint32_t base = 0; base < n; base += kSchedChunk) {
-    const uint32_t f = (base == 0u ? f0 : f4[(base >> 2) + tid]) & 0x01010101u;
-    uint32_t wt;
+    const uint32_t fr = base == 0u ? f0 : f4[(base >> 2) + tid];
+    const uint32_t f = fr & 0x01010101u;
+    const uint32_t fd = dk ? ((fr >> 3) & 0x01010101u) & ~f : 0u;  // dark background tiles
+    uint32_t wt, wtd = 0u, pred = 0u;
     const uint32_t pre = wave_scan_small(__popc(f), wt);
-    if (lane == 0u) s_red[w] = wt;
+    if (dk) pred = wave_scan_small(__popc(fd), wtd);
+    if (lane == 0u) {
+      s_red[w] = wt;
+      if (dk) s_red[32u + w] = wtd;
+    }
     __syncthreads();
-    uint32_t before = run, total = 0u;
+    uint32_t before = run, total = 0u, dbefore = 0u, nd = 0u;
     for (uint32_t k = 0; k < 16u; k++) {
       uint32_t t = s_red[k];
       before += (k < w) ? t : 0u;
       total += t;
     }
+    if (dk) {
+      for (uint32_t k = 0; k < 16u; k++) {
+        const uint32_t t = s_red[32u + k];
+        dbefore += (k < w) ? t : 0u;
+        nd += t;
+      }
+    }
     if (n <= kSchedChunk) nv = total;
     KO_NV(nv);
+    const uint32_t pairs = nv > 4u * G ? nv - 4u * G : 0u, lone = pairs < 4u * G ? 4u * G - pairs : 0u;
+    const bool ddeal = dk && pairs > 0u && lone > 0u && nd > 0u;
     uint32_t ones = before + pre;  // volume tiles before tile base + 4*tid
+    uint32_t darks = dbefore + pred;  // dark background tiles before it
 #pragma unroll
     for (uint32_t q = 0; q < 4u; q++) {
       const uint32_t t = base + 4u * tid + q;
       const uint32_t fl = (f >> (8u * q)) & 1u;
+      const uint32_t fk = (fd >> (8u * q)) & 1u;
       if (t < n) {
-        const uint32_t slot = fl ? ones : nv + (t - ones);
+        uint32_t slot = fl ? ones : nv + (t - ones);
+        if (!fl && ddeal) {
+          // the background slot list: [beside pairs (2 pairs)] ++ [the other CUs (3 lone)]
+          const uint32_t r = fk ? darks : nd + (t - ones - darks);
+          if (r < 2u * pairs) {
+            const uint32_t g = r / pairs;
+            slot = (2u + g) * 4u * G + (r - g * pairs);
+          } else {
+            const uint32_t r2 = r - 2u * pairs, g = r2 / lone;
+            slot = (1u + g) * 4u * G + pairs + (r2 - g * lone);
+          }
+        }
         const uint32_t k = slot / (4u * G), rem = slot - k * 4u * G;
         if ((rem >> 2) == lb) {
           const uint32_t j = rem & 3u;
-          s_tile[4u * j + ((k + j) & 3u)] = t | (fl << 31);
+          s_tile[4u * j + ((k + j) & 3u)] = t | (fl << 31) | (fk << kSlotDarkBit);
         }
       }
       ones += fl;
+      darks += fk;
     }
     run += total;
     __syncthreads();  // s_red reused by the next chunk; s_tile complete after the last
@@ -645,7 +680,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   const size_t i = (size_t)tile * 64u + lane;
   // tiles outside the band (whole tiles: band rows are multiples of 8) are idle
   const bool live = tile != 0xffffffffu && x < P.R && y < P.R && y >= P.band_y0 && y < P.band_y1;
-  bool entered = false;  // wave-uniform: some lane of this wave was inside the volume
+  uint32_t entered = 0u;  // wave-uniform flag bits for the next schedule: kFlagVolume (a lane was inside the volume), kFlagDark (the dark chain)
   STAMP_BEGIN();
   // The TF copy into LDS (global_load_lds, issued at entry) is complete for
   // the block only after every wave has waited for its own share (LDS-DMA
@@ -856,6 +891,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     p.lambda = lambda_of(P, h5);
     p.bin = bin_of_draw<UNIB, LUTB>(P, p.lambda, h5, s_binlut);
     stale = true;
+    entered = kFlagDark;
     write_image();
   } else {
   for (uint32_t pass = 0; pass < n_passes; pass++) {
@@ -869,14 +905,14 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 #endif
   }
 #if VPT_PRIO
-  if (pass > 0u) hot = entered;
+  if (pass > 0u) hot = entered != 0u;
   if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) {
     if (CARRY && VPT_OWE_PRIO && owing) __builtin_amdgcn_s_setprio(VPT_PRIO + 1);  // the owing wave of a pair leads
     else __builtin_amdgcn_s_setprio(VPT_PRIO);
   } else {
     __builtin_amdgcn_s_setprio(0);
   }
-  entered = false;
+  entered = 0u;
 #endif
   uint32_t st = hash3(x, y, pass_seed(first + pass));  // wgsl:122 (state is not carried across passes)
 
@@ -952,7 +988,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         continue;
       }
 
-      entered = true;
+      entered = kFlagVolume;
       STAMP_AT(0);
       const VolTap vt = vol_fetch<L>(P, vol, p.pos);  // gather in flight from here
 
@@ -1051,7 +1087,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       float wheel = rnd_uniform(st);  // wgsl:141 (drawn before the branch either way)
       bool oob = p.pos.x > 1.0f || p.pos.y > 1.0f || p.pos.z > 1.0f || p.pos.x < 0.0f ||
                  p.pos.y < 0.0f || p.pos.z < 0.0f;
-      entered = entered || __builtin_amdgcn_ballot_w64(!oob) != 0ull;
+      if (__builtin_amdgcn_ballot_w64(!oob) != 0ull) entered = kFlagVolume;
 
       // sample_volume_color (wgsl:75-80); its value is unused when out of bounds.
       float pabs = 0.0f, pscat = 0.0f, fr = 0.0f;
@@ -1113,7 +1149,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   if (lane == 0u) {  // the next launch's schedule: volume flag and lag bucket
     const uint32_t owe = n_passes - done_passes;
     const uint32_t bucket = owe == 0u ? 0u : owe < 4u ? 1u : owe < 8u ? 2u : 3u;
-    T.flags_out[tile] = (entered ? kFlagVolume : 0u) | (bucket << kLagShift);
+    T.flags_out[tile] = entered | (bucket << kLagShift);
     if (CARRY) T.tile_next[tile] = PS.base + first + done_passes;
   }
   if (stop_ok && hot0 && n_passes == done_passes) {

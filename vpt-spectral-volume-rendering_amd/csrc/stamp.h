@@ -34,7 +34,7 @@
     if (lane == 0u) {                                                                    \
       uint32_t* _o = reinterpret_cast<uint32_t*>(out) + (size_t)(tile) * 8u;             \
       for (int _k = 0; _k < 5; _k++) _o[_k] = tl[_k];                                    \
-      _o[5] = ((entered) ? 1u : 0u) | ((__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xffu) << 8); \
+      _o[5] = ((uint32_t)(entered) & 1u) | ((__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xffu) << 8); \
       _o[6] = (extra) ? (uint32_t)(extra) : tl[5];                                       \
       _o[7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);                                 \
     }                                                                                    \
@@ -96,7 +96,7 @@
     if (lane == 0u) {                                                                    \
       uint32_t* _o = reinterpret_cast<uint32_t*>(out) + (size_t)(tile) * 8u;             \
       for (int _k = 0; _k < 5; _k++) _o[_k] = prof[_k];                                  \
-      _o[5] = ((entered) ? 1u : 0u) | ((__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xffu) << 8); \
+      _o[5] = ((uint32_t)(entered) & 1u) | ((__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xffu) << 8); \
       _o[6] = _rt;                                                                       \
       _o[7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);                                 \
     }                                                                                    \

@@ -88,7 +88,7 @@ struct vptmcm {
   // queued pass (flush_renders).
   bool carry_on = false;       // spectral, one schedule chunk, not disabled (VPTMCM_CARRY=0)
   bool carry_bg = false;       // VPTMCM_CARRY_BG=1: background tiles carry too (MarchParams::bg_lag)
-  bool dark = true;            // the dark-background chain (MarchParams::dark; VPTMCM_DARK=0: off)
+  uint32_t dark = 1;           // MarchParams::dark: 1 dark chain + dark-first deal, 2 chain only, 0 off (VPTMCM_DARK)
   bool carry_pending = false;  // a launch with early stops ran since all tiles were complete
   bool tile_next_stale = false;  // tile_next lags the launches (every tile is at pass_target)
   float carry_mvp[16] = {};    // the matrix of the owed passes
@@ -582,7 +582,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n, boo
   P.lag_sched = (carry && h->carry_pending) ? 1u : 0u;
   P.stop_q = h->stop_q;
   P.bg_lag = (carry && h->carry_bg) ? 1u : 0u;
-  P.dark = h->dark ? 1u : 0u;
+  P.dark = h->dark;
   hipEvent_t eb = nullptr, ee = nullptr;
   int rc = time_slot(h, &eb);
   if (rc) return rc;
@@ -1088,7 +1088,7 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
                   (h->variant & (1u | 2u | 128u)) == 0u;
   if (const char* v = getenv("VPTMCM_STOP_Q")) h->stop_q = (uint32_t)strtoul(v, nullptr, 10);
   if (const char* v = getenv("VPTMCM_CARRY_BG")) h->carry_bg = v[0] == '1';
-  if (const char* v = getenv("VPTMCM_DARK")) h->dark = v[0] != '0';
+  if (const char* v = getenv("VPTMCM_DARK")) h->dark = v[0] == '0' ? 0u : v[0] == '2' ? 2u : 1u;
   if (h->kind == VPTMCM_RENDERER_RGB) {  // WebGPUAbstractComputeRenderer.js:23-28
     static const uint8_t kDefaultTf[8] = {255, 0, 0, 0, 255, 0, 0, 255};
     if (vptmcm_set_transfer_function(h, kDefaultTf, 2, 1)) return fail(VPTMCM_EHIP);
