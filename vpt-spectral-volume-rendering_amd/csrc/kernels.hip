@@ -472,12 +472,14 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
         uint32_t slot = fl ? ones : nv + (t - ones);
         if (!fl && ddeal) {
           // the background slot list: [beside pairs (2 pairs)] ++ [the other CUs (3 lone)]
+          // (groups by compares: r < 2 pairs + 3 lone, no integer division in
+          // the schedule, which a one-pass launch waits for)
           const uint32_t r = fk ? darks : nd + (t - ones - darks);
           if (r < 2u * pairs) {
-            const uint32_t g = r / pairs;
+            const uint32_t g = r >= pairs ? 1u : 0u;
             slot = (2u + g) * 4u * G + (r - g * pairs);
           } else {
-            const uint32_t r2 = r - 2u * pairs, g = r2 / lone;
+            const uint32_t r2 = r - 2u * pairs, g = (r2 >= lone ? 1u : 0u) + (r2 >= 2u * lone ? 1u : 0u);
             slot = (1u + g) * 4u * G + pairs + (r2 - g * lone);
           }
         }
