@@ -715,14 +715,17 @@ def _expected_schedule(table: np.ndarray, n_tiles: int, xcd_by_xcd: bool = False
     return exp
 
 
-@pytest.mark.parametrize("R,variant", [(256, "0"), (512, "0"), (512, "128"), (1024, "0")])
-def test_tile_schedule_is_the_latin_square_deal(R, variant, monkeypatch):
+@pytest.mark.parametrize("R,variant,dark", [(256, "0", "1"), (512, "0", "1"), (512, "128", "1"), (1024, "0", "1"),
+                                            (256, "0", "2"), (512, "0", "2")])
+def test_tile_schedule_is_the_latin_square_deal(R, variant, dark, monkeypatch):
     """N2, checked directly: after each launch every tile ran on exactly one
     wave slot, volume tiles first, dealt over the slots exactly as
     schedule_tile's ballot / prefix scan intends (vptmcm_debug_schedule), in
     the XCD round-robin slot order and in round 2's XCD-by-XCD one (variant
-    bit 7); a camera change re-deals it."""
+    bit 7); a camera change re-deals it. dark = 2 (VPTMCM_DARK): the
+    dark-first deal of the background tiles."""
     monkeypatch.setenv("VPTMCM_MARCH_VARIANT", variant)
+    monkeypatch.setenv("VPTMCM_DARK", dark)
     gpu = vptmcm.Renderer(R, device=0)
     assert (gpu.debug_schedule() == 0xFFFFFFFF).all()  # fresh handle: no launch yet
     gpu.set_volume(cf.fbm_volume(128, 77))

@@ -116,7 +116,7 @@ for s in $STEPS; do
     done
     echo "hullab rc=0" | tee -a $OUT/status.txt; cat $OUT/hullab.jsonl ;;
   darkab)  # dark-background chain (VPTMCM_DARK=1) on the default line and the driver's line, alternating
-    for d in ${DARK_CASES:-0 1 0 1 0 1}; do  # VPTMCM_DARK values (0 off, 1 default, 2 chain only)
+    for d in ${DARK_CASES:-0 1 0 1 0 1}; do  # VPTMCM_DARK values (0 off, 1 the chain (default), 2 chain + dark-first deal)
       export VPTMCM_DARK=$d
       timeout -k 10 300 python bench.py --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 0 --unfused-steps 64 > $OUT/dark_$d.json 2>> $OUT/darkab.err
       rc=$?; [ $rc -ne 0 ] && { echo "darkab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }

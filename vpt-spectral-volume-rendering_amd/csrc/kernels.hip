@@ -425,12 +425,12 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
     __syncthreads();
     nv = s_red[16];
   }
-  // Dark-first deal (plain launches with the dark chain, one chunk): the
+  // Dark-first deal (MarchParams::dark == 2, plain launches, one chunk): the
   // background tiles whose waves took the dark chain last launch (kFlagDark,
   // ~70 instead of ~240 instructions per step) go first to the background
   // slots beside SIMD pairs (group 2-3, positions < pairs), the others first
   // to the CUs without pairs, so the paired SIMDs carry the cheap background.
-  const bool dk = !LAG && P.dark == 1u && n <= kSchedChunk;
+  const bool dk = !LAG && P.dark == 2u && n <= kSchedChunk;
   uint32_t run = 0u;  // volume tiles before this chunk
   for (uint32_t base = 0; base < n; base += kSchedChunk) {
     const uint32_t fr = base == 0u ? f0 : f4[(base >> 2) + tid];

@@ -121,9 +121,10 @@ struct MarchParams {
   // owing to the CUs without SIMD pairs.
   uint32_t carry, allow_stop, stop_q, lag_sched, bg_lag;
   // Dark background (k_march, FAST geometry): waves whose every sample is
-  // provably +0 run the draw chain alone; 1 (default) also deals the tiles that
-  // were dark first to the background slots beside SIMD pairs (plain deal),
-  // 2 the chain only, 0 off (VPTMCM_DARK).
+  // provably +0 run the draw chain alone (1, the default); 2 also deals the
+  // tiles that were dark first to the background slots beside SIMD pairs
+  // (plain deal; measured no faster, one-pass launches slower); 0 off
+  // (VPTMCM_DARK).
   uint32_t dark;
 };
 constexpr uint32_t kBinLutCells = 1024u;

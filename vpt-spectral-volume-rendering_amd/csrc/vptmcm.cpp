@@ -88,7 +88,7 @@ struct vptmcm {
   // queued pass (flush_renders).
   bool carry_on = false;       // spectral, one schedule chunk, not disabled (VPTMCM_CARRY=0)
   bool carry_bg = false;       // VPTMCM_CARRY_BG=1: background tiles carry too (MarchParams::bg_lag)
-  uint32_t dark = 1;           // MarchParams::dark: 1 dark chain + dark-first deal, 2 chain only, 0 off (VPTMCM_DARK)
+  uint32_t dark = 1;           // MarchParams::dark: 1 dark chain, 2 chain + dark-first deal, 0 off (VPTMCM_DARK)
   bool carry_pending = false;  // a launch with early stops ran since all tiles were complete
   bool tile_next_stale = false;  // tile_next lags the launches (every tile is at pass_target)
   float carry_mvp[16] = {};    // the matrix of the owed passes
