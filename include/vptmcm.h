@@ -349,20 +349,12 @@ int vptmcm_debug_last_launch(vptmcm* h, uint32_t info[4], uint64_t* launches);
 /* The tile schedule of the last spectral march launch (after launching any
  * queued render() passes): per wave slot (block * 16 + wave of the march grid)
  * the tile it ran, with bit 31 set when the tile entered the volume in the
- * launch before (the schedule's volume class) and bits 29-30 its lag bucket in
- * a cross-launch-balanced launch (0 otherwise), 0xffffffff for an idle slot.
+ * launch before (the schedule's volume class), 0xffffffff for an idle slot.
  * *n_slots receives the slot count; out (may be NULL to query the count)
  * must hold n_words >= *n_slots words. Only launches with the balanced
  * schedule (R <= 1024, not the raster variant) write it; a fresh handle reports
  * every slot idle. */
 int vptmcm_debug_schedule(vptmcm* h, uint32_t* out, uint32_t n_words, uint32_t* n_slots);
-
-/* Cross-launch balancing: per 8x8 tile (tile y/8 * ceil(R/8) +
- * x/8) the passes it still owes after the launches so far, launching any
- * queued render() passes first but NOT the owed ones (every other entry point
- * runs every tile to the last queued pass first). *n_tiles receives the tile
- * count; out (may be NULL) must hold n_words >= *n_tiles words. */
-int vptmcm_debug_owed(vptmcm* h, uint32_t* out, uint32_t n_words, uint32_t* n_tiles);
 
 /* Library version string. */
 const char* vptmcm_version(void);

@@ -59,14 +59,6 @@ for s in $STEPS; do
       NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,BOOTSTRAP timeout -k 10 90 tools/comm_diag $m > $OUT/comm_diag_$m.log 2>&1
       rc=$?; echo "commdiag $m rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
     done ;;
-  carryab)  # cross-launch balancing A/B on the default 1024-pass line (alternating, one box)
-    for c in ${CARRY_CASES:-0 1 0 1}; do  # 0 off, 1 on (quota: lone slots), q<N>: on with VPTMCM_STOP_Q=N
-      case $c in q*) cv=1; q=${c#q};; *) cv=$c; q=0;; esac
-      VPTMCM_CARRY=$cv VPTMCM_STOP_Q=$q timeout -k 10 300 python bench.py --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 256 --unfused-steps 0 > $OUT/carry_$c.json 2>> $OUT/carry.err
-      rc=$?; [ $rc -ne 0 ] && { echo "carryab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
-      python3 -c "import json; d=json.load(open('$OUT/carry_$c.json')); print(json.dumps({'carry': '$c', 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'render_api': d['render_api']['value']}))" >> $OUT/carryab.jsonl
-    done
-    echo "carryab rc=0" | tee -a $OUT/status.txt; cat $OUT/carryab.jsonl ;;
   wallsplit)  # the driver's exact command under a kernel trace + host clocks of its timed region
     (cd /tmp && export TMPDIR=/tmp VPTMCM_BENCH_STAMPS="$GRAFT_REPO_ROOT/$OUT/stamps.json" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/drvprof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 > "$GRAFT_REPO_ROOT/$OUT/drvprof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/drvprof.err")
     rc=$?; echo "wallsplit rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
@@ -85,28 +77,6 @@ for s in $STEPS; do
   ingest_r03)
     VPTMCM_LIB=r03 timeout -k 10 300 python tools/ingest_time.py > $OUT/ingest_r03.jsonl 2> $OUT/ingest_r03.err
     rc=$?; echo "ingest_r03 rc=$rc" | tee -a $OUT/status.txt; cat $OUT/ingest_r03.jsonl; fault $rc && exit $rc ;;
-  carryprobe)  # launch-by-launch owed passes and kernel-trace durations, carry on and off
-    for c in 1 0; do
-      (cd /tmp && export TMPDIR=/tmp VPTMCM_CARRY=$c && timeout -k 10 300 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$OUT/cprobe_$c" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/carry_probe.py" > "$GRAFT_REPO_ROOT/$OUT/cprobe_$c.jsonl" 2> "$GRAFT_REPO_ROOT/$OUT/cprobe_$c.err")
-      rc=$?; echo "carryprobe $c rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
-    done ;;
-  carrysweep)  # lib:carry cases (lib 'cur' = the product library; carry 0, 1, q<N> = VPTMCM_STOP_Q, b = 1 with VPTMCM_CARRY_BG=1)
-    for cs in ${SWEEP_CASES:-cur:0 cur:1}; do
-      lib=${cs%%:*}; c=${cs#*:}
-      bgv=0
-      case $c in q*) cv=1; q=${c#q}; f=0;; f) cv=1; q=1000000; f=1;; b) cv=1; q=0; f=0; bgv=1;; *) cv=$c; q=0; f=0;; esac
-      if [ $lib = cur ]; then unset VPTMCM_LIB; else export VPTMCM_LIB=$lib; fi
-      VPTMCM_CARRY=$cv VPTMCM_CARRY_BG=$bgv VPTMCM_STOP_Q=$q VPTMCM_CARRY_FORCE=$f timeout -k 10 300 python bench.py --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 256 --unfused-steps 0 > $OUT/cs.json 2>> $OUT/carrysweep.err
-      rc=$?; unset VPTMCM_LIB; [ $rc -ne 0 ] && { echo "carrysweep rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
-      python3 -c "import json; d=json.load(open('$OUT/cs.json')); print(json.dumps({'case': '$cs', 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'render_api': d['render_api']['value']}))" >> $OUT/carrysweep.jsonl
-    done
-    echo "carrysweep rc=0" | tee -a $OUT/status.txt; cat $OUT/carrysweep.jsonl ;;
-  ctl)  # per-wave timeline of the last carry launch vs a plain one (VPT_STAMP=2 build 'tl')
-    for c in ${CTL_CASES:-1 0 b}; do  # b: carry with VPTMCM_CARRY_BG=1
-      case $c in b) cv=1; bgv=1;; *) cv=$c; bgv=0;; esac
-      VPTMCM_LIB=tl VPTMCM_CARRY_NOFINAL=1 VPTMCM_CARRY=$cv VPTMCM_CARRY_BG=$bgv timeout -k 10 300 python tools/carry_timeline.py 12 >> $OUT/ctl.jsonl 2>> $OUT/ctl.err
-      rc=$?; echo "ctl $c rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
-    done; cat $OUT/ctl.jsonl ;;
   hullab)  # robust-miss pixels by the projected hull vs the box only (VPTMCM_LIB=nohull), orbit camera
     for lib in ${HULL_LIBS:-nohull cur nohull cur}; do
       if [ $lib = cur ]; then unset VPTMCM_LIB; else export VPTMCM_LIB=$lib; fi

@@ -35,41 +35,27 @@ struct TileSched {
   // launch (tile | flag << 31, 0xffffffff idle): a hot wave starts loading that
   // tile's photon state before its own schedule ends, and reloads on a change
   uint32_t* prev;
-  // Cross-launch balancing (MarchParams::carry): per tile the absolute index of
-  // its next pass; the completion counters of the early stop (this launch's,
-  // and the next launch's, which this launch zeroes).
-  uint32_t* tile_next;
-  uint32_t* stop_ctr;
-  uint32_t* stop_ctr_next;
+  // Completion signal (vptmcm_synchronize): every wave of the launch adds 1 to
+  // done_ctr (device memory, cumulative over launches) once its stores have
+  // landed; the wave that brings it to MarchParams::done_target writes
+  // MarchParams::done_seq to done_flag, a word of fine-grained host memory the
+  // host polls. Null: no signal.
+  uint32_t* done_ctr;
+  uint32_t* done_flag;
 };
 // Flag byte of a tile (written by each launch for the next one's schedule):
-// bit 0 its wave entered the volume, bits 1-2 its lag bucket (passes it still
-// owes after the launch: 0, 1-3, 4-7, >= 8).
-constexpr uint32_t kFlagVolume = 1u, kLagShift = 1u;
-// The tile's wave took the dark-background chain (k_march): the next plain
-// deal gives such tiles the background slots beside SIMD pairs first.
-constexpr uint32_t kFlagDark = 8u;
-// Packed schedule word of a background tile in the plain deal with the dark
-// chain on: the tile was dark last launch.
-constexpr uint32_t kSlotDarkBit = 29u;
-// A launch's stop block (TileSched::stop_ctr): counter line + flag lines.
-constexpr uint32_t kStopFlagLines = 64u, kStopLineWords = 32u;
-constexpr uint32_t kStopBlockWords = (1u + kStopFlagLines) * kStopLineWords;
+// bit 0 its wave entered the volume.
+constexpr uint32_t kFlagVolume = 1u;
 constexpr uint32_t kSchedChunk = 4 * kMarchBlock;  // tiles scanned per block-wide round
 constexpr uint32_t kSchedMaxTiles = 16384;         // larger frames use the raster mapping
 // Seeds of the passes one march launch runs back to back (render_passes): the
 // photon state stays in registers between them; every pass reseeds the RNG
-// from its own seed (wgsl:122). A launch queues n <= kMaxFusedPasses new
-// passes; its window holds the seeds of the last kSeedWindow passes queued
-// since create (absolute pass indices [base, base + kSeedWindow), the launch's
-// target is base + kSeedWindow), so a tile that owes passes of earlier
-// launches (MarchParams::carry) finds their seeds too.
+// from its own seed (wgsl:122). A launch runs n <= kMaxFusedPasses passes.
 constexpr uint32_t kMaxFusedPasses = 32;
-constexpr uint32_t kSeedWindow = 64;
 struct PassSeeds {
   uint32_t n;
-  uint32_t base;
-  uint32_t seed[kSeedWindow];
+  uint32_t pad;
+  uint32_t seed[kMaxFusedPasses];
 };
 static_assert(offsetof(PassSeeds, seed) == 8, "pass_seed() reads seed[] at kernarg byte 8");
 // k_march(PassSeeds, MarchParams, ...): MarchParams starts right after PassSeeds

@@ -13,17 +13,8 @@
 #ifndef VPT_NB_ZERO
 #define VPT_NB_ZERO 1  // nb < 12: unguarded 12-bin loops over zeroed unused bins
 #endif
-#ifndef VPT_CTR_EARLY
-#define VPT_CTR_EARLY 0  // 1: read the carry stop counter at the top of each pass (one pass stale)
-#endif
-#ifndef VPT_OWE_PRIO
-#define VPT_OWE_PRIO 1  // carry: the owing wave of a pair takes the higher issue priority
-#endif
 #ifndef VPT_RB_HULL
 #define VPT_RB_HULL 1  // robust-miss pixels beyond the projected hull's edges too (0: the box only)
-#endif
-#ifndef VPT_KO_BG
-#define VPT_KO_BG 0  // experiment only (wrong images): background waves of paired CUs skip their passes
 #endif
 #ifndef VPT_PRIO
 #define VPT_PRIO 1  // s_setprio level of volume waves (0 = off); 11 % faster passes
@@ -273,134 +264,8 @@ __device__ __forceinline__ void deal_slot(uint32_t slot, uint32_t G, uint32_t lb
   }
 }
 
-// Cross-launch balancing (MarchParams::lag_sched, one chunk of tiles): the
-// volume tiles in four classes by the passes they still owe (most first, raster
-// order inside a class), then dealt so that the most owing ones get the lone
-// SIMD slots (the group-0 slots of the blocks whose group-1 slots are
-// background: slots [P, 4G) for P = nv - 4G pairs), the next ones the paired
-// group-0 slots, the least owing ones group 1. A SIMD with a single volume
-// wave then has work for the whole launch, and in a pair the owing wave leads
-// (it also takes the higher issue priority). Returns the slot's packed tile
-// (tile | volume << 31 | lag bucket << 29) and the launch's stop quota in *q
-// (the lone slot count, 0 without pairs).
-#if VPT_KO_BG
-#define KO_NV(v) \
-  if (threadIdx.x == 0u) s_tile[16] = (v)
-#else
-#define KO_NV(v)
-#endif
-// With bg (MarchParams::bg_lag) the background tiles are classed the same way
-// and dealt most owing first to the background slots of the CUs without pairs
-// (group 1-3 slots at positions >= pairs), the least owing to the paired CUs'
-// group 2-3 slots (positions < pairs): those SIMDs already run two volume waves.
-__device__ uint32_t schedule_tile_lag(uint32_t n, uint32_t f, uint32_t lb, uint32_t* s_red,
-                                      uint32_t* s_tile, uint32_t* q, bool bg) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6, G = gridDim.x;
-  uint32_t cc = 0u, cb = 0u;  // per class (k = 3 - bucket) the lane's count, 4 bits each
-#pragma unroll
-  for (uint32_t b = 0; b < 4u; b++) {
-    const uint32_t fb = (f >> (8u * b)) & 0xffu;
-    const uint32_t one = 1u << (4u * (3u - ((fb >> kLagShift) & 3u)));
-    if (fb & kFlagVolume) cc += one;
-    else if (4u * tid + b < n) cb += one;
-  }
-  uint32_t pre[4], wt[4], preb[4] = {0u, 0u, 0u, 0u}, wtb[4];
-#pragma unroll
-  for (uint32_t k = 0; k < 4u; k++) pre[k] = wave_scan_small((cc >> (4u * k)) & 0xfu, wt[k]);
-  if (bg) {
-#pragma unroll
-    for (uint32_t k = 0; k < 4u; k++) preb[k] = wave_scan_small((cb >> (4u * k)) & 0xfu, wtb[k]);
-  }
-  if (lane == 0u) {
-#pragma unroll
-    for (uint32_t k = 0; k < 4u; k++) s_red[4u * w + k] = wt[k];
-    if (bg) {
-#pragma unroll
-      for (uint32_t k = 0; k < 4u; k++) s_red[64u + 4u * w + k] = wtb[k];
-    }
-  }
-  __syncthreads();
-  uint32_t before[4] = {0u, 0u, 0u, 0u}, tot[4] = {0u, 0u, 0u, 0u};
-  uint32_t beforeb[4] = {0u, 0u, 0u, 0u}, totb[4] = {0u, 0u, 0u, 0u};
-  for (uint32_t v = 0; v < 16u; v++) {
-#pragma unroll
-    for (uint32_t k = 0; k < 4u; k++) {
-      const uint32_t t = s_red[4u * v + k];
-      before[k] += (v < w) ? t : 0u;
-      tot[k] += t;
-    }
-  }
-  if (bg) {
-    for (uint32_t v = 0; v < 16u; v++) {
-#pragma unroll
-      for (uint32_t k = 0; k < 4u; k++) {
-        const uint32_t t = s_red[64u + 4u * v + k];
-        beforeb[k] += (v < w) ? t : 0u;
-        totb[k] += t;
-      }
-    }
-  }
-  const uint32_t nv = tot[0] + tot[1] + tot[2] + tot[3];
-  // pairs >= 4G (two or more volume waves on every SIMD): no lone SIMDs, no
-  // remap and no early stop
-  const uint32_t pairs = nv > 4u * G ? nv - 4u * G : 0u, lone = pairs < 4u * G ? 4u * G - pairs : 0u;
-  const bool remap = pairs > 0u && lone > 0u && (tot[0] + tot[1] + tot[2]) > 0u;
-  if (q) *q = (pairs > 0u && lone > 0u) ? lone : 0u;
-  KO_NV(nv);
-  // running rank inside each class, and the volume tiles before this lane's four
-  uint32_t seen[4], seenb[4];
-  uint32_t ones = 0u;
-#pragma unroll
-  for (uint32_t k = 0; k < 4u; k++) {
-    seen[k] = before[k] + pre[k];
-    seenb[k] = beforeb[k] + preb[k];
-    ones += seen[k];
-  }
-  const uint32_t base1 = tot[0], base2 = tot[0] + tot[1], base3 = base2 + tot[2];
-  const uint32_t bb1 = totb[0], bb2 = totb[0] + totb[1], bb3 = bb2 + totb[2];
-  const bool bgdeal = bg && pairs > 0u && lone > 0u;
-#pragma unroll
-  for (uint32_t b = 0; b < 4u; b++) {
-    const uint32_t t = 4u * tid + b;
-    const uint32_t fb = (f >> (8u * b)) & 0xffu;
-    const uint32_t vol = fb & kFlagVolume, bucket = (fb >> kLagShift) & 3u, k = 3u - bucket;
-    if (t < n) {
-      uint32_t slot;
-      if (vol) {
-        const uint32_t r = (k == 0u ? seen[0] : k == 1u ? base1 + seen[1] : k == 2u ? base2 + seen[2]
-                                                                               : base3 + seen[3]);
-        slot = !remap ? r : (r < lone ? pairs + r : (r < 4u * G ? r - lone : r));
-      } else if (bgdeal) {
-        const uint32_t r = (k == 0u ? seenb[0] : k == 1u ? bb1 + seenb[1] : k == 2u ? bb2 + seenb[2]
-                                                                         : bb3 + seenb[3]);
-        if (r < 3u * lone) {  // group 1..3, positions [pairs, 4G)
-          const uint32_t g = r / lone;
-          slot = (1u + g) * 4u * G + pairs + (r - g * lone);
-        } else {  // group 2..3, positions [0, pairs)
-          const uint32_t r2 = r - 3u * lone, g = r2 / pairs;
-          slot = (2u + g) * 4u * G + (r2 - g * pairs);
-        }
-      } else {
-        slot = nv + (t - ones);
-      }
-      deal_slot(slot, G, lb, t | (vol << 31) | (bucket << 29), s_tile);
-    }
-    if (vol) {
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; j++) seen[j] += (j == k) ? 1u : 0u;
-      ones++;
-    } else if (t < n) {
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; j++) seenb[j] += (j == k) ? 1u : 0u;
-    }
-  }
-  __syncthreads();  // s_tile complete
-  return s_tile[w];
-}
-
-template <bool LAG = false>
 __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8_t* __restrict__ flags,
-                                  uint32_t* s_red, uint32_t* s_tile, uint32_t* stop_q = nullptr) {
+                                  uint32_t* s_red, uint32_t* s_tile) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
   const uint32_t n = P.n_tiles, G = gridDim.x;
   // Consecutive slots go to consecutive hardware blocks, i.e. round-robin over
@@ -411,8 +276,6 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
   const uint32_t lb = P.sched == 2u ? xcd_swizzle(blockIdx.x, G) : blockIdx.x;
   const uint32_t* f4 = reinterpret_cast<const uint32_t*>(flags);  // flag bytes, padded to kSchedChunk
   if (tid < 16u) s_tile[tid] = 0xffffffffu;  // idle unless a tile is dealt to it
-  if (LAG && P.lag_sched && n <= kSchedChunk)
-    return schedule_tile_lag(n, f0, lb, s_red, s_tile, stop_q, P.bg_lag != 0u);
   uint32_t nv = 0u;  // number of volume tiles; one chunk (R <= 512): the scan's total
   if (n > kSchedChunk) {
     if (tid == 0u) s_red[16] = 0u;
@@ -425,72 +288,27 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
     __syncthreads();
     nv = s_red[16];
   }
-  // Dark-first deal (MarchParams::dark == 2, plain launches, one chunk): the
-  // background tiles whose waves took the dark chain last launch (kFlagDark,
-  // ~70 instead of ~240 instructions per step) go first to the background
-  // slots beside SIMD pairs (group 2-3, positions < pairs), the others first
-  // to the CUs without pairs, so the paired SIMDs carry the cheap background.
-  const bool dk = !LAG && P.dark == 2u && n <= kSchedChunk;
   uint32_t run = 0u;  // volume tiles before this chunk
   for (uint32_t base = 0; base < n; base += kSchedChunk) {
-    const uint32_t fr = base == 0u ? f0 : f4[(base >> 2) + tid];
-    const uint32_t f = fr & 0x01010101u;
-    const uint32_t fd = dk ? ((fr >> 3) & 0x01010101u) & ~f : 0u;  // dark background tiles
-    uint32_t wt, wtd = 0u, pred = 0u;
+    const uint32_t f = (base == 0u ? f0 : f4[(base >> 2) + tid]) & 0x01010101u;
+    uint32_t wt;
     const uint32_t pre = wave_scan_small(__popc(f), wt);
-    if (dk) pred = wave_scan_small(__popc(fd), wtd);
-    if (lane == 0u) {
-      s_red[w] = wt;
-      if (dk) s_red[32u + w] = wtd;
-    }
+    if (lane == 0u) s_red[w] = wt;
     __syncthreads();
-    uint32_t before = run, total = 0u, dbefore = 0u, nd = 0u;
+    uint32_t before = run, total = 0u;
     for (uint32_t k = 0; k < 16u; k++) {
       uint32_t t = s_red[k];
       before += (k < w) ? t : 0u;
       total += t;
     }
-    if (dk) {
-      for (uint32_t k = 0; k < 16u; k++) {
-        const uint32_t t = s_red[32u + k];
-        dbefore += (k < w) ? t : 0u;
-        nd += t;
-      }
-    }
     if (n <= kSchedChunk) nv = total;
-    KO_NV(nv);
-    const uint32_t pairs = nv > 4u * G ? nv - 4u * G : 0u, lone = pairs < 4u * G ? 4u * G - pairs : 0u;
-    const bool ddeal = dk && pairs > 0u && lone > 0u && nd > 0u;
     uint32_t ones = before + pre;  // volume tiles before tile base + 4*tid
-    uint32_t darks = dbefore + pred;  // dark background tiles before it
 #pragma unroll
     for (uint32_t q = 0; q < 4u; q++) {
       const uint32_t t = base + 4u * tid + q;
       const uint32_t fl = (f >> (8u * q)) & 1u;
-      const uint32_t fk = (fd >> (8u * q)) & 1u;
-      if (t < n) {
-        uint32_t slot = fl ? ones : nv + (t - ones);
-        if (!fl && ddeal) {
-          // the background slot list: [beside pairs (2 pairs)] ++ [the other CUs (3 lone)]
-          // (groups by compares: r < 2 pairs + 3 lone, no integer division in
-          // the schedule, which a one-pass launch waits for)
-          const uint32_t r = fk ? darks : nd + (t - ones - darks);
-          if (r < 2u * pairs) {
-            const uint32_t g = r >= pairs ? 1u : 0u;
-            slot = (2u + g) * 4u * G + (r - g * pairs);
-          } else {
-            const uint32_t r2 = r - 2u * pairs, g = (r2 >= lone ? 1u : 0u) + (r2 >= 2u * lone ? 1u : 0u);
-            slot = (1u + g) * 4u * G + pairs + (r2 - g * lone);
-          }
-        }
-        const uint32_t k = slot / (4u * G), rem = slot - k * 4u * G;
-        if ((rem >> 2) == lb) {
-          const uint32_t j = rem & 3u;
-          s_tile[4u * j + ((k + j) & 3u)] = t | (fl << 31) | (fk << kSlotDarkBit);
-        }
-      }
+      if (t < n) deal_slot(fl ? ones : nv + (t - ones), G, lb, t | (fl << 31), s_tile);
       ones += fl;
-      darks += fk;
     }
     run += total;
     __syncthreads();  // s_red reused by the next chunk; s_tile complete after the last
@@ -501,15 +319,19 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
 // s_waitcnt immediate (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8]
 // | vmcnt_hi[15:14]) for vmcnt(0) with expcnt and lgkmcnt left unconstrained.
 constexpr uint32_t kWaitVmcnt0 = 0x0F70u;
-// Early stop of a carry launch (TileSched::stop_ctr): the completion counter in
-// word 0, then kStopFlagLines flag lines, one 128-B line each, raised together
-// when the counter reaches the quota; a wave polls the line of its tile (one
-// load per pass, second half of its passes only), so the 1600 pollers spread
-// over 64 lines instead of queueing on the counter's (round 4: polling the
-// counter itself every pass cost 8 % per pass).
-__device__ __forceinline__ uint32_t stop_flag_load(const TileSched& T, uint32_t tile) {
-  return __hip_atomic_load(T.stop_ctr + kStopLineWords * (1u + (tile & (kStopFlagLines - 1u))),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Completion signal (TileSched::done_ctr, done_flag): once this wave's stores
+// have landed (vmcnt(0)), lane 0 adds it to the launch's cumulative wave count;
+// the wave that completes the count writes the launch's sequence number to
+// the host's flag word with a vector store at system scope (the host polls
+// it in vptmcm_synchronize instead of waiting for the end-of-kernel packet).
+__device__ __forceinline__ void signal_done(const MarchParams& P, const TileSched& T) {
+  if (T.done_flag == nullptr) return;
+  __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+  if ((threadIdx.x & 63u) == 0u) {
+    const uint32_t old = __hip_atomic_fetch_add(T.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1u == P.done_target)
+      __hip_atomic_store(T.done_flag, P.done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 // The tile of a packed schedule slot word (TileSched::prev, s_tile).
 constexpr uint32_t kSlotTileMask = 0x1fffffffu;
@@ -532,9 +354,9 @@ __device__ __forceinline__ void stage_lds_16(uint4* dst, const uint4* __restrict
 // from the kernarg segment (one scalar load per pass) instead of keeping all
 // kMaxFusedPasses seeds live in SGPRs.
 typedef const __attribute__((address_space(4))) uint32_t* karg_u32;
-__device__ __forceinline__ uint32_t pass_seed(uint32_t widx) {  // widx: index in the seed window
+__device__ __forceinline__ uint32_t pass_seed(uint32_t pass) {
   karg_u32 k = (karg_u32)__builtin_amdgcn_kernarg_segment_ptr();
-  return k[2u + widx];  // offsetof(PassSeeds, seed) == 8
+  return k[2u + pass];  // offsetof(PassSeeds, seed) == 8
 }
 // The CMF bin means of MarchParams (the second kernel argument), re-read from
 // the kernarg segment at every pass's radiance_to_rgb through a pointer the
@@ -569,10 +391,7 @@ __device__ __forceinline__ bool robust_pixel(const MarchParams& P, float sx, flo
 // 5: MODE 2's geometry and light with any bin layout and a TF of more than
 // kTfRowsMax distinct rows (u16 LDS TF; anisotropy from the row table or the
 // tf_b4 gather).
-// CARRY: cross-launch balancing (MarchParams::carry; the per-tile pass window,
-// the early stop and the owing waves' priority); without it the kernel is the
-// plain n-pass launch.
-template <uint32_t L, bool SPEC, uint32_t MODE, bool CARRY>
+template <uint32_t L, bool SPEC, uint32_t MODE>
 __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const MarchParams P,
                                                        const TileSched T, float* __restrict__ ph,
                                                        const uint8_t* __restrict__ vol,
@@ -601,8 +420,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __shared__ uint32_t s_rowmap[256];  // P.tf_dedup: density row -> first texel of its distinct row
   __shared__ uint32_t s_binlut[LUTB ? kBinLutCells + kBinLutCells / 4 : 1];  // MODE 6 / 7
 
-  __shared__ uint32_t s_red[CARRY ? 128 : 64];
-  __shared__ uint32_t s_tile[VPT_KO_BG ? 17 : 16];
+  __shared__ uint32_t s_red[64];
+  __shared__ uint32_t s_tile[16];
 
   TL_DECL();
   TL_MARK(0);
@@ -621,7 +440,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   if (P.sched != 1u) {  // a scalar load (lgkmcnt): its use does not wait for the TF copy
     const auto pt = (const __attribute__((address_space(4))) uint32_t*)T.prev;
     prev = pt[blockIdx.x * 16u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
-    // (the packed slot word: tile | volume << 31 | lag bucket << 29)
+    // (the packed slot word: tile | volume << 31)
     if (prev != 0xffffffffu && (prev >> 31) != 0u && (prev & kSlotTileMask) < P.n_tiles)
       load_photon(ph, S, (size_t)(prev & kSlotTileMask) * 64u + lane, p);
   }
@@ -642,15 +461,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   uint32_t tile;
   bool hot0;  // the tile entered the volume last launch (its wave is a long one)
   bool have = false;  // p already holds this tile's state (the slot's tile did not change)
-  bool owing = false;  // the tile owes passes of earlier launches (lag bucket > 0)
-  uint32_t stop_q = 0u;
-  // the next launch's stop block: its counter (word 0) and its 64 flag lines
-  if (CARRY && blockIdx.x == 0u && threadIdx.x <= kStopFlagLines) T.stop_ctr_next[kStopLineWords * threadIdx.x] = 0u;
   if (P.sched != 1u) {
-    const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile<CARRY>(P, f0, T.flags_in, s_red, s_tile, &stop_q));
+    const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile(P, f0, T.flags_in, s_red, s_tile));
     tile = s == 0xffffffffu ? s : s & kSlotTileMask;
     hot0 = s != 0xffffffffu && (s >> 31) != 0u;
-    owing = CARRY && s != 0xffffffffu && ((s >> 29) & 3u) != 0u;
     have = hot0 && s == prev;
     if (lane == 0u && s != prev) T.prev[blockIdx.x * 16u + (threadIdx.x >> 6)] = s;
   } else {  // raster: the block's 16 consecutive tiles
@@ -659,30 +473,12 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     hot0 = true;
   }
   TL_MARK(1);
-  if (CARRY) stop_q = __builtin_amdgcn_readfirstlane(P.stop_q ? P.stop_q : stop_q);
-  // The tile's passes: from its own next pass (carry) or the launch's n new
-  // ones, up to the window's end (target); todo <= kSeedWindow always holds
-  // for a tile of this handle (the host keeps every tile within the window).
-  uint32_t todo = PS.n;
-  if (CARRY && tile < P.n_tiles) {
-    const auto tn = (const __attribute__((address_space(4))) uint32_t*)T.tile_next;  // scalar load
-    const uint32_t owed = PS.base + kSeedWindow - tn[tile];
-    todo = owed <= kSeedWindow ? owed : PS.n;
-  }
-#if VPT_KO_BG
-  if (P.sched != 1u && !hot0) {  // a CU whose four SIMDs all hold two volume waves
-    const uint32_t nv = s_tile[16], pairs = nv > 4u * gridDim.x ? nv - 4u * gridDim.x : 0u;
-    if (blockIdx.x * 4u + 4u <= pairs) todo = 0u;
-  }
-#endif
-  todo = __builtin_amdgcn_readfirstlane(todo);
-  const uint32_t first = kSeedWindow - todo;  // window index of the tile's first pass
   const uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
   const uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
   const size_t i = (size_t)tile * 64u + lane;
   // tiles outside the band (whole tiles: band rows are multiples of 8) are idle
   const bool live = tile != 0xffffffffu && x < P.R && y < P.R && y >= P.band_y0 && y < P.band_y1;
-  uint32_t entered = 0u;  // wave-uniform flag bits for the next schedule: kFlagVolume (a lane was inside the volume), kFlagDark (the dark chain)
+  uint32_t entered = 0u;  // the next schedule's flag: kFlagVolume (a lane of the wave was inside the volume)
   STAMP_BEGIN();
   // The TF copy into LDS (global_load_lds, issued at entry) is complete for
   // the block only after every wave has waited for its own share (LDS-DMA
@@ -723,10 +519,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __syncthreads();
   if (live && !hot0) load_photon(ph, S, i, p);
   TL_MARK_WAIT(2);
-  if (!live || todo == 0u) {
-    // an idle out-of-band tile; or a tile with no pass owed (a completion
-    // launch): its flag carries over
+  if (!live || PS.n == 0u) {
+    // an idle out-of-band tile (or a launch of no pass): its flag carries over
     if (tile < P.n_tiles && lane == 0u) T.flags_out[tile] = (live && hot0) ? kFlagVolume : 0u;
+    signal_done(P, T);
     return;
   }
   const uint16_t* s_tf = reinterpret_cast<const uint16_t*>(s_tf4);
@@ -803,13 +599,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     p.bin = rc.bin;
     rb = rbpix;
   };
-  const uint32_t n_passes = todo;
-  // early stop (MarchParams::allow_stop): a volume wave (with bg_lag any wave)
-  // ends the launch at a pass boundary once stop_q volume waves have reached
-  // the target; the counter is read one pass ahead (lane 0, coherent across
-  // the XCDs) so its latency hides in the pass
-  const bool stop_ok = CARRY && P.allow_stop && (hot0 || P.bg_lag) && stop_q != 0u;
-  uint32_t ctr_v = 0u, done_passes = n_passes;
+  const uint32_t n_passes = PS.n;
   auto write_image = [&]() {
     float X = 0.0f, Y = 0.0f, Z = 0.0f;
     {
@@ -849,8 +639,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   // observable.
   bool dark = false;
   if constexpr (GEO) {
-    // (carry: not when background waves may stop early, MarchParams::bg_lag)
-    if (P.dark != 0u && !(CARRY && P.bg_lag) && __builtin_amdgcn_ballot_w64(!rbpix) == 0ull &&
+    if (P.dark != 0u && __builtin_amdgcn_ballot_w64(!rbpix) == 0ull &&
         n_passes != 0u && P.steps != 0u) {
       bool ok = true;
 #pragma unroll
@@ -864,7 +653,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
         ok = ok && cl < -1e-3f * (__builtin_fabsf(dx) + __builtin_fabsf(dy) + __builtin_fabsf(dz));
       }
       {  // the launch's first step, as the general path computes it
-        const uint32_t s1 = pcg_hash(hash3(x, y, pass_seed(first)));
+        const uint32_t s1 = pcg_hash(hash3(x, y, pass_seed(0u)));
         const float dist = -spec_log_unit(s1) * P.rcp_extinction;
         const float qx = fmaf(dist, p.dir.x, p.pos.x), qy = fmaf(dist, p.dir.y, p.pos.y),
                     qz = fmaf(dist, p.dir.z, p.pos.z);
@@ -878,7 +667,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   if (dark) {
     uint32_t h3 = 0u, h4 = 0u, h5 = 0u;
     for (uint32_t pass = 0; pass < n_passes; pass++) {
-      uint32_t st = hash3(x, y, pass_seed(first + pass));
+      uint32_t st = hash3(x, y, pass_seed(pass));
       for (uint32_t step = 0; step < P.steps; step++) {
         const uint32_t s1 = pcg_hash(st), sw = pcg_hash(s1), h1 = pcg_hash(sw), h2 = pcg_hash(h1);
         h3 = pcg_hash(h2);
@@ -893,41 +682,20 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     p.lambda = lambda_of(P, h5);
     p.bin = bin_of_draw<UNIB, LUTB>(P, p.lambda, h5, s_binlut);
     stale = true;
-    entered = kFlagDark;
     write_image();
   } else {
   for (uint32_t pass = 0; pass < n_passes; pass++) {
-  if (stop_ok) {
-    if (pass > 0u && __builtin_amdgcn_readfirstlane(ctr_v) != 0u && n_passes - pass <= kMaxFusedPasses) {
-      done_passes = pass;  // the pending sample is applied after the loop
-      break;
-    }
-#if VPT_CTR_EARLY
-    if (lane == 0u && 2u * pass >= n_passes) ctr_v = stop_flag_load(T, tile);
-#endif
-  }
 #if VPT_PRIO
   if (pass > 0u) hot = entered != 0u;
-  if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) {
-    if (CARRY && VPT_OWE_PRIO && owing) __builtin_amdgcn_s_setprio(VPT_PRIO + 1);  // the owing wave of a pair leads
-    else __builtin_amdgcn_s_setprio(VPT_PRIO);
-  } else {
-    __builtin_amdgcn_s_setprio(0);
-  }
+  if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) __builtin_amdgcn_s_setprio(VPT_PRIO);
+  else __builtin_amdgcn_s_setprio(0);
   entered = 0u;
 #endif
-  uint32_t st = hash3(x, y, pass_seed(first + pass));  // wgsl:122 (state is not carried across passes)
+  uint32_t st = hash3(x, y, pass_seed(pass));  // wgsl:122 (state is not carried across passes)
 
   if constexpr (SPEC) {
     for (uint32_t step = 0; step < P.steps; step++) {
       STAMP_RESTART();
-#if !VPT_CTR_EARLY
-      // the stop counter, read during the pass's last step (lane 0, coherent
-      // across the XCDs): it lands with that step's gather and is at most one
-      // step old at the pass boundary
-      if (stop_ok && step + 1u == P.steps && lane == 0u && 2u * pass >= n_passes)
-        ctr_v = stop_flag_load(T, tile);
-#endif
       // The previous step's deferred add_radiance, once, ahead of every path:
       // one definition of the bins for the loop's back edge (per-path updates
       // left 12 + 14 register copies in the volume and all-exit latches), and
@@ -1140,7 +908,6 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   }  // pass
   }  // not dark
   TL_MARK(3);
-  if (CARRY && done_passes != n_passes) apply_pending();  // an early stop (the last pass applies its own)
 
   if (stale) p.pos = ray_start(from, p.dir);  // the last robust reset's start point
   store_state(ph, S, i, p);  // uPhotons[globalIndex] = p (wgsl:165), once per launch
@@ -1148,21 +915,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   for (int b = 0; b < kMaxBins; b++)
     if (NBF || !VPT_NB_ZERO || (uint32_t)b < P.nb) ph[(kRad0 + b) * S + i] = p.rad[b];
 
-  if (lane == 0u) {  // the next launch's schedule: volume flag and lag bucket
-    const uint32_t owe = n_passes - done_passes;
-    const uint32_t bucket = owe == 0u ? 0u : owe < 4u ? 1u : owe < 8u ? 2u : 3u;
-    T.flags_out[tile] = entered | (bucket << kLagShift);
-    if (CARRY) T.tile_next[tile] = PS.base + first + done_passes;
-  }
-  if (stop_ok && hot0 && n_passes == done_passes) {
-    // count the completion; the one that reaches the quota raises the 64 flag lines
-    uint32_t old = 0u;
-    if (lane == 0u) old = __hip_atomic_fetch_add(T.stop_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__builtin_amdgcn_readfirstlane(old) + 1u == stop_q)
-      __hip_atomic_store(T.stop_ctr + kStopLineWords * (1u + lane), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (lane == 0u) T.flags_out[tile] = entered;  // the next launch's schedule
+  signal_done(P, T);
   STAMP_END(rgb32, tile, entered);
-  TL_END(rgb32, tile, entered, CARRY ? ((n_passes << 16) | (done_passes << 8) | (owing ? 1u : 0u)) : 0u);
+  TL_END(rgb32, tile, entered, 0u);
 }
 
 
@@ -1289,7 +1045,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
     if (__builtin_amdgcn_readfirstlane(hot ? 1u : 0u)) __builtin_amdgcn_s_setprio(VPT_PRIO);
     else __builtin_amdgcn_s_setprio(0);
     entered = false;
-    uint32_t st = hash3(x, y, pass_seed(kSeedWindow - PS.n + pass));  // MCMComputeRenderer.wgsl:112
+    uint32_t st = hash3(x, y, pass_seed(pass));  // MCMComputeRenderer.wgsl:112
     for (uint32_t step = 0; step < P.steps; step++) {
       if (__builtin_amdgcn_ballot_w64(!rb) == 0ull) {
         // robust path: the exit and the reset of wgsl:126-139 without the
@@ -1594,14 +1350,9 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   if (info) *info = MarchLaunchInfo{mode, tpl, spec ? 1u : 0u, PS.n};
   // hipExtLaunchKernelGGL stamps the events from the dispatch packet itself
   // (no extra barrier/marker packets between back-to-back launches)
-#define VPT_LAUNCH_C(LAY, SP, MO, CA)                                                              \
-  hipExtLaunchKernelGGL((k_march<LAY, SP, MO, CA>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
+#define VPT_LAUNCH(LAY, SP, MO)                                                                \
+  hipExtLaunchKernelGGL((k_march<LAY, SP, MO>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
                         PS, Q, T, ph, vol, tf_lds, tf_b4, tf_brow, light, rgba, rgb32, rowmap, bin_lut)
-#define VPT_LAUNCH(LAY, SP, MO)                                   \
-  do {                                                            \
-    if (SP && Q.carry) VPT_LAUNCH_C(LAY, SP, MO, SP);             \
-    else VPT_LAUNCH_C(LAY, SP, MO, false);                        \
-  } while (0)
 #define VPT_LAUNCH_NB(LAY)                 \
   do {                                     \
     switch (spec ? mode : 8u + mode) {     \
@@ -1626,7 +1377,6 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   }
 #undef VPT_LAUNCH_NB
 #undef VPT_LAUNCH
-#undef VPT_LAUNCH_C
   return hipGetLastError();
 }
 

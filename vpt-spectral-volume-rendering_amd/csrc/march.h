@@ -111,21 +111,12 @@ struct MarchParams {
   // host-built and exact (kBinLutCells u32 thresholds, then as many bytes of
   // base | count << 4). Set when no cell holds two distinct thresholds.
   uint32_t bins_lut;
-  // Cross-launch balancing (vptmcm.cpp, "carry"): each tile runs from its own
-  // next pass (TileSched::tile_next) to the launch's target; with allow_stop a
-  // volume wave may end its launch at a pass boundary once stop_q volume waves
-  // (0: the lone SIMD slots of the deal) have reached the target, owing the
-  // rest to the next launch; lag_sched deals the owing tiles first (the
-  // previous launch allowed stops). bg_lag: background waves stop at the same
-  // signal, and the background tiles are dealt by what they owe too, the most
-  // owing to the CUs without SIMD pairs.
-  uint32_t carry, allow_stop, stop_q, lag_sched, bg_lag;
   // Dark background (k_march, FAST geometry): waves whose every sample is
-  // provably +0 run the draw chain alone (1, the default); 2 also deals the
-  // tiles that were dark first to the background slots beside SIMD pairs
-  // (plain deal; measured no faster, one-pass launches slower); 0 off
-  // (VPTMCM_DARK).
+  // provably +0 run the draw chain alone (1, the default); 0 off (VPTMCM_DARK).
   uint32_t dark;
+  // Completion signal (TileSched::done_ctr / done_flag): the cumulative wave
+  // count after this launch and the value its last wave writes to the flag.
+  uint32_t done_target, done_seq;
 };
 constexpr uint32_t kBinLutCells = 1024u;
 constexpr uint32_t kBinLutShift = 22u;

@@ -78,26 +78,7 @@ struct vptmcm {
   uint8_t* sched = nullptr;    // tile schedule flags: [2][sched_flag_bytes(n_tiles)]
   uint32_t* sched_prev = nullptr;  // each wave slot's last scheduled tile (TileSched::prev)
   uint32_t sched_cur = 0;      // which flag row the next march reads
-  // Cross-launch balancing ("carry", MarchParams::carry): a
-  // launch queued while more passes follow may end when the lone SIMDs' waves
-  // reach its target, the other volume waves stopping at a pass boundary and
-  // owing the rest (per tile: tile_next, the absolute index of its next pass);
-  // the next launch deals the owing tiles first and runs each tile from its
-  // own next pass. Every photon's passes and seeds are unchanged, so the bits
-  // are; any observation or input change first runs every tile to the last
-  // queued pass (flush_renders).
-  bool carry_on = false;       // spectral, one schedule chunk, not disabled (VPTMCM_CARRY=0)
-  bool carry_bg = false;       // VPTMCM_CARRY_BG=1: background tiles carry too (MarchParams::bg_lag)
-  uint32_t dark = 1;           // MarchParams::dark: 1 dark chain, 2 chain + dark-first deal, 0 off (VPTMCM_DARK)
-  bool carry_pending = false;  // a launch with early stops ran since all tiles were complete
-  bool tile_next_stale = false;  // tile_next lags the launches (every tile is at pass_target)
-  float carry_mvp[16] = {};    // the matrix of the owed passes
-  uint32_t* tile_next = nullptr;
-  uint32_t* stop_ctr = nullptr;  // two stop blocks (counter + flag lines), alternating per launch
-  uint32_t ctr_parity = 0;
-  uint32_t stop_q = 0;         // VPTMCM_STOP_Q: the early-stop quota (0: the lone SIMD slots)
-  uint32_t pass_target = 0;    // absolute index of the next pass to queue
-  uint32_t seed_ring[kSeedWindow] = {};  // seeds of the last kSeedWindow passes queued
+  uint32_t dark = 1;           // MarchParams::dark: 1 the dark-background chain, 0 off (VPTMCM_DARK)
 
   float spectrum[VPTMCM_SPECTRUM_FLOATS] = {};
   uint8_t light_host[256];
@@ -126,6 +107,18 @@ struct vptmcm {
   // through an interrupt, whose latency on a busy host adds tens of
   // microseconds to every short region
   int64_t sync_spin_us = 2000;
+  // Completion signal of the spectral march (TileSched::done_ctr/done_flag):
+  // the last wave of a launch writes its sequence number to a word of
+  // fine-grained host memory once every wave's stores have landed, so
+  // vptmcm_synchronize sees a march-terminated stream finish without the
+  // end-of-kernel packet's cache write-back and completion signal (~9 us on
+  // the driver's one-launch region). VPTMCM_DONE_FLAG=0 turns it off.
+  bool done_on = true;
+  uint32_t* done_ctr = nullptr;        // device: cumulative wave count
+  uint32_t* done_host = nullptr;       // host (fine-grained): the last signalled sequence number
+  uint32_t* done_dev = nullptr;        // its device address
+  uint32_t done_total = 0, done_seq = 0;
+  bool done_pending = false;           // the stream's last enqueued work is march done_seq
   MarchLaunchInfo last_launch{};
 
   // multi-GPU
@@ -532,6 +525,7 @@ int time_close(vptmcm* h) {
   }
   HIPCHK(h, hipEventRecord(h->region.end, h->stream));
   h->region_closed = true;
+  h->done_pending = false;  // work behind the signalling march
   return VPTMCM_OK;
 }
 
@@ -548,40 +542,17 @@ int flush_relayout(vptmcm* h) {
   return VPTMCM_OK;
 }
 
-// One march launch queueing n <= kMaxFusedPasses new passes (seeds) with
-// matrix mvp. allow_stop: more passes follow, so volume waves may stop early
-// and owe passes to the next launch (carry); otherwise every tile reaches the
-// new target. A launch with another matrix first completes the owed passes
-// with theirs.
-int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n, bool allow_stop = false) {
+// One march launch of n <= kMaxFusedPasses passes (seeds) with matrix mvp.
+int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   if (!h->volume_ready) FAIL(h, VPTMCM_ESTATE, "render: no volume set (setVolume first)");
-  if (h->carry_pending && memcmp(mvp, h->carry_mvp, sizeof h->carry_mvp) != 0) {
-    if (int rc = do_march(h, h->carry_mvp, nullptr, 0, false)) return rc;
-  }
+  if (n == 0) return VPTMCM_OK;
+  if (n > kMaxFusedPasses) FAIL(h, VPTMCM_EINVAL, "internal: %u passes in one launch", n);
   if (int rc = flush_relayout(h)) return rc;
-  MarchParams P = make_params(h, mvp, n ? seeds[0] : 0u);
-  // VPTMCM_CARRY_FORCE=1 (measurement): the carry kernel for every launch, stops or not
-  static const bool force = [] {
-    const char* v = getenv("VPTMCM_CARRY_FORCE");
-    return v && v[0] == '1';
-  }();
-  const bool carry = h->carry_on && (allow_stop || h->carry_pending || force);
-  if (carry && h->tile_next_stale) {  // every tile is at the last target: the one this launch starts from
-    HIPCHK(h, hipMemsetD32Async(h->tile_next, (int)h->pass_target, h->n_tiles, h->stream));
-    h->tile_next_stale = false;
-  }
-  for (uint32_t k = 0; k < n; k++) h->seed_ring[(h->pass_target + k) % kSeedWindow] = seeds[k];
-  h->pass_target += n;
+  MarchParams P = make_params(h, mvp, seeds[0]);
   PassSeeds PS;
   memset(&PS, 0, sizeof PS);
   PS.n = n;
-  PS.base = h->pass_target - kSeedWindow;
-  for (uint32_t k = 0; k < kSeedWindow; k++) PS.seed[k] = h->seed_ring[(PS.base + k) % kSeedWindow];
-  P.carry = carry ? 1u : 0u;
-  P.allow_stop = (carry && allow_stop) ? 1u : 0u;
-  P.lag_sched = (carry && h->carry_pending) ? 1u : 0u;
-  P.stop_q = h->stop_q;
-  P.bg_lag = (carry && h->carry_bg) ? 1u : 0u;
+  for (uint32_t k = 0; k < n; k++) PS.seed[k] = seeds[k];
   P.dark = h->dark;
   hipEvent_t eb = nullptr, ee = nullptr;
   int rc = time_slot(h, &eb);
@@ -589,8 +560,15 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n, boo
   if (h->timing && h->time_stop) ee = h->region.end;
   const uint8_t* vol = h->layout != kLayoutLinear ? (const uint8_t*)h->vol_c8 : h->vol_lin;
   const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
-  TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev, h->tile_next,
-              h->stop_ctr + h->ctr_parity * kStopBlockWords, h->stop_ctr + (h->ctr_parity ^ 1u) * kStopBlockWords};
+  TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev, nullptr, nullptr};
+  const bool signal = h->done_on && h->kind == VPTMCM_RENDERER_SPECTRAL;
+  if (signal) {  // every wave of the grid counts once (kMarchBlock / 64 per block)
+    h->done_total += tile_blocks(P, kMarchBlock) * (kMarchBlock / 64u);
+    P.done_target = h->done_total;
+    P.done_seq = ++h->done_seq;
+    T.done_ctr = h->done_ctr;
+    T.done_flag = h->done_dev;
+  }
   // variant bit 1: raster mapping; bit 7: round 2's XCD-by-XCD slot order
   P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : (h->variant & 128u) ? 2u : 0u;
   if (h->kind == VPTMCM_RENDERER_RGB)
@@ -603,31 +581,17 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n, boo
   h->march_launches++;
   h->sched_cur = c ^ 1u;
   h->grp_dirty = true;
-  if (carry) h->ctr_parity ^= 1u;
-  else h->tile_next_stale = true;
-  h->carry_pending = P.allow_stop != 0u;
-  if (h->carry_pending) memcpy(h->carry_mvp, mvp, sizeof h->carry_mvp);
+  h->done_pending = signal;
   return VPTMCM_OK;
 }
 
-// Launch the queued render() passes (see vptmcm::pend_n). keep_lag: more
-// passes follow (the queue is full), so the launch may leave owed passes;
-// otherwise (an observation, an input change, another matrix) every tile is
-// run to the last queued pass, with a completion launch if nothing is queued.
-int flush_renders(vptmcm* h, bool keep_lag = false) {
-  // VPTMCM_CARRY_NOFINAL=1 (timeline diagnostics only; results then wrong): no
-  // completion launch, so a read sees the stamps of the last early-stop launch
-  static const bool nofinal = [] {
-    const char* v = getenv("VPTMCM_CARRY_NOFINAL");
-    return v && v[0] == '1';
-  }();
-  if (nofinal) keep_lag = true;
-  if (h->pend_n == 0 && (keep_lag || !h->carry_pending)) return VPTMCM_OK;
+// Launch the queued render() passes (see vptmcm::pend_n) as one march.
+int flush_renders(vptmcm* h) {
+  if (h->pend_n == 0) return VPTMCM_OK;
   HIPCHK(h, hipSetDevice(h->device));
-  if (h->pend_n == 0) return do_march(h, h->carry_mvp, nullptr, 0, false);
   const uint32_t n = h->pend_n;
   h->pend_n = 0;
-  return do_march(h, h->pend_mvp, h->pend_seeds, n, keep_lag);
+  return do_march(h, h->pend_mvp, h->pend_seeds, n);
 }
 
 // ---- communicator waits (see vptmcm::comm_timeout_ms)
@@ -640,11 +604,8 @@ int64_t now_ms() {
 // VPTMCM_COMM_TRACE=1: timestamped lines on stderr at each stage of the
 // communicator's setup and failure handling (diagnostics of RCCL hangs).
 void comm_trace(const char* fmt, ...) {
-  static const bool on = [] {
-    const char* v = getenv("VPTMCM_COMM_TRACE");
-    return v && v[0] == '1';
-  }();
-  if (!on) return;
+  const char* on = getenv("VPTMCM_COMM_TRACE");
+  if (!on || on[0] != '1') return;
   char b[256];
   va_list ap;
   va_start(ap, fmt);
@@ -833,6 +794,7 @@ static int group_alloc(vptmcm* h, const int32_t* devs, uint32_t n) {
   });
   if (rc) return rc;
   HIPCHK(h, hipSetDevice(h->device));
+  h->done_pending = false;
   const size_t slots = h->group_transport == VPTMCM_GROUP_RCCL ? 1 : n - 1;
   if (slots) HIPCHK(h, hipMalloc(&h->grp_gather, slots * npx * sizeof(float4)));
   HIPCHK(h, hipMalloc(&h->grp_rgb32, npx * 3 * sizeof(float)));
@@ -936,6 +898,7 @@ static int group_composite(vptmcm* h) {
   int rc = for_replicas(h, [&](vptmcm* c) {
     if (int r = flush_renders(c)) return r;
     HIPCHK(c, hipSetDevice(c->device));
+    c->done_pending = false;  // the pack follows the march on this stream
     HIPCHK(c, hipStreamWaitEvent(c->stream, h->grp_done, 0));  // the last composite read the pack
     const MarchParams P = make_params(c, kNoMatrix, 0);
     HIPCHK(c, launch_pack(P, c->photons, c->rgb32, c->grp_pack, c->stream));
@@ -1075,20 +1038,13 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   CK(hipMemsetAsync(h->sched, 0, 2 * (size_t)sched_flag_bytes(h->n_tiles), h->stream));
   CK(hipMalloc(&h->sched_prev, sched_slot_words(h->n_tiles) * sizeof(uint32_t)));
   CK(hipMemsetAsync(h->sched_prev, 0xff, sched_slot_words(h->n_tiles) * sizeof(uint32_t), h->stream));
-  CK(hipMalloc(&h->tile_next, h->n_tiles * sizeof(uint32_t)));
-  CK(hipMemsetAsync(h->tile_next, 0, h->n_tiles * sizeof(uint32_t), h->stream));
-  CK(hipMalloc(&h->stop_ctr, 2 * kStopBlockWords * sizeof(uint32_t)));
-  CK(hipMemsetAsync(h->stop_ctr, 0, 2 * kStopBlockWords * sizeof(uint32_t), h->stream));
-  // carry (VPTMCM_CARRY=1): the spectral march with the balanced schedule in one
-  // chunk (R <= 512). Off by default: bit-exact, but measured no faster — the
-  // background waves' work fills the tail it removes
-  h->carry_on = false;
-  if (const char* v = getenv("VPTMCM_CARRY"))
-    h->carry_on = v[0] == '1' && h->kind == VPTMCM_RENDERER_SPECTRAL && h->n_tiles <= kSchedChunk &&
-                  (h->variant & (1u | 2u | 128u)) == 0u;
-  if (const char* v = getenv("VPTMCM_STOP_Q")) h->stop_q = (uint32_t)strtoul(v, nullptr, 10);
-  if (const char* v = getenv("VPTMCM_CARRY_BG")) h->carry_bg = v[0] == '1';
-  if (const char* v = getenv("VPTMCM_DARK")) h->dark = v[0] == '0' ? 0u : v[0] == '2' ? 2u : 1u;
+  if (const char* v = getenv("VPTMCM_DARK")) h->dark = v[0] == '0' ? 0u : 1u;
+  if (const char* v = getenv("VPTMCM_DONE_FLAG")) h->done_on = v[0] != '0';
+  CK(hipMalloc(&h->done_ctr, sizeof(uint32_t)));
+  CK(hipMemsetAsync(h->done_ctr, 0, sizeof(uint32_t), h->stream));
+  CK(hipHostMalloc(&h->done_host, sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
+  *h->done_host = 0u;
+  CK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->done_dev), h->done_host, 0));
   if (h->kind == VPTMCM_RENDERER_RGB) {  // WebGPUAbstractComputeRenderer.js:23-28
     static const uint8_t kDefaultTf[8] = {255, 0, 0, 0, 255, 0, 0, 255};
     if (vptmcm_set_transfer_function(h, kDefaultTf, 2, 1)) return fail(VPTMCM_EHIP);
@@ -1101,20 +1057,39 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
 
 void vptmcm_destroy(vptmcm* h) {
   if (!h) return;
-  for (vptmcm* c : h->peers) {  // replicas first: their streams may feed this one's composite
+  // Replicas first: their streams may feed this one's composite (they hold no
+  // communicator, so their waits are plain stream waits).
+  for (vptmcm* c : h->peers) {
     if (c->stream) (void)wait_stream(c, c->stream, "destroy");
   }
-  if (h->stream) (void)wait_stream(h, h->stream, "destroy");
+  // Bounded waits while a communicator exists or after its abort; streams that
+  // did not drain may still touch the handle's buffers (a composite kernel and
+  // its copies queued behind an RCCL call that never completed), which are
+  // then left allocated (a deliberate leak) rather than freed under running
+  // work: every device free below comes after this check.
+  bool drained = true;
+  if (h->comm_stream) drained = wait_stream(h, h->comm_stream, "destroy") == VPTMCM_OK && drained;
+  if (h->stream) drained = wait_stream(h, h->stream, "destroy") == VPTMCM_OK && drained;
   for (ncclComm_t c : h->grp_comms)
     if (c) (void)ncclCommDestroy(c);
+  h->grp_comms.clear();
+  if (h->comm && comm_call(h, ncclCommFinalize(h->comm), "destroy: ncclCommFinalize") == VPTMCM_OK)
+    (void)ncclCommDestroy(h->comm);
   for (vptmcm* c : h->peers) {
-    if (c->grp_pack) (void)hipFree(c->grp_pack);
-    if (c->grp_packed) (void)hipEventDestroy(c->grp_packed);
-    c->grp_pack = nullptr;
-    c->grp_packed = nullptr;
+    if (drained) {  // a peer's pack may be read by this handle's (undrained) composite
+      if (c->grp_pack) (void)hipFree(c->grp_pack);
+      if (c->grp_packed) (void)hipEventDestroy(c->grp_packed);
+      c->grp_pack = nullptr;
+      c->grp_packed = nullptr;
+    }
     vptmcm_destroy(c);
   }
   h->peers.clear();
+  if (!drained) {
+    comm_trace("destroy: streams not drained; device buffers left allocated");
+    delete h;
+    return;
+  }
   (void)hipSetDevice(h->device);
   if (h->grp_pack) (void)hipFree(h->grp_pack);
   if (h->grp_packed) (void)hipEventDestroy(h->grp_packed);
@@ -1125,19 +1100,6 @@ void vptmcm_destroy(vptmcm* h) {
   if (h->comp_rgb32) (void)hipFree(h->comp_rgb32);
   if (h->comp_rgba) (void)hipFree(h->comp_rgba);
   if (h->comp_counts) (void)hipFree(h->comp_counts);
-  // bounded waits while a communicator exists or after its abort; streams that
-  // did not drain may still touch the handle's buffers, which are then left
-  // allocated (a deliberate leak) rather than freed under running work
-  bool drained = true;
-  if (h->comm_stream) drained = wait_stream(h, h->comm_stream, "destroy") == VPTMCM_OK && drained;
-  if (h->stream) drained = wait_stream(h, h->stream, "destroy") == VPTMCM_OK && drained;
-  if (h->comm && comm_call(h, ncclCommFinalize(h->comm), "destroy: ncclCommFinalize") == VPTMCM_OK)
-    (void)ncclCommDestroy(h->comm);
-  if (!drained) {
-    comm_trace("destroy: streams not drained; device buffers left allocated");
-    delete h;
-    return;
-  }
   if (h->band_cover) (void)hipFree(h->band_cover);
   for (int k = 0; k < 2; k++) {
     if (h->comp[k]) (void)hipFree(h->comp[k]);
@@ -1162,8 +1124,8 @@ void vptmcm_destroy(vptmcm* h) {
   if (h->light) (void)hipFree(h->light);
   if (h->sched) (void)hipFree(h->sched);
   if (h->sched_prev) (void)hipFree(h->sched_prev);
-  if (h->tile_next) (void)hipFree(h->tile_next);
-  if (h->stop_ctr) (void)hipFree(h->stop_ctr);
+  if (h->done_ctr) (void)hipFree(h->done_ctr);
+  if (h->done_host) (void)hipHostFree(h->done_host);
   if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -1422,6 +1384,7 @@ static int set_band_one(vptmcm* h, uint32_t y0, uint32_t y1) {
   HIPCHK(h, hipSetDevice(h->device));
   h->band_y0 = y0;
   h->band_y1 = y1;
+  h->done_pending = false;
   const size_t row = (size_t)h->R * 3 * sizeof(float);
   if (y0 > 0) HIPCHK(h, hipMemsetAsync(h->rgb32, 0, y0 * row, h->stream));
   if (y1 < h->R)
@@ -1450,7 +1413,7 @@ static int reset_one(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   if (!mvp) FAIL(h, VPTMCM_EINVAL, "reset: null matrix");
   HIPCHK(h, hipSetDevice(h->device));
   MarchParams P = make_params(h, mvp, seed_bits);
-  h->tile_next_stale = true;  // no pass is owed after a reset (flush_renders ran them)
+  h->done_pending = false;
   if (h->kind == VPTMCM_RENDERER_RGB)
     HIPCHK(h, launch_reset_rgb(P, h->photons, h->stream));
   else
@@ -1466,10 +1429,7 @@ static int render_one(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   // queue the pass; a different matrix or a full queue launches the queue
   // first (the launch order, and so every result, is unchanged)
   if (h->pend_n == kMaxFusedPasses || (h->pend_n && memcmp(h->pend_mvp, mvp, sizeof h->pend_mvp))) {
-    // a full queue: more passes follow, owed passes may carry; another matrix:
-    // the queued ones complete first
-    int rc = flush_renders(h, h->pend_n == kMaxFusedPasses && !memcmp(h->pend_mvp, mvp, sizeof h->pend_mvp));
-    if (rc) return rc;
+    if (int rc = flush_renders(h)) return rc;
   }
   if (h->pend_n == 0) memcpy(h->pend_mvp, mvp, sizeof h->pend_mvp);
   h->pend_seeds[h->pend_n++] = seed_bits;
@@ -1483,10 +1443,7 @@ static int render_passes_one(vptmcm* h, const float* mvp, const uint32_t* seeds,
   HIPCHK(h, hipSetDevice(h->device));
   const uint32_t fuse = (h->variant & 4u) ? 1u : kMaxFusedPasses;  // variant bit 2: one pass per launch
   for (uint32_t k = 0; k < n; k += fuse) {
-    // every launch but the call's last may leave owed passes (carry); the last
-    // one completes every tile
-    int rc = do_march(h, mvp, seeds + k, n - k < fuse ? n - k : fuse, k + fuse < n);
-    if (rc) return rc;
+    if (int rc = do_march(h, mvp, seeds + k, n - k < fuse ? n - k : fuse)) return rc;
   }
   return VPTMCM_OK;
 }
@@ -1497,7 +1454,22 @@ static int synchronize_one(vptmcm* h) {
   HIPCHK(h, hipSetDevice(h->device));
   int rc = time_close(h);
   if (rc) return rc;
-  if ((rc = wait_stream(h, h->stream, "synchronize"))) return rc;
+  // The stream ends with a signalling march: poll its flag word (every wave's
+  // stores have landed once it holds the launch's sequence number); past the
+  // spin bound, or without a signal, wait for the stream itself.
+  bool done = false;
+  if (h->done_pending && h->sync_spin_us > 0) {
+    const volatile uint32_t* f = h->done_host;
+    const int64_t t0 = now_us();
+    for (uint32_t k = 0;; k++) {
+      if (*f == h->done_seq) {
+        done = true;
+        break;
+      }
+      if ((k & 63u) == 0u && now_us() - t0 > h->sync_spin_us) break;
+    }
+  }
+  if (!done && (rc = wait_stream(h, h->stream, "synchronize"))) return rc;
   if (h->comm_stream && (rc = wait_stream(h, h->comm_stream, "synchronize"))) return rc;
   return VPTMCM_OK;
 }
@@ -1565,6 +1537,7 @@ int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out
   T.saturation = params[3];
   const float midpoint = (mid - low) / range;
   T.exponent = (float)(-std::log((double)midpoint) / std::log(2.0)) / params[4];
+  h->done_pending = false;
   HIPCHK(h, launch_tonemap_artistic(composited(h) ? h->grp_rgba : h->rgba, (uint32_t)npx, T, h->ldr,
                                     h->stream));
   if (rgba8_out) {
@@ -1764,6 +1737,7 @@ int vptmcm_comm_allreduce_radiance(vptmcm* h) {
   if (!h->comm) FAIL(h, VPTMCM_ECOMM, "comm_allreduce_radiance: no communicator");
   HIPCHK(h, hipSetDevice(h->device));
   int k = h->comp_next;
+  h->done_pending = false;
   // the buffer must be free of the all-reduce issued two passes ago
   HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[k], 0));
   MarchParams P = make_params(h, kNoMatrix, 0);
@@ -1875,6 +1849,7 @@ int vptmcm_comm_gather_bands(vptmcm* h, float* rgb) {
   // a -0.0 pixel (-0 + +0 = +0).
   const size_t n = (size_t)h->R * h->R * 3;
   float* sum = reinterpret_cast<float*>(h->comp[h->comp_next]);  // R*R float4 >= R*R*3 floats
+  h->done_pending = false;
   HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[h->comp_next], 0));
   HIPCHK(h, hipMemcpyAsync(sum, h->rgb32, n * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(h, hipEventRecord(h->comp_ready[h->comp_next], h->stream));
@@ -1921,25 +1896,6 @@ int vptmcm_debug_last_launch(vptmcm* h, uint32_t info[4], uint64_t* launches) {
   info[2] = h->last_launch.spec;
   info[3] = h->last_launch.passes;
   if (launches) *launches = h->march_launches;
-  return VPTMCM_OK;
-}
-
-int vptmcm_debug_owed(vptmcm* h, uint32_t* out, uint32_t n_words, uint32_t* n_tiles) {
-  if (check_handle(h)) return VPTMCM_EINVAL;
-  if (int rc_ = flush_renders(h, true)) return rc_;  // queued passes launch; owed ones stay owed
-  if (!n_tiles) FAIL(h, VPTMCM_EINVAL, "debug_owed: null tile count");
-  *n_tiles = h->n_tiles;
-  if (!out) return VPTMCM_OK;
-  if (n_words < h->n_tiles) FAIL(h, VPTMCM_EINVAL, "debug_owed: output holds fewer words than tiles");
-  HIPCHK(h, hipSetDevice(h->device));
-  if (h->tile_next_stale || !h->carry_on) {
-    for (uint32_t t = 0; t < h->n_tiles; t++) out[t] = 0u;
-    return VPTMCM_OK;
-  }
-  HIPCHK(h, hipMemcpyAsync(out, h->tile_next, h->n_tiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                           h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  for (uint32_t t = 0; t < h->n_tiles; t++) out[t] = h->pass_target - out[t];
   return VPTMCM_OK;
 }
 

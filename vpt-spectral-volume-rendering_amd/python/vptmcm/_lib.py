@@ -35,7 +35,7 @@ EXPORTS = [
     "vptmcm_comm_init", "vptmcm_comm_allreduce_radiance", "vptmcm_comm_read_composite",
     "vptmcm_comm_barrier", "vptmcm_comm_allreduce_host", "vptmcm_debug_eval",
     "vptmcm_debug_verify", "vptmcm_debug_last_launch", "vptmcm_debug_schedule", "vptmcm_version",
-    "vptmcm_read_composite", "vptmcm_composite", "vptmcm_group_devices", "vptmcm_debug_owed",
+    "vptmcm_read_composite", "vptmcm_composite", "vptmcm_group_devices",
 ]
 MAX_DEVICES = 8
 GROUP_PEER, GROUP_RCCL = 0, 1
@@ -128,7 +128,6 @@ def load() -> C.CDLL:
         "vptmcm_read_composite": (C.c_int, [vp, vp, vp, vp]),
         "vptmcm_composite": (C.c_int, [vp]),
         "vptmcm_group_devices": (C.c_int, [vp, C.POINTER(C.c_int32), u32p]),
-        "vptmcm_debug_owed": (C.c_int, [vp, u32p, C.c_uint32, u32p]),
     }
     variant = bool(os.environ.get("VPTMCM_LIB"))
     for name, (res, args) in sig.items():
@@ -432,15 +431,6 @@ class Renderer:
         self._ck(self.L.vptmcm_debug_schedule(self.h, None, 0, _u32p(n)))
         out = np.empty(int(n[0]), np.uint32)
         self._ck(self.L.vptmcm_debug_schedule(self.h, _u32p(out), out.size, _u32p(n)))
-        return out
-
-    def debug_owed(self) -> np.ndarray:
-        """Per tile the passes it still owes (cross-launch balancing; queued
-        render() passes are launched first, owed ones are not run)."""
-        n = np.zeros(1, np.uint32)
-        self._ck(self.L.vptmcm_debug_owed(self.h, None, 0, _u32p(n)))
-        out = np.empty(int(n[0]), np.uint32)
-        self._ck(self.L.vptmcm_debug_owed(self.h, _u32p(out), out.size, _u32p(n)))
         return out
 
     def uniform_bins(self) -> bool:
