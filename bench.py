@@ -9,10 +9,13 @@ Workload (BASELINE.md C3 at N = 1, C4 at N = 8): 512^3 fBm volume (seed 512),
 spectral TF with HG g = 0.702, R = 512, S = 8, 12 bins, extinction 32, default
 camera. Inputs are resident in HBM before the timed region.
 
-Launch: `python bench.py --gpus N --steps K --warmup W` (N = 1), or under
+Launch: `python bench.py --gpus N --steps K --warmup W`, or under
 `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`:
 one process per GPU (LOCAL_RANK), RCCL bootstrapped torch-free (rendezvous.py).
-Rank 0 prints one JSON line.
+Without a launcher (no WORLD_SIZE) and N > 1, one process drives the N GPUs
+through one device-list handle (the north_star's one-process JS host shape:
+replica k on device k, composited on device 0); it fails if fewer than N
+devices are visible. Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -59,7 +62,7 @@ def parse():
     ap.add_argument("--volume", type=int, default=512)
     ap.add_argument("--photon-steps", type=int, default=8, help="S: steps per pass")
     ap.add_argument("--extinction", type=float, default=32.0)
-    ap.add_argument("--layout", choices=["corner8", "brick8", "linear"], default="corner8")
+    ap.add_argument("--layout", choices=["corner8", "brick8", "column4", "linear"], default="corner8")
     ap.add_argument("--tf", choices=["spectral", "grey", "zero", "materials", "materials_const"],
                     default="spectral", help="TF (non-spectral: analysis only)")
     ap.add_argument("--bins", default="12", help="spectrum bin layout (non-12: analysis only)")
@@ -70,7 +73,11 @@ def parse():
                          "registers between them, every pass stores its image); 1 = one launch "
                          "per render() call")
     ap.add_argument("--allreduce-every", type=int, default=32,
-                    help="passes between radiance all-reduces (N > 1)")
+                    help="passes between radiance composites (N > 1)")
+    ap.add_argument("--transport", choices=["peer", "rccl"], default="peer",
+                    help="N > 1 without a launcher: the device-list composite's transport "
+                         "(peer: every GPU pushes its (rgb*n, n) buffer to device 0 over its own "
+                         "xGMI link; rccl: ncclCommInitAll + grouped ncclReduce)")
     ap.add_argument("--per-pass-steps", type=int, default=64,
                     help="N > 1: passes of a second timed region compositing after EVERY pass "
                          "(north_star's 'all-reduce each progressive pass'; one launch per pass; "
@@ -204,13 +211,25 @@ def stdout_to_stderr(fn):
         os.close(saved)
 
 
+def group_devices(n: int) -> list:
+    """The device list of the launcher-less N-GPU run: 0..N-1, or the
+    comma-separated VPTMCM_BENCH_DEVICES (test-only override, e.g. "0,0" to
+    run the control flow with a repeated device on a one-GPU box)."""
+    v = os.environ.get("VPTMCM_BENCH_DEVICES")
+    devs = [int(x) for x in v.split(",")] if v else list(range(n))
+    if len(devs) != n:
+        raise SystemExit(f"VPTMCM_BENCH_DEVICES={v!r} names {len(devs)} devices, --gpus {n}")
+    return devs
+
+
 def main():
     a = parse()
     rank, world, local = rendezvous.env_world()
+    group = 1  # GPUs this process drives (a device-list handle when > 1)
     if world != a.gpus:
         if "WORLD_SIZE" in os.environ:
             raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-        world = 1
+        world, group = 1, a.gpus
     if rank != 0:
         # only rank 0's stdout carries the JSON line: everything the other
         # ranks' libraries print (RCCL's banner, warnings) goes to stderr
@@ -218,7 +237,7 @@ def main():
         os.dup2(2, 1)
     R, S = a.resolution, a.photon_steps
     layout = {"corner8": vptmcm.LAYOUT_CORNER8, "brick8": vptmcm.LAYOUT_BRICK8,
-              "linear": vptmcm.LAYOUT_LINEAR}[a.layout]
+              "column4": vptmcm.LAYOUT_COLUMN4, "linear": vptmcm.LAYOUT_LINEAR}[a.layout]
 
     # ---- inputs (synthetic)
     t = time.perf_counter()
@@ -234,7 +253,17 @@ def main():
     # VPTMCM_BENCH_DEVICE pins every rank to one ordinal (rehearsing the N > 1
     # path on a one-GPU box); the default is one GPU per local rank
     device = int(os.environ.get("VPTMCM_BENCH_DEVICE", local))
-    r = vptmcm.Renderer(R, device=device, layout=layout)
+    grouped = group > 1
+    devs = group_devices(group) if grouped else [device]
+    transport = {"peer": vptmcm.GROUP_PEER, "rccl": vptmcm.GROUP_RCCL}[a.transport]
+    if grouped:
+        try:
+            r = vptmcm.Renderer(R, layout=layout, devices=devs, transport=transport)
+        except vptmcm.VptError as e:  # e.g. fewer than N devices visible
+            raise SystemExit(f"--gpus {group} without a launcher drives devices {devs} from one "
+                             f"process through one device-list handle, and that failed: {e}")
+    else:
+        r = vptmcm.Renderer(R, device=device, layout=layout)
     r.set_volume(vol)
     r.set_material_tf(tf)
     r.set_light(spd, ldir)
@@ -244,7 +273,7 @@ def main():
     # VPTMCM_BENCH_FORCE_COMM=1: the N > 1 code path (RCCL communicator,
     # composites, barriers, max-over-ranks) with however many ranks there are,
     # e.g. one: a hardware check of that path on a one-GPU box
-    multi = world > 1 or os.environ.get("VPTMCM_BENCH_FORCE_COMM") == "1"
+    multi = world > 1 or (os.environ.get("VPTMCM_BENCH_FORCE_COMM") == "1" and not grouped)
     if multi:
         key = rendezvous.job_key()
         # every peer alive before any rank enters RCCL's bootstrap (bounded;
@@ -270,9 +299,13 @@ def main():
         if rank == 0:
             rendezvous.cleanup(key, world)
 
-    n_unfused = a.unfused_steps if not multi else 0
-    n_api = a.api_steps if not multi else 0
-    n_pp = a.per_pass_steps if multi else 0
+    # the composite that ends a region (and runs every `every` passes): the
+    # RCCL all-reduce across ranks, or the device-list handle's composite
+    composite = r.allreduce_radiance if multi else (r.composite if grouped else None)
+    single = not multi and not grouped
+    n_unfused = a.unfused_steps if single else 0
+    n_api = a.api_steps if single else 0
+    n_pp = a.per_pass_steps if not single else 0
     seeds = cf.seed_stream(a.warmup + a.steps + n_unfused + n_api + n_pp + 1, start=0, rank=rank)
     F = max(1, min(a.fuse, 32))
     every = max(1, a.allreduce_every)
@@ -292,7 +325,7 @@ def main():
         after the region's last pass (so every region ends with a composite
         the display could show). Returns the pass count of every march launch."""
         launches, done = [], 0
-        if not multi and F == 32:
+        if composite is None and F == 32:
             # one call: the library launches it in 32-pass launches, the ones
             # before the last balancing their tails across launch boundaries
             # (DESIGN.md §5, cross-launch balancing); the last completes every tile
@@ -300,13 +333,13 @@ def main():
             return [min(32, count - k) for k in range(0, count, 32)]
         while done < count:
             n = min(F, count - done)
-            if multi:  # never fuse across a composite
+            if composite:  # never fuse across a composite
                 n = min(n, every - (first - 1 + done) % every)
             r.render_passes(mvp, seeds[first + done:first + done + n])
             launches.append(n)
             done += n
-            if multi and ((first - 1 + done) % every == 0 or done == count):
-                r.allreduce_radiance()
+            if composite and ((first - 1 + done) % every == 0 or done == count):
+                composite()
         return launches
 
     r.reset(mvp, seeds[0])
@@ -339,7 +372,7 @@ def main():
     launches = passes(1 + a.warmup, a.steps)
     if stamps:
         t_enq = time.perf_counter()
-    r.synchronize()  # the march stream and (N > 1) the composite stream: the last all-reduce is done
+    r.synchronize()  # the march stream and (N > 1) the composite: the last all-reduce / composite is done
     el = time.perf_counter() - t0
     if stamps:
         clk.append((time.clock_gettime_ns(time.CLOCK_MONOTONIC), time.clock_gettime_ns(time.CLOCK_BOOTTIME)))
@@ -352,6 +385,8 @@ def main():
         # is the display's cost, not the pass's (done outside the timed region)
         r.read_composite()
         r.barrier()
+    elif grouped:
+        r.read_composite_all()  # the composite on devices[0] to the host, after the region
     kern_ms, n_launch = r.kernel_time()
     if a.no_timing:
         kern_ms, n_launch = float("nan"), len(launches)
@@ -361,7 +396,7 @@ def main():
         vals = r.allreduce_host(vals, op="max")
     el_max, kern_ms_max = float(vals[0]), float(vals[1])
 
-    photon_steps = world * R * R * S * a.steps
+    photon_steps = world * group * R * R * S * a.steps
     value = photon_steps / el_max / 1e6
     # roofline of the march kernel: the algorithmic bytes its launches
     # materialise over the GPU time of the timed region, stamped by HIP events
@@ -381,18 +416,24 @@ def main():
     per_pass = None
     if n_pp > 0:
         r.synchronize()
-        r.barrier()
+        if multi:
+            r.barrier()
         t5 = time.perf_counter()
         passes(1 + a.warmup + a.steps, n_pp, F=1, every=1)
         r.synchronize()
         el5 = time.perf_counter() - t5
-        r.read_composite()
-        r.barrier()
-        el5 = float(r.allreduce_host(np.array([el5, 0.0]), op="max")[0])
-        per_pass = {"value": round(world * R * R * S * n_pp / el5 / 1e6, 3),
+        if multi:
+            r.read_composite()
+            r.barrier()
+            el5 = float(r.allreduce_host(np.array([el5, 0.0]), op="max")[0])
+        else:
+            r.read_composite_all()
+        per_pass = {"value": round(world * group * R * R * S * n_pp / el5 / 1e6, 3),
                     "ms_per_step": round(el5 * 1e3 / n_pp, 5), "steps": n_pp,
-                    "note": "one march launch and one RCCL all-reduce of the R^2 float4 "
-                            "(rgb*n, n) buffer per pass (north_star's per-pass composite)"}
+                    "note": ("one march launch and one RCCL all-reduce of the R^2 float4 (rgb*n, n) "
+                             "buffer per pass (north_star's per-pass composite)") if multi else
+                            (f"one march launch per GPU and one device-list composite ({a.transport}) "
+                             "per pass (north_star's per-pass composite)")}
 
     unfused = None
     if n_unfused > 0:
@@ -467,7 +508,7 @@ def main():
     # a materials TF with wavelength-varying anisotropy (MODE 6: FAST geometry,
     # the TF's distinct rows and the exact wavelength-bin table in LDS)
     general = None
-    if a.general_steps > 0 and not multi:
+    if a.general_steps > 0 and single:
         r.synchronize()
         r.set_material_tf(cf.tf_materials(True))
         r.set_spectrum(cf.spectrum_buffer("8_uneven"))
@@ -494,7 +535,7 @@ def main():
     # The RGB sibling ('mcm-compute') on the same volume and camera:
     # a 256 x 1 sRGB TF ramp, HG anisotropy 0.7, white 1x1 environment
     rgb = None
-    if a.rgb_steps > 0 and not multi:
+    if a.rgb_steps > 0 and single:
         r.synchronize()
         q = vptmcm.Renderer(R, device=device, layout=layout, renderer=vptmcm.RENDERER_RGB)
         x = np.arange(256)
@@ -530,24 +571,37 @@ def main():
 
     r.synchronize()
     js_api = None
-    if a.js_steps > 0 and not multi and a.tf == "spectral" and a.camera == "default":
+    if a.js_steps > 0 and single and a.tf == "spectral" and a.camera == "default":
         js_api = js_api_line(vol, tf, spec, R, S, a.extinction, a.js_steps, a.settle_ms)
 
+    n_gpus = world * group
+    if multi:
+        parallelism = (f"photon-parallel replicas x{world}, one process per GPU, RCCL all-reduce of "
+                       f"(rgb*n, n) every {every} pass(es)")
+        comp_kind = "rccl-allreduce"
+    elif grouped:
+        parallelism = (f"photon-parallel replicas x{group} in one process (device-list handle over "
+                       f"devices {devs}), composite of (rgb*n, n) on device {devs[0]} every {every} "
+                       f"pass(es)")
+        comp_kind = {"peer": "peer-push", "rccl": "rccl-reduce"}[a.transport]
+    else:
+        parallelism, comp_kind = "single GPU", None
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mphoton-steps/s",
-            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "n_gpus": n_gpus, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(el_max * 1e3 / a.steps, 5), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {
-                "workload": f"C{'4' if multi else '3'}: {a.volume}^3 fBm volume (seed 512), spectral TF "
+                "workload": f"C{'4' if n_gpus > 1 else '3'}: {a.volume}^3 fBm volume (seed 512), spectral TF "
                             f"(HG g=0.702), R={R}, S={S}, {a.bins} bins, extinction {a.extinction}, "
                             f"{a.camera} camera",
                 "resolution": R, "photon_steps_per_pass": S, "volume": a.volume,
                 "volume_layout": a.layout, "passes_per_launch": ppl,
                 "clock_settle_ms": round(settle_ms, 1), "clock_settle_passes": settle_passes,
-                "parallelism": (f"photon-parallel replicas x{world}, RCCL all-reduce of (rgb*n, n) "
-                                f"every {every} pass(es)") if multi else "single GPU",
+                "parallelism": parallelism,
+                "composite_transport": comp_kind,
+                "devices": devs if grouped else None,
             },
             "hbm_gbps_algorithmic": round(achieved, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
@@ -590,7 +644,7 @@ def main():
             "cpu_baseline": None,
             "volume_gen_s": round(gen_s, 2),
         }
-        if world == 1 and a.cpu_seconds > 0:
+        if n_gpus == 1 and a.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(vol, tf, spec, spd, ldir, mvp, R, S, a.extinction,
                                                a.cpu_seconds)
         print(json.dumps(out), flush=True)

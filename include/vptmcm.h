@@ -58,6 +58,8 @@ extern "C" {
 #define VPTMCM_LAYOUT_LINEAR 0   /* x-fastest u8, as writeTexture lays it out */
 #define VPTMCM_LAYOUT_CORNER8 1  /* one u64 of the 8 trilinear corners per cell */
 #define VPTMCM_LAYOUT_BRICK8 2   /* CORNER8 cells in 4x4x4-cell bricks (512 B), Z-ordered inside */
+#define VPTMCM_LAYOUT_COLUMN4 3  /* per cell column the 2x2-corner quads (u32), z fastest: one
+                                    8-B load per sample from half CORNER8's footprint */
 
 /* Multi-device handles (one process driving several GPUs, SURVEY 8(b)
  * "device list/mode"): how the replicas' radiance is composited. */
@@ -203,8 +205,15 @@ int vptmcm_render_passes(vptmcm* h, const float* mvp_inverse, const uint32_t* se
                          uint32_t n);
 
 /* Block until all work enqueued on the handle's streams (march + composite) has finished.
- * The wait polls the stream for up to VPTMCM_SYNC_SPIN_US microseconds (environment,
- * read at create; default 2000, 0 = block at once) before blocking. */
+ * When the stream ends with a spectral march, its completion signal is polled: the
+ * launch's last wave writes the launch's sequence number to a word of fine-grained
+ * host memory once every wave's stores have landed (in the device's coherent L2),
+ * so the call returns without waiting for the end-of-kernel cache write-back
+ * and completion packet; every host read (vptmcm_read_*) still waits for the
+ * stream itself. Otherwise (or past the spin bound) the wait polls the stream for
+ * up to VPTMCM_SYNC_SPIN_US microseconds (environment, read at create; default
+ * 2000, 0 = block at once) before blocking. VPTMCM_DONE_FLAG=0 (read at create)
+ * turns the signal off. */
 int vptmcm_synchronize(vptmcm* h);
 
 /* ---- outputs ------------------------------------------------------------- */
@@ -257,6 +266,7 @@ int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out
  * from it are upper bounds) and the launch count since the last enable, and
  * synchronises. */
 int vptmcm_enable_kernel_timing(vptmcm* h, int enable);
+/* A device-list handle reports the longest replica's region. */
 int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches);
 
 /* ---- multi-GPU (photon-parallel replicas, RCCL over xGMI) ----------------- */
@@ -264,17 +274,22 @@ int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches);
 /* ncclGetUniqueId on rank 0; the caller ships the 128 bytes to other ranks. */
 int vptmcm_comm_unique_id(uint8_t* out /* 128 */);
 
-/* ncclCommInitRank on the handle's device, in the calling thread. RCCL
- * (2.27.7) does not return from it while its bootstrap waits for a rank that
- * never arrives (a non-blocking config included), so the caller establishes
- * that every rank is alive first (the torch-free rendezvous's join barrier,
- * python/vptmcm/rendezvous.py, bounded by VPTMCM_COMM_TIMEOUT_MS). Every later
- * wait on the communicator (an RCCL enqueue in progress, synchronize and the
- * composite reads while RCCL work is queued) polls ncclCommGetAsyncError under
- * VPTMCM_COMM_TIMEOUT_MS (environment, read here; default 120000): on an
- * asynchronous error or the timeout the communicator is aborted and the call
- * returns VPTMCM_ECOMM, so a rank that dies mid-run ends every rank instead of
- * hanging it. A device-list handle (n_devices > 1) refuses (VPTMCM_ESTATE). */
+/* ncclCommInitRank on the handle's device. RCCL (2.27.7) does not return from
+ * it while its bootstrap waits for a rank that never arrives (a non-blocking
+ * config included), so the caller first establishes that every rank is alive
+ * (the torch-free rendezvous's join barrier, python/vptmcm/rendezvous.py,
+ * bounded by VPTMCM_COMM_TIMEOUT_MS). The call itself is bounded too: the
+ * initialisation runs on a helper thread, joined when it returns; if it has not
+ * returned within VPTMCM_COMM_TIMEOUT_MS (environment, read here; default
+ * 120000; a peer that joined and then died) the call returns VPTMCM_ECOMM and
+ * the helper thread, blocked inside RCCL, is detached: the caller must then
+ * end the process without running exit handlers (_exit). Every later wait on
+ * the communicator (an RCCL enqueue in progress, synchronize and the composite
+ * reads while RCCL work is queued) polls ncclCommGetAsyncError under the same
+ * bound: on an asynchronous error or the timeout the communicator is aborted
+ * and the call returns VPTMCM_ECOMM, so a rank that dies mid-run ends every
+ * rank instead of hanging it. A device-list handle (n_devices > 1) refuses
+ * (VPTMCM_ESTATE). */
 int vptmcm_comm_init(vptmcm* h, const uint8_t* unique_id, int nranks, int rank);
 
 /* Enqueue the cross-rank radiance composite of the current pass:

@@ -30,8 +30,15 @@ DRIVER = textwrap.dedent('''
     LOG = []
 
     class Fake:
-        def __init__(self, R, device=0, layout=1):
-            LOG.append(["create", R, device, layout])
+        def __init__(self, R, device=0, layout=1, devices=None, transport=0):
+            if devices is not None:
+                ndev = int(os.environ.get("FAKE_NDEV", "8"))
+                bad = [d for d in devices if d >= ndev]
+                if bad:  # the library refuses an ordinal past the device count
+                    raise bench.vptmcm.VptError(-1, f"devices: {bad[0]} is not a device ordinal ({ndev} devices)")
+                LOG.append(["create_group", R, list(devices), transport, layout])
+            else:
+                LOG.append(["create", R, device, layout])
             self.t0, self.launches = None, 0
         def set_volume(self, v): LOG.append(["volume", list(v.shape)])
         def set_material_tf(self, tf): pass
@@ -50,6 +57,7 @@ DRIVER = textwrap.dedent('''
         def render_passes(self, mvp, seeds):
             LOG.append(["passes", [int(s) for s in seeds]])
             self.launches += 1
+            time.sleep(float(os.environ.get("FAKE_PASS_SLEEP", "0")))
         def synchronize(self): pass
         def enable_kernel_timing(self, on):
             self.t0, self.launches = time.perf_counter(), 0
@@ -63,11 +71,17 @@ DRIVER = textwrap.dedent('''
         def read_composite(self):
             LOG.append(["composite"])
             return np.zeros((4, 4, 3), np.float32), np.zeros((4, 4), np.float32)
+        def composite(self):
+            LOG.append(["group_composite"])
+        def read_composite_all(self):
+            LOG.append(["read_group_composite"])
         def allreduce_host(self, vals, op="sum"):
             t = __import__("torch").tensor(np.asarray(vals, np.float64))
             dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
             return t.numpy()
-        def close(self): dist.destroy_process_group()
+        def close(self):
+            if dist.is_initialized():
+                dist.destroy_process_group()
 
     bench.vptmcm.Renderer = Fake
     bench.vptmcm.unique_id = lambda: os.urandom(128)
@@ -208,3 +222,67 @@ def test_bench_hung_comm_init_ends_every_rank(tmp_path):
         assert "did not return within 4 s" in e
         assert not [ln for ln in o.splitlines() if ln.startswith("{")]
     assert took < 90, took
+
+
+def _run_launcherless(tmp_path, argv, **env_extra):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(BENCH_ARGV=json.dumps(argv), BENCH_PATH=str(REPO / "bench.py"),
+               LOG_OUT=str(tmp_path / "log.json"), **env_extra)
+    return subprocess.run([sys.executable, "-c", DRIVER], env=env, capture_output=True, text=True,
+                          cwd=str(tmp_path), timeout=300)
+
+
+@pytest.mark.parametrize("transport", ["peer", "rccl"])
+def test_bench_gpus4_without_launcher_is_one_device_list_handle(tmp_path, transport):
+    """`python bench.py --gpus 4` with no launcher: one
+    process, ONE 4-device handle over devices 0..3 (the north_star's JS host
+    shape), the timed region ends with the device-list composite, the line
+    reports n_gpus 4, the parallelism and the composite transport, and the
+    whole-job value counts all four replicas' photon-steps."""
+    argv = ["--gpus", "4", "--steps", "20", "--warmup", "5", "--volume", "16", "--resolution", "16",
+            "--cpu-seconds", "0", "--transport", transport]
+    p = _run_launcherless(tmp_path, argv, FAKE_NDEV="4", FAKE_PASS_SLEEP="0.002")
+    assert p.returncode == 0, p.stdout + p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 4 and rec["config"]["workload"].startswith("C4")
+    assert rec["config"]["devices"] == [0, 1, 2, 3]
+    assert rec["config"]["composite_transport"] == {"peer": "peer-push", "rccl": "rccl-reduce"}[transport]
+    assert "one process" in rec["config"]["parallelism"] and "x4" in rec["config"]["parallelism"]
+    assert rec["cpu_baseline"] is None and rec["unfused"] is None
+    log = json.loads((tmp_path / "log.json").read_text())
+    creates = [e for e in log if e[0].startswith("create")]
+    assert creates == [["create_group", 16, [0, 1, 2, 3], 0 if transport == "peer" else 1, 1]]
+    assert not [e for e in log if e[0] in ("comm_init", "allreduce")]
+    t = [e[0] for e in log].index("timing")
+    after = [e[0] for e in log[t + 1:]]
+    last_pass = max(i for i, k in enumerate(after[:after.index("read_group_composite")]) if k == "passes")
+    assert "group_composite" in after[last_pass:after.index("read_group_composite")], \
+        "timed region must end with the composite"
+    # the whole job: 4 replicas x R^2 x S x steps over the region's wall time
+    assert abs(rec["value"] - 4 * 16 * 16 * 8 * 20 / (rec["roofline"]["region_wall_us"] * 1e-6) / 1e6) \
+        <= 0.01 * rec["value"]
+
+
+def test_bench_gpus2_with_one_visible_device_fails(tmp_path):
+    """Fewer visible devices than --gpus and no launcher: exit non-zero with the
+    library's reason, no result line (never a silent one-GPU run)."""
+    argv = ["--gpus", "2", "--steps", "20", "--warmup", "5", "--volume", "16", "--resolution", "16",
+            "--cpu-seconds", "0"]
+    p = _run_launcherless(tmp_path, argv, FAKE_NDEV="1")
+    assert p.returncode != 0
+    assert "not a device ordinal" in p.stderr and "device-list handle" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_devices_override_repeats_a_device(tmp_path):
+    """VPTMCM_BENCH_DEVICES (test-only) repeats device 0: the control flow of
+    --gpus 2 on a one-GPU box."""
+    argv = ["--gpus", "2", "--steps", "20", "--warmup", "5", "--volume", "16", "--resolution", "16",
+            "--cpu-seconds", "0"]
+    p = _run_launcherless(tmp_path, argv, FAKE_NDEV="1", VPTMCM_BENCH_DEVICES="0,0")
+    assert p.returncode == 0, p.stdout + p.stderr
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert rec["n_gpus"] == 2 and rec["config"]["devices"] == [0, 0]

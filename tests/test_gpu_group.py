@@ -217,3 +217,30 @@ def test_group_rgb_sibling_composites():
     assert_rgb32_equal(g.read_rgb(), want_rgb, "RGB sibling composite")
     assert_rgba_equal(g.read_rgba16f(), want_rgba, "RGB sibling composite")
     g.close()
+
+
+def test_bench_launcherless_two_gpus_repeated_device():
+    """bench.py --gpus 2 without a launcher on the one-GPU box (VERDICT r04
+    next 1): the test-only VPTMCM_BENCH_DEVICES=0,0 repeats device 0, so the
+    launcher-less path runs end to end on hardware — one process, one
+    2-replica device-list handle, each timed region ending with the PEER
+    composite — and the line reports 2 GPUs, the device list and the
+    transport. (Two replicas share one GPU here, so the value says nothing
+    about N-GPU scaling: N > 1 distinct GPUs stay unmeasured.)"""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    env["VPTMCM_BENCH_DEVICES"] = "0,0"
+    p = subprocess.run([sys.executable, str(repo / "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5",
+                        "--volume", "64", "--resolution", "64", "--cpu-seconds", "0", "--settle-ms", "20",
+                        "--per-pass-steps", "8"], env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout + p.stderr[-3000:]
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["n_gpus"] == 2 and rec["config"]["devices"] == [0, 0]
+    assert rec["config"]["composite_transport"] == "peer-push" and "one process" in rec["config"]["parallelism"]
+    assert rec["value"] > 0 and rec["per_pass_allreduce"]["value"] > 0
+    assert rec["roofline"]["passes_per_launch"] == 20

@@ -1,0 +1,73 @@
+"""Every environment knob the library reads ("Environment
+knobs") leaves every result bit unchanged: the same small
+case — a fused call, queued render() passes, a camera change, timing on — is
+rendered once per knob setting, each in a fresh handle (knobs are read at
+vptmcm_create), and photons, the fp32 image and the rgba16f image must equal
+the knob-free run, which itself equals the oracle."""
+import numpy as np
+import pytest
+
+import vptmcm
+from vptmcm import configs as cf
+
+from test_gpu_parity import assert_photons_equal, assert_rgb32_equal, assert_rgba_equal, make_pair
+
+pytestmark = pytest.mark.gpu
+
+# (variable, value): every documented knob, each variant bit of VPTMCM_MARCH_VARIANT
+KNOBS = [("VPTMCM_MARCH_VARIANT", str(b)) for b in (1, 2, 4, 8, 16, 32, 64, 128)] + [
+    ("VPTMCM_MARCH_VARIANT", "255"),
+    ("VPTMCM_DARK", "0"),
+    ("VPTMCM_DONE_FLAG", "0"),
+    ("VPTMCM_TIME_STOP", "0"),
+    ("VPTMCM_TIME_BEGIN", "marker"),
+    ("VPTMCM_SYNC_SPIN_US", "0"),
+    ("VPTMCM_SYNC_SPIN", "1"),
+    ("VPTMCM_COMM_TRACE", "1"),
+    ("VPTMCM_COMM_TIMEOUT_MS", "5000"),
+]
+
+
+def _run(layout, tf, spec, with_oracle=False):
+    R = 64
+    vol = cf.fbm_volume(48, 21, nthreads=8)
+    gpu, cpu = make_pair(R, vol, tf, spec=spec, ext=24.0, layout=layout)
+    m1, m2 = cf.golden_mvp("orbit"), cf.default_mvp_inverse()
+    seeds = cf.seed_stream(14, start=3)
+    gpu.enable_kernel_timing(True)
+    gpu.reset(m1, seeds[0])
+    gpu.render_passes(m1, seeds[1:7])
+    for s in seeds[7:10]:
+        gpu.render(m1, s)
+    for s in seeds[10:]:
+        gpu.render(m2, s)
+    gpu.synchronize()
+    ms, n = gpu.kernel_time()
+    assert n >= 2 and ms > 0
+    got = (gpu.read_photons(), gpu.read_rgb(), gpu.read_rgba16f())
+    gpu.close()
+    if with_oracle:
+        cpu.reset(m1, seeds[0], nthreads=16)
+        for k, s in enumerate(seeds[1:], 1):
+            rgb, want = cpu.render(m1 if k < 10 else m2, s, nthreads=16)
+        assert_photons_equal(got[0], cpu.photons, "no knobs vs oracle")
+        assert_rgb32_equal(got[1], rgb, "no knobs vs oracle")
+        assert_rgba_equal(got[2], want, "no knobs vs oracle")
+    return got
+
+
+@pytest.mark.parametrize("layout,tfname,spec", [(vptmcm.LAYOUT_CORNER8, "spectral", "12"),
+                                                (vptmcm.LAYOUT_BRICK8, "materials", "8_uneven")])
+def test_every_knob_leaves_the_bits(layout, tfname, spec, monkeypatch):
+    tf = cf.tf_spectral() if tfname == "spectral" else cf.tf_materials(True)
+    for var, _ in KNOBS:
+        monkeypatch.delenv(var, raising=False)
+    base = _run(layout, tf, spec, with_oracle=True)
+    for var, val in KNOBS:
+        monkeypatch.setenv(var, val)
+        got = _run(layout, tf, spec)
+        monkeypatch.delenv(var)
+        what = f"{var}={val}"
+        assert_photons_equal(got[0], base[0], what)
+        assert_rgb32_equal(got[1], base[1], what)
+        assert_rgba_equal(got[2], base[2], what)

@@ -15,7 +15,7 @@ from vptmcm import configs as cf
 
 pytestmark = pytest.mark.gpu
 
-LAYOUTS = [vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_LINEAR, vptmcm.LAYOUT_BRICK8]
+LAYOUTS = [vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_LINEAR, vptmcm.LAYOUT_BRICK8, vptmcm.LAYOUT_COLUMN4]
 
 
 def same_words(a: np.ndarray, b: np.ndarray) -> np.ndarray:
@@ -334,7 +334,10 @@ def test_blockwise_volume_ingest_equals_whole():
     for r in (a, b):
         r.reset(mvp, 5)
         r.render(mvp, 6)
-    assert np.array_equal(a.read_photons(), b.read_photons())
+    cpu.reset(mvp, 5)
+    cpu.render(mvp, 6)
+    assert_photons_equal(b.read_photons(), cpu.photons, "whole volume")
+    assert_photons_equal(a.read_photons(), cpu.photons, "block-wise volume")
     a.close()
     b.close()
 
@@ -387,6 +390,21 @@ def test_composite_single_rank():
     assert np.array_equal(n.reshape(-1), ph[:, 7].astype(np.float32))
     m = n > 0
     np.testing.assert_allclose(rgb[m], img[m], rtol=3e-7, atol=0)  # (rgb*n)/n: <= 2 roundings
+
+    def from_pack(pk):  # k_composite of one (rgb*n, n) buffer, in numpy (f32, correctly rounded)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            return np.where(pk[..., 3:] > 0, pk[..., :3] / pk[..., 3:], np.float32(0)).astype(np.float32)
+
+    # the march wrote the all-reduced buffer itself (k_pack's values, no k_pack
+    # launch): bit-exact against k_pack's buffer through the same division
+    assert_rgb32_equal(rgb, from_pack(gpu.pack_radiance()), "fused pack vs k_pack")
+    # a reset between the march and the all-reduce: k_pack packs the reset photons
+    gpu.render_passes(mvp, cf.seed_stream(4, start=7))
+    gpu.reset(mvp, 9)
+    gpu.allreduce_radiance()
+    rgb2, n2 = gpu.read_composite()
+    assert (n2 == 0).all()  # a reset zeroes every sample count
+    assert_rgb32_equal(rgb2, from_pack(gpu.pack_radiance()), "k_pack after a reset")
     gpu.barrier()
     v = gpu.allreduce_host([1.0, 2.0], op="max")
     assert list(v) == [1.0, 2.0]

@@ -270,3 +270,28 @@ def test_js_device_list_renderer_composites(tmp_path):
     want_rgb, want_rgba, _ = _composite(reps)
     assert np.array_equal(rgba, want_rgba)
     assert same(run_case.rgb32.view(np.uint32), want_rgb.view(np.uint32))
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+def test_napi_comm_init():
+    """The communicator through the N-API shim: a one-rank
+    communicator composites a pass (the composite of one replica is its own
+    image); a two-rank communicator whose rank 1 never arrives makes commInit
+    throw the communicator error within VPTMCM_COMM_TIMEOUT_MS instead of
+    blocking the JS host forever, and the process then ends."""
+    import os
+    import time
+    r = subprocess.run(["node", str(ROOT / "tests" / "js" / "comm_init.js"), "one"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["uid_bytes"] == 128 and out["max_rel"] <= 2.5e-7, out
+    env = dict(os.environ, VPTMCM_COMM_TIMEOUT_MS="3000")
+    t0 = time.monotonic()
+    r = subprocess.run(["node", str(ROOT / "tests" / "js" / "comm_init.js"), "never"], capture_output=True,
+                       text=True, timeout=120, env=env)
+    took = time.monotonic() - t0
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out.get("code") == -5 and "did not return within 3000 ms" in out["message"], out
+    assert 3000 <= out["took_ms"] < 20000, out
+    assert r.returncode == 3 and took < 100, (r.returncode, took, r.stderr[-2000:])

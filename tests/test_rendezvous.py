@@ -56,19 +56,21 @@ def test_stale_payload_of_another_attempt_is_ignored(monkeypatch):
         rendezvous.cleanup(key)
 
 
-def _join_worker(rank, world, key, q):
+def _join_worker(rank, world, key, q, done):
     rendezvous.join(rank, world, key=key, timeout_s=30)
     q.put(rank)
+    done.wait(60)  # a rank stays alive past the join (a marker counts only while its process runs)
 
 
 def test_join_all_ranks_present():
     key = f"join-{os.getpid()}"
     ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_join_worker, args=(r, 3, key, q)) for r in (2, 0, 1)]
+    q, done = ctx.Queue(), ctx.Event()
+    procs = [ctx.Process(target=_join_worker, args=(r, 3, key, q, done)) for r in (2, 0, 1)]
     for p in procs:
         p.start()
     got = sorted(q.get(timeout=60) for _ in procs)
+    done.set()
     for p in procs:
         p.join(30)
         assert p.exitcode == 0
@@ -99,3 +101,31 @@ def test_join_timeout_from_environment(monkeypatch):
     assert rendezvous.default_timeout_s() == 2.5
     monkeypatch.setenv("VPTMCM_COMM_TIMEOUT_MS", "junk")
     assert rendezvous.default_timeout_s() == 120.0
+
+
+def test_stale_join_marker_is_not_a_live_peer(tmp_path):
+    """A join marker left by a rank that is gone (a crashed job with the same
+    key, or a reused pid with another start time) does not count as present:
+    rank 0 still fails in the rendezvous, and removes its own marker when it
+    does."""
+    import subprocess
+    import sys
+
+    import pytest
+    key = f"stale-{os.getpid()}"
+    p = subprocess.run([sys.executable, "-c", "import os; print(os.getpid())"], capture_output=True,
+                       text=True, check=True)
+    dead = int(p.stdout)
+    rendezvous.join_path(key, 1).write_text(f"{key}\n{dead}\n12345")  # a rank that exited
+    rendezvous.join_path(key, 2).write_text(f"{key}\n{os.getpid()}\n1")  # live pid, wrong start time
+    try:
+        assert not rendezvous.marker_alive(rendezvous.join_path(key, 1), key)
+        assert not rendezvous.marker_alive(rendezvous.join_path(key, 2), key)
+        with pytest.raises(rendezvous.RendezvousError, match=r"\[1, 2\]"):
+            rendezvous.join(0, 3, key=key, timeout_s=0.3)
+        assert not rendezvous.join_path(key, 0).exists()  # its own marker is gone
+        # a live marker of the same key from this very process counts
+        rendezvous.join(0, 1, key=key, timeout_s=5)
+        assert rendezvous.marker_alive(rendezvous.join_path(key, 0), key)
+    finally:
+        rendezvous.cleanup(key, 3)

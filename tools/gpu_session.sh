@@ -66,6 +66,24 @@ for s in $STEPS; do
   ingest)  # block-wise volume ingest time (tools/ingest_time.py)
     timeout -k 10 300 python tools/ingest_time.py > $OUT/ingest.jsonl 2> $OUT/ingest.err
     rc=$?; echo "ingest rc=$rc" | tee -a $OUT/status.txt; cat $OUT/ingest.jsonl; fault $rc && exit $rc ;;
+  layoutab)  # volume layouts alternating on one box: "volume:layout:camera" cases, µs per fused pass
+    for c in ${LAYOUT_CASES:-512:corner8:default 512:column4:default 512:corner8:default 512:column4:default 512:corner8:orbit 512:column4:orbit 1024:corner8:default 1024:column4:default 1024:corner8:default 1024:column4:default}; do
+      IFS=: read v l cam <<< "$c"
+      timeout -k 10 300 python bench.py --volume $v --layout $l --camera $cam --steps 256 --warmup 256 --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 0 --unfused-steps 0 > $OUT/lay.json 2>> $OUT/layoutab.err
+      rc=$?; [ $rc -ne 0 ] && { echo "layoutab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      python3 -c "import json; d=json.load(open('$OUT/lay.json')); r=d['roofline']; print(json.dumps({'case': '$c', 'value': d['value'], 'us_per_pass': r['kernel_us_per_pass']}))" >> $OUT/layoutab.jsonl
+    done
+    echo "layoutab rc=0" | tee -a $OUT/status.txt; cat $OUT/layoutab.jsonl ;;
+  diag)  # a diagnostic script: DIAG=tools/<script>.py
+    timeout -k 10 300 python ${DIAG} > $OUT/diag.jsonl 2> $OUT/diag.err
+    rc=$?; echo "diag rc=$rc" | tee -a $OUT/status.txt; cat $OUT/diag.jsonl; fault $rc && exit $rc ;;
+  flagab)  # the driver's command, alternating the completion signal off (VPTMCM_DONE_FLAG=0) and on
+    for f in ${FLAG_CASES:-0 1 0 1 0 1 0 1 0 1}; do
+      VPTMCM_DONE_FLAG=$f timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 > $OUT/flag_$f.json 2>> $OUT/flagab.err
+      rc=$?; [ $rc -ne 0 ] && { echo "flagab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      python3 -c "import json; d=json.load(open('$OUT/flag_$f.json')); r=d['roofline']; print(json.dumps({'done_flag': $f, 'value': d['value'], 'region_wall_us': r['region_wall_us'], 'kernel_us': r['kernel_avg_us'], 'wall_minus_kernel_us': r['wall_minus_kernel_us']}))" >> $OUT/flagab.jsonl
+    done
+    echo "flagab rc=0" | tee -a $OUT/status.txt; cat $OUT/flagab.jsonl ;;
   drvab)  # the driver's command, alternating the round-3 library (VPTMCM_LIB=r03) and the current one
     for lib in ${DRV_LIBS:-r03 cur r03 cur r03 cur r03 cur}; do
       if [ $lib = cur ]; then unset VPTMCM_LIB; else export VPTMCM_LIB=$lib; fi

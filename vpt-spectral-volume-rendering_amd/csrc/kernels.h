@@ -42,6 +42,9 @@ struct TileSched {
   // host polls. Null: no signal.
   uint32_t* done_ctr;
   uint32_t* done_flag;
+  // (rgb * n, n) per pixel of the launch's last pass (k_pack's values, written
+  // with the image; the cross-rank composite's buffer), or null
+  float4* pack;
 };
 // Flag byte of a tile (written by each launch for the next one's schedule):
 // bit 0 its wave entered the volume.
@@ -104,6 +107,10 @@ hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSee
 hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, uint32_t BW,
                           uint32_t BH, void* out, hipStream_t s, const uint32_t c0[3] = nullptr,
                           const uint32_t n[3] = nullptr);
+// LINEAR -> COLUMN4 quads of the box [c0, c0 + n) over (cx, cy, k) (default:
+// every quad of the (W+1)(H+1)(D+2) grid)
+hipError_t launch_column4(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, void* out,
+                          hipStream_t s, const uint32_t c0[3] = nullptr, const uint32_t n[3] = nullptr);
 hipError_t launch_pack(const MarchParams& P, const float* ph, const float* rgb32, float4* out,
                        hipStream_t s);
 // Multi-replica composite (k_composite): the n source buffers of R^2 (rgb*n, n)

@@ -104,6 +104,15 @@ __device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) 
   return r;
 }
 
+// 8 bytes at a 4-B-aligned address as one global_load_dwordx2 (COLUMN4)
+struct alignas(4) U32x2 {
+  uint32_t x, y;
+};
+__device__ __forceinline__ uint2 load8_a4(const uint8_t* __restrict__ p) {
+  const U32x2 v = *reinterpret_cast<const U32x2*>(p);
+  return make_uint2(v.x, v.y);
+}
+
 template <uint32_t L>
 __device__ __forceinline__ VolTap vol_fetch(const MarchParams& P, const uint8_t* __restrict__ vol,
                                             f3 q) {
@@ -123,6 +132,18 @@ __device__ __forceinline__ VolTap vol_fetch(const MarchParams& P, const uint8_t*
       c = *reinterpret_cast<const uint2*>(vol + ((brick << 9) | inner));
     else
       c = *reinterpret_cast<const uint2*>(vol + (((size_t)brick << 9) | inner));
+    t.lo = c.x;
+    t.hi = c.y;
+  } else if constexpr (L == kTplColumn4 || L == kTplColumn4Wide) {
+    const uint32_t W1 = P.W + 1u, D2 = P.D + 2u;
+    const uint32_t cx = (uint32_t)(clampi(ix + 1, (int)P.W));
+    const uint32_t cy = (uint32_t)(clampi(iy + 1, (int)P.H));
+    const uint32_t cz = (uint32_t)(clampi(iz + 1, (int)P.D));
+    uint2 c;
+    if constexpr (L == kTplColumn4)  // quad index (cy * W1 + cx) * D2 + cz, 32-bit byte offset
+      c = load8_a4(vol + ((__umul24(mad_u24(cy, W1, cx), D2) + cz) << 2));
+    else
+      c = load8_a4(vol + ((((size_t)cy * W1 + cx) * D2 + cz) << 2));
     t.lo = c.x;
     t.hi = c.y;
   } else if constexpr (L == kTplCorner8 || L == kTplCorner8Wide) {
@@ -320,17 +341,23 @@ __device__ uint32_t schedule_tile(const MarchParams& P, uint32_t f0, const uint8
 // | vmcnt_hi[15:14]) for vmcnt(0) with expcnt and lgkmcnt left unconstrained.
 constexpr uint32_t kWaitVmcnt0 = 0x0F70u;
 // Completion signal (TileSched::done_ctr, done_flag): once this wave's stores
-// have landed (vmcnt(0)), lane 0 adds it to the launch's cumulative wave count;
-// the wave that completes the count writes the launch's sequence number to
-// the host's flag word with a vector store at system scope (the host polls
-// it in vptmcm_synchronize instead of waiting for the end-of-kernel packet).
-__device__ __forceinline__ void signal_done(const MarchParams& P, const TileSched& T) {
+// have landed (vmcnt(0)), lane 0 counts it in the block's LDS word s_done; the
+// block's last wave adds the block to the launch's cumulative block count in
+// device memory (one device-scope atomic per block: one per wave serialised
+// ~30 us onto the tail of a one-pass launch), and the block that completes
+// the count writes the launch's sequence number to the host's flag word with a
+// vector store at system scope (the host polls it in vptmcm_synchronize
+// instead of waiting for the end-of-kernel packet).
+__device__ __forceinline__ void signal_done(const MarchParams& P, const TileSched& T, uint32_t* s_done) {
   if (T.done_flag == nullptr) return;
   __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
   if ((threadIdx.x & 63u) == 0u) {
-    const uint32_t old = __hip_atomic_fetch_add(T.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1u == P.done_target)
-      __hip_atomic_store(T.done_flag, P.done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t w = __hip_atomic_fetch_add(s_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (w + 1u == kMarchBlock / 64u) {
+      const uint32_t old = __hip_atomic_fetch_add(T.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old + 1u == P.done_target)
+        __hip_atomic_store(T.done_flag, P.done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 // The tile of a packed schedule slot word (TileSched::prev, s_tile).
@@ -422,6 +449,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 
   __shared__ uint32_t s_red[64];
   __shared__ uint32_t s_tile[16];
+  __shared__ uint32_t s_done;  // the block's waves past their stores (signal_done)
+  if (threadIdx.x == 0u) s_done = 0u;  // published by the prologue's barriers
 
   TL_DECL();
   TL_MARK(0);
@@ -522,7 +551,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   if (!live || PS.n == 0u) {
     // an idle out-of-band tile (or a launch of no pass): its flag carries over
     if (tile < P.n_tiles && lane == 0u) T.flags_out[tile] = (live && hot0) ? kFlagVolume : 0u;
-    signal_done(P, T);
+    signal_done(P, T, &s_done);
     return;
   }
   const uint16_t* s_tf = reinterpret_cast<const uint16_t*>(s_tf4);
@@ -625,6 +654,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       o[0] = r;
       o[1] = g;
       o[2] = bl;
+      if (T.pack != nullptr) {  // k_pack's (rgb * n, n) from the same values
+        const float n = (float)p.samples;
+        T.pack[(size_t)y * P.R + x] = make_float4(r * n, g * n, bl * n, n);
+      }
     }
   };
   // Dark background (MarchParams::dark, FAST geometry): a wave whose every
@@ -916,7 +949,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     if (NBF || !VPT_NB_ZERO || (uint32_t)b < P.nb) ph[(kRad0 + b) * S + i] = p.rad[b];
 
   if (lane == 0u) T.flags_out[tile] = entered;  // the next launch's schedule
-  signal_done(P, T);
+  signal_done(P, T, &s_done);
   STAMP_END(rgb32, tile, entered);
   TL_END(rgb32, tile, entered, 0u);
 }
@@ -1195,6 +1228,29 @@ __global__ __launch_bounds__(256) void k_corner8(const uint8_t* __restrict__ lin
   }
 }
 
+// COLUMN4 quads of the box [c0, c0 + n) over (cx, cy, k), k in [0, D + 1]:
+// q(cx, cy, k) = voxels (clamp(cx-1 .. cx), clamp(cy-1 .. cy)) at z = clamp(k - 1),
+// byte (dy * 2 + dx); quad index (cy * (W + 1) + cx) * (D + 2) + k.
+__global__ __launch_bounds__(256) void k_column4(const uint8_t* __restrict__ lin, uint32_t W,
+                                                 uint32_t H, uint32_t D, uint32_t* __restrict__ out,
+                                                 uint3 c0, uint3 n) {
+  const uint32_t W1 = W + 1u, D2 = D + 2u;
+  const size_t nbox = (size_t)n.x * n.y * n.z;
+  for (size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x; c < nbox;
+       c += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t k = c0.z + (uint32_t)(c % n.z);  // z fastest, as stored
+    const size_t rest = c / n.z;
+    const uint32_t cx = c0.x + (uint32_t)(rest % n.x);
+    const uint32_t cy = c0.y + (uint32_t)(rest / n.x);
+    const uint32_t x0 = clampi((int)cx - 1, (int)W - 1), x1 = clampi((int)cx, (int)W - 1);
+    const uint32_t y0 = clampi((int)cy - 1, (int)H - 1), y1 = clampi((int)cy, (int)H - 1);
+    const uint32_t z = clampi((int)k - 1, (int)D - 1);
+    const size_t r0 = ((size_t)z * H + y0) * W, r1 = ((size_t)z * H + y1) * W;
+    out[((size_t)cy * W1 + cx) * D2 + k] = (uint32_t)lin[r0 + x0] | ((uint32_t)lin[r0 + x1] << 8) |
+                                           ((uint32_t)lin[r1 + x0] << 16) | ((uint32_t)lin[r1 + x1] << 24);
+  }
+}
+
 // ----------------------------------------------------- multi-GPU composite
 // (rgb * n, n) per pixel from the fp32 image of the last pass (before its f16
 // rounding) and the photon sample count n: the running mean rgb weighted by
@@ -1345,6 +1401,7 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   else mode = 0u;
   uint32_t tpl;
   if (layout == kLayoutBrick8) tpl = P.vol32 ? kTplBrick8 : kTplBrick8Wide;
+  else if (layout == kLayoutColumn4) tpl = P.vol32 ? kTplColumn4 : kTplColumn4Wide;
   else if (layout == kLayoutCorner8) tpl = P.vol32 ? kTplCorner8 : kTplCorner8Wide;
   else tpl = kTplLinear;
   if (info) *info = MarchLaunchInfo{mode, tpl, spec ? 1u : 0u, PS.n};
@@ -1371,6 +1428,8 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   switch (tpl) {
     case kTplBrick8: VPT_LAUNCH_NB(kTplBrick8); break;
     case kTplBrick8Wide: VPT_LAUNCH_NB(kTplBrick8Wide); break;
+    case kTplColumn4: VPT_LAUNCH_NB(kTplColumn4); break;
+    case kTplColumn4Wide: VPT_LAUNCH_NB(kTplColumn4Wide); break;
     case kTplCorner8: VPT_LAUNCH_NB(kTplCorner8); break;
     case kTplCorner8Wide: VPT_LAUNCH_NB(kTplCorner8Wide); break;
     default: VPT_LAUNCH_NB(kTplLinear); break;
@@ -1393,6 +1452,7 @@ hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSee
   const bool geo = P.w_bounded && P.blur == 0.0f && (P.R & 1u) == 0u;
   if (info) {  // mode: 1 with the FAST geometry (k_march_rgb<L, true>), else 0
     const uint32_t tpl = layout == kLayoutBrick8 ? (P.vol32 ? kTplBrick8 : kTplBrick8Wide)
+                       : layout == kLayoutColumn4 ? (P.vol32 ? kTplColumn4 : kTplColumn4Wide)
                        : layout == kLayoutCorner8 ? (P.vol32 ? kTplCorner8 : kTplCorner8Wide)
                        : kTplLinear;
     *info = MarchLaunchInfo{geo ? 1u : 0u, tpl, 1u, PS.n};
@@ -1410,6 +1470,10 @@ hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSee
     VPT_LAUNCH_RGB(kTplBrick8);
   else if (layout == kLayoutBrick8)
     VPT_LAUNCH_RGB(kTplBrick8Wide);
+  else if (layout == kLayoutColumn4 && P.vol32)
+    VPT_LAUNCH_RGB(kTplColumn4);
+  else if (layout == kLayoutColumn4)
+    VPT_LAUNCH_RGB(kTplColumn4Wide);
   else if (layout == kLayoutCorner8 && P.vol32)
     VPT_LAUNCH_RGB(kTplCorner8);
   else if (layout == kLayoutCorner8)
@@ -1432,6 +1496,20 @@ hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D
   if (blocks > 65536) blocks = 65536;
   hipLaunchKernelGGL(k_corner8, dim3((uint32_t)blocks), dim3(256), 0, s, lin, W, H, D, BW, BH,
                      reinterpret_cast<uint2*>(out), o, e);
+  return hipGetLastError();
+}
+
+hipError_t launch_column4(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, void* out,
+                          hipStream_t s, const uint32_t c0[3], const uint32_t n[3]) {
+  const uint3 o = c0 ? make_uint3(c0[0], c0[1], c0[2]) : make_uint3(0u, 0u, 0u);
+  const uint3 e = n ? make_uint3(n[0], n[1], n[2]) : make_uint3(W + 1u, H + 1u, D + 2u);
+  if (o.x + e.x > W + 1u || o.y + e.y > H + 1u || o.z + e.z > D + 2u) return hipErrorInvalidValue;
+  const size_t nq = (size_t)e.x * e.y * e.z;
+  if (nq == 0) return hipSuccess;
+  size_t blocks = (nq + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(k_column4, dim3((uint32_t)blocks), dim3(256), 0, s, lin, W, H, D,
+                     reinterpret_cast<uint32_t*>(out), o, e);
   return hipGetLastError();
 }
 

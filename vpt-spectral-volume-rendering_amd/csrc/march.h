@@ -26,12 +26,19 @@
 
 namespace vpt {
 
-enum : uint32_t { kLayoutLinear = 0, kLayoutCorner8 = 1, kLayoutBrick8 = 2 };
-// Kernel template layouts: CORNER8 / BRICK8 with 32-bit byte offsets
+enum : uint32_t { kLayoutLinear = 0, kLayoutCorner8 = 1, kLayoutBrick8 = 2, kLayoutColumn4 = 3 };
+// Kernel template layouts: CORNER8 / BRICK8 / COLUMN4 with 32-bit byte offsets
 // (MarchParams::vol32) or with 64-bit ones (cell arrays over 4 GiB, e.g. 1024^3).
 enum : uint32_t {
-  kTplLinear = 0, kTplCorner8 = 1, kTplCorner8Wide = 2, kTplBrick8 = 3, kTplBrick8Wide = 4
+  kTplLinear = 0, kTplCorner8 = 1, kTplCorner8Wide = 2, kTplBrick8 = 3, kTplBrick8Wide = 4,
+  kTplColumn4 = 5, kTplColumn4Wide = 6
 };
+// COLUMN4: per (cx, cy) cell column the D + 2 quads q(k) = the 2x2 corner
+// voxels (clamped x cx-1 .. cx, y cy-1 .. cy) at z = clamp(k - 1), as u32 in
+// CORNER8's byte order (dy * 2 + dx), z fastest: the CORNER8 cell
+// (cx, cy, cz) is q(cz) | q(cz + 1) << 32, the 8 bytes at quad index cz of its
+// column — one 4-B-aligned 8-B load per sample from half CORNER8's footprint
+// (4 B per cell: 541 MB at 512^3, 4.3 GB at 1024^3).
 // BRICK8: the CORNER8 cells grouped into 4x4x4-cell bricks of 512 B (bricks in
 // raster order, x fastest); inside a brick the cell index interleaves the
 // coordinate bits as (x0 x1 y0 z0 y1 z1), so one 128-B line holds a 4x2x2 cell

@@ -119,6 +119,11 @@ struct vptmcm {
   uint32_t* done_dev = nullptr;        // its device address
   uint32_t done_total = 0, done_seq = 0;
   bool done_pending = false;           // the stream's last enqueued work is march done_seq
+  // With a communicator, every spectral march over the whole frame also writes
+  // (rgb * n, n) into comp[comp_next] (TileSched::pack, k_pack's values): when
+  // it is the stream's last work, vptmcm_comm_allreduce_radiance reduces that
+  // buffer without a k_pack launch.
+  bool pack_fresh = false;
   MarchLaunchInfo last_launch{};
 
   // multi-GPU
@@ -415,6 +420,8 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
     P.BH = (uint32_t)bh;
     if (h->layout == kLayoutBrick8)
       P.vol32 = (bw * bh * bd * 512ull < (1ull << 32) && bd * bh < (1ull << 24)) ? 1u : 0u;
+    else if (h->layout == kLayoutColumn4)  // u24 products: (H+1)(W+1) and D+2 below 2^24
+      P.vol32 = (w1 * h1 * (d1 + 1ull) * 4ull < (1ull << 32) && w1 * h1 < (1ull << 24)) ? 1u : 0u;
     else
       P.vol32 = (w1 * h1 * d1 * 8ull < (1ull << 32) && d1 * h1 < (1ull << 24) && w1 < (1ull << 24))
                     ? 1u : 0u;
@@ -424,6 +431,14 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
 }
 
 int check_handle(vptmcm* h) { return h ? VPTMCM_OK : VPTMCM_EINVAL; }
+
+// Work other than a march is enqueued on the handle's stream: the stream no
+// longer ends with a signalling march (vptmcm::done_pending) or with one that
+// packed the composite buffer (vptmcm::pack_fresh).
+void stream_op(vptmcm* h) {
+  h->done_pending = false;
+  h->pack_fresh = false;
+}
 
 // MarchParams::bins_lut (march MODE 6 / 7): the wavelength bin as a step
 // function of the draw h5. lambda_of(h5) = fma(f32(h5) * 2^-32, max - min,
@@ -525,7 +540,7 @@ int time_close(vptmcm* h) {
   }
   HIPCHK(h, hipEventRecord(h->region.end, h->stream));
   h->region_closed = true;
-  h->done_pending = false;  // work behind the signalling march
+  stream_op(h);  // work behind the signalling march
   return VPTMCM_OK;
 }
 
@@ -536,6 +551,14 @@ int flush_relayout(vptmcm* h) {
   h->vol_dirty = false;
   const bool brick = h->layout == kLayoutBrick8;
   const uint32_t n[3] = {h->vol_c1[0] - h->vol_c0[0], h->vol_c1[1] - h->vol_c0[1], h->vol_c1[2] - h->vol_c0[2]};
+  if (h->layout == kLayoutColumn4) {
+    // quad k holds voxel slice clamp(k - 1): the cells' z range [z0, z1) needs
+    // quads [z0, z1 + 1), clipped to the column's D + 2
+    const uint32_t z1 = std::min(h->vol_c1[2] + 1u, h->D + 2u);
+    const uint32_t nq[3] = {n[0], n[1], z1 - h->vol_c0[2]};
+    HIPCHK(h, launch_column4(h->vol_lin, h->W, h->H, h->D, h->vol_c8, h->stream, h->vol_c0, nq));
+    return VPTMCM_OK;
+  }
   HIPCHK(h, launch_corner8(h->vol_lin, h->W, h->H, h->D, brick ? (h->W + kBrickCells) / kBrickCells : 0u,
                            brick ? (h->H + kBrickCells) / kBrickCells : 0u, h->vol_c8, h->stream,
                            h->vol_c0, n));
@@ -560,10 +583,15 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   if (h->timing && h->time_stop) ee = h->region.end;
   const uint8_t* vol = h->layout != kLayoutLinear ? (const uint8_t*)h->vol_c8 : h->vol_lin;
   const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
-  TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev, nullptr, nullptr};
+  TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev, nullptr, nullptr, nullptr};
   const bool signal = h->done_on && h->kind == VPTMCM_RENDERER_SPECTRAL;
-  if (signal) {  // every wave of the grid counts once (kMarchBlock / 64 per block)
-    h->done_total += tile_blocks(P, kMarchBlock) * (kMarchBlock / 64u);
+  const bool pack = h->comm && h->kind == VPTMCM_RENDERER_SPECTRAL && h->band_y0 == 0 && h->band_y1 == h->R;
+  if (pack) {  // the buffer is free once the all-reduce issued two composites ago is done
+    HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[h->comp_next], 0));
+    T.pack = h->comp[h->comp_next];
+  }
+  if (signal) {  // every block of the grid counts once
+    h->done_total += tile_blocks(P, kMarchBlock);
     P.done_target = h->done_total;
     P.done_seq = ++h->done_seq;
     T.done_ctr = h->done_ctr;
@@ -582,6 +610,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   h->sched_cur = c ^ 1u;
   h->grp_dirty = true;
   h->done_pending = signal;
+  h->pack_fresh = pack;
   return VPTMCM_OK;
 }
 
@@ -794,7 +823,7 @@ static int group_alloc(vptmcm* h, const int32_t* devs, uint32_t n) {
   });
   if (rc) return rc;
   HIPCHK(h, hipSetDevice(h->device));
-  h->done_pending = false;
+  stream_op(h);
   const size_t slots = h->group_transport == VPTMCM_GROUP_RCCL ? 1 : n - 1;
   if (slots) HIPCHK(h, hipMalloc(&h->grp_gather, slots * npx * sizeof(float4)));
   HIPCHK(h, hipMalloc(&h->grp_rgb32, npx * 3 * sizeof(float)));
@@ -887,21 +916,26 @@ static int create_group(const vptmcm_config* cfg, vptmcm** out) {
 }
 
 // The composite of the current frame over every replica, enqueued on replica
-// 0's stream: each replica packs (rgb*n, n) on its own stream; PEER copies the
-// peers' packs to devices[0] in replica order (a peer copy over xGMI, or a
-// device copy for a repeated device) and k_composite sums them in that order;
-// RCCL reduces the packs to devices[0] (grouped ncclReduce) and k_composite
-// divides. Asynchronous.
+// 0's stream: each replica packs (rgb*n, n) on its own stream; PEER: each peer
+// then pushes its pack to its slot on devices[0] on its own stream (its own
+// xGMI link, all peers at once; a device copy for a repeated device) and
+// k_composite sums the slots in replica order; RCCL reduces the packs to
+// devices[0] (grouped ncclReduce) and k_composite divides. Asynchronous.
 static int group_composite(vptmcm* h) {
   const uint32_t n = 1u + (uint32_t)h->peers.size();
   const size_t npx = (size_t)h->R * h->R, bytes = npx * sizeof(float4);
+  const bool peer = h->group_transport == VPTMCM_GROUP_PEER;
   int rc = for_replicas(h, [&](vptmcm* c) {
     if (int r = flush_renders(c)) return r;
     HIPCHK(c, hipSetDevice(c->device));
-    c->done_pending = false;  // the pack follows the march on this stream
-    HIPCHK(c, hipStreamWaitEvent(c->stream, h->grp_done, 0));  // the last composite read the pack
+    stream_op(c);  // the pack follows the march on this stream
+    // the last composite has read this replica's pack (and its slot on devices[0])
+    HIPCHK(c, hipStreamWaitEvent(c->stream, h->grp_done, 0));
     const MarchParams P = make_params(c, kNoMatrix, 0);
     HIPCHK(c, launch_pack(P, c->photons, c->rgb32, c->grp_pack, c->stream));
+    if (peer && c != h)
+      HIPCHK(c, hipMemcpyPeerAsync(h->grp_gather + (size_t)(c->replica - 1) * npx, h->device, c->grp_pack,
+                                   c->device, bytes, c->stream));
     HIPCHK(c, hipEventRecord(c->grp_packed, c->stream));
     return VPTMCM_OK;
   });
@@ -926,12 +960,9 @@ static int group_composite(vptmcm* h) {
     HIPCHK(h, hipSetDevice(h->device));
     S.n = n;
     S.p[0] = h->grp_pack;
-    for (uint32_t k = 1; k < n; k++) {
-      vptmcm* c = h->peers[k - 1];
-      float4* dst = h->grp_gather + (size_t)(k - 1) * npx;
-      HIPCHK(h, hipStreamWaitEvent(h->stream, c->grp_packed, 0));
-      HIPCHK(h, hipMemcpyPeerAsync(dst, h->device, c->grp_pack, c->device, bytes, h->stream));
-      S.p[k] = dst;
+    for (uint32_t k = 1; k < n; k++) {  // every peer's push has landed
+      HIPCHK(h, hipStreamWaitEvent(h->stream, h->peers[k - 1]->grp_packed, 0));
+      S.p[k] = h->grp_gather + (size_t)(k - 1) * npx;
     }
   }
   HIPCHK(h, launch_composite(S, (uint32_t)npx, h->grp_rgb32, h->grp_rgba, nullptr, h->stream));
@@ -959,7 +990,7 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
     g_create_error = "vptmcm_create: unknown renderer kind";
     return VPTMCM_EINVAL;
   }
-  if (cfg->volume_layout > VPTMCM_LAYOUT_BRICK8) {
+  if (cfg->volume_layout > VPTMCM_LAYOUT_COLUMN4) {
     g_create_error = "vptmcm_create: unknown volume layout";
     return VPTMCM_EINVAL;
   }
@@ -1159,19 +1190,22 @@ static int volume_begin_one(vptmcm* h, uint32_t width, uint32_t height, uint32_t
   if (h->layout != kLayoutLinear) {
     // CORNER8: (W+1)(H+1)(D+1) cells in raster order; BRICK8: the same cells
     // in 4x4x4-cell bricks (the brick grid rounds each edge up to whole bricks)
-    const bool brick = h->layout == kLayoutBrick8;
+    const bool brick = h->layout == kLayoutBrick8, col = h->layout == kLayoutColumn4;
     const size_t bw = (width + kBrickCells) / kBrickCells, bh = (height + kBrickCells) / kBrickCells,
                  bd = (depth + kBrickCells) / kBrickCells;
-    const size_t ncell = brick ? bw * bh * bd * 64 : (size_t)(width + 1) * (height + 1) * (depth + 1);
-    // VPTMCM_VOL_ALLOC=contig (measurement knob): a physically contiguous
-    // allocation, for the TLB reach of the 8.6 GB cell array of a 1024^3 volume
-    const char* va = getenv("VPTMCM_VOL_ALLOC");
-    const bool contig = va && strcmp(va, "contig") == 0;
-    if ((contig ? hipExtMallocWithFlags(&h->vol_c8, ncell * 8, hipDeviceMallocContiguous)
-                : hipMalloc(&h->vol_c8, ncell * 8)) != hipSuccess) {
+    // COLUMN4: (W+1)(H+1)(D+2) quads of 4 B = half as many 8-B units
+    const size_t ncell = brick ? bw * bh * bd * 64
+                         : col ? ((size_t)(width + 1) * (height + 1) * (depth + 2) + 1) / 2
+                               : (size_t)(width + 1) * (height + 1) * (depth + 1);
+    // (Round 3's VPTMCM_VOL_ALLOC=contig knob, hipExtMallocWithFlags(...,
+    // hipDeviceMallocContiguous), bought nothing and is gone: in round 5 the
+    // knob test found that once such an allocation had been freed, later
+    // handles in the process rendered wrong bits)
+    if (hipMalloc(&h->vol_c8, ncell * 8) != hipSuccess) {
       h->vol_c8 = nullptr;
       free_volume(h);
-      FAIL(h, VPTMCM_ENOMEM, "%s volume allocation of %zu bytes failed", brick ? "brick8" : "corner8",
+      FAIL(h, VPTMCM_ENOMEM, "%s volume allocation of %zu bytes failed",
+           brick ? "brick8" : col ? "column4" : "corner8",
            ncell * 8);
     }
     HIPCHK(h, hipMemsetAsync(h->vol_c8, 0, ncell * 8, h->stream));
@@ -1384,7 +1418,7 @@ static int set_band_one(vptmcm* h, uint32_t y0, uint32_t y1) {
   HIPCHK(h, hipSetDevice(h->device));
   h->band_y0 = y0;
   h->band_y1 = y1;
-  h->done_pending = false;
+  stream_op(h);
   const size_t row = (size_t)h->R * 3 * sizeof(float);
   if (y0 > 0) HIPCHK(h, hipMemsetAsync(h->rgb32, 0, y0 * row, h->stream));
   if (y1 < h->R)
@@ -1413,7 +1447,7 @@ static int reset_one(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   if (!mvp) FAIL(h, VPTMCM_EINVAL, "reset: null matrix");
   HIPCHK(h, hipSetDevice(h->device));
   MarchParams P = make_params(h, mvp, seed_bits);
-  h->done_pending = false;
+  stream_op(h);
   if (h->kind == VPTMCM_RENDERER_RGB)
     HIPCHK(h, launch_reset_rgb(P, h->photons, h->stream));
   else
@@ -1537,7 +1571,7 @@ int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out
   T.saturation = params[3];
   const float midpoint = (mid - low) / range;
   T.exponent = (float)(-std::log((double)midpoint) / std::log(2.0)) / params[4];
-  h->done_pending = false;
+  stream_op(h);
   HIPCHK(h, launch_tonemap_artistic(composited(h) ? h->grp_rgba : h->rgba, (uint32_t)npx, T, h->ldr,
                                     h->stream));
   if (rgba8_out) {
@@ -1650,7 +1684,7 @@ static int enable_kernel_timing_one(vptmcm* h, int enable) {
   return VPTMCM_OK;
 }
 
-int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
+static int kernel_time_one(vptmcm* h, double* total_ms, uint64_t* launches) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!total_ms || !launches) FAIL(h, VPTMCM_EINVAL, "kernel_time: null output");
@@ -1662,6 +1696,27 @@ int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
   if (h->timing && h->launches) HIPCHK(h, hipEventElapsedTime(&ms, h->region.beg, h->region.end));
   *total_ms = ms;
   *launches = h->timing ? h->launches : 0;
+  return VPTMCM_OK;
+}
+
+// A device-list handle: the longest replica's region (its launches counted
+// once: every replica runs the same launches).
+int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (!total_ms || !launches) FAIL(h, VPTMCM_EINVAL, "kernel_time: null output");
+  double mx = 0.0;
+  uint64_t n0 = 0;
+  int rc = for_replicas(h, [&](vptmcm* c) {
+    double ms = 0.0;
+    uint64_t n = 0;
+    if (int r = kernel_time_one(c, &ms, &n)) return r;
+    if (c == h) n0 = n;
+    mx = ms > mx ? ms : mx;
+    return VPTMCM_OK;
+  });
+  if (rc) return rc;
+  *total_ms = mx;
+  *launches = n0;
   return VPTMCM_OK;
 }
 
@@ -1702,13 +1757,49 @@ int vptmcm_comm_init(vptmcm* h, const uint8_t* uid, int nranks, int rank) {
   // thread sleep-polls inside the call while the init job spins on the
   // bootstrap sockets and the root thread waits in accept()
   // (tools/comm_diag.cpp, profiles/r04/s1/comm_diag_nb.log), and no
-  // communicator handle exists to abort until the call returns. Peer liveness
-  // is therefore established before this call (rendezvous.join: every rank
-  // present, bounded by VPTMCM_COMM_TIMEOUT_MS, ECOMM otherwise), and the call
-  // runs in the caller's thread: no helper thread is left behind.
-  comm_trace("comm_init: ncclCommInitRank nranks=%d rank=%d", nranks, rank);
-  ncclComm_t c = nullptr;
-  const ncclResult_t r = ncclCommInitRank(&c, nranks, id, rank);
+  // communicator handle exists to abort until the call returns (aborting one
+  // still in bootstrap hung in round 3). Peer liveness is therefore
+  // established before this call (rendezvous.join: every rank present,
+  // bounded by VPTMCM_COMM_TIMEOUT_MS, ECOMM otherwise). The residual window —
+  // a peer that joined and then died before its init — is bounded here: the
+  // initialisation runs on a helper thread and the caller waits for it at most
+  // VPTMCM_COMM_TIMEOUT_MS. On success the thread is joined. On expiry the
+  // call returns ECOMM and the thread, blocked inside RCCL, cannot be
+  // reclaimed: it is detached (should the initialisation ever return, it
+  // aborts the unused communicator) and the caller must end the process
+  // without running exit handlers (_exit), as bench.py does.
+  struct InitJob {
+    std::atomic<int> state{0};  // 0 running, 1 returned, 2 abandoned by the caller
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = ncclSuccess;
+  };
+  auto job = std::make_shared<InitJob>();
+  comm_trace("comm_init: ncclCommInitRank nranks=%d rank=%d (helper thread)", nranks, rank);
+  const int dev = h->device;
+  std::thread th([job, id, nranks, rank, dev]() {
+    ncclComm_t c = nullptr;
+    (void)hipSetDevice(dev);
+    const ncclResult_t r = ncclCommInitRank(&c, nranks, id, rank);
+    job->comm = c;
+    job->r = r;
+    int running = 0;
+    if (!job->state.compare_exchange_strong(running, 1) && c) (void)ncclCommAbort(c);  // abandoned
+  });
+  const int64_t t0 = now_ms();
+  while (job->state.load() == 0 && now_ms() - t0 <= h->comm_timeout_ms)
+    std::this_thread::sleep_for(std::chrono::microseconds(500));
+  int running = 0;
+  if (job->state.compare_exchange_strong(running, 2)) {  // still inside RCCL: give it up
+    th.detach();
+    comm_trace("comm_init: no return after %lld ms; helper thread detached", (long long)h->comm_timeout_ms);
+    FAIL(h, VPTMCM_ECOMM,
+         "ncclCommInitRank (rank %d of %d) did not return within %lld ms (a peer died after the "
+         "rendezvous?); its thread is blocked inside RCCL and cannot be reclaimed: end the process "
+         "(_exit)", rank, nranks, (long long)h->comm_timeout_ms);
+  }
+  th.join();
+  const ncclResult_t r = job->r;
+  ncclComm_t c = job->comm;
   comm_trace("comm_init: ncclCommInitRank returned %d", (int)r);
   if (r != ncclSuccess) {
     if (c) (void)ncclCommAbort(c);
@@ -1737,11 +1828,14 @@ int vptmcm_comm_allreduce_radiance(vptmcm* h) {
   if (!h->comm) FAIL(h, VPTMCM_ECOMM, "comm_allreduce_radiance: no communicator");
   HIPCHK(h, hipSetDevice(h->device));
   int k = h->comp_next;
-  h->done_pending = false;
-  // the buffer must be free of the all-reduce issued two passes ago
-  HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[k], 0));
-  MarchParams P = make_params(h, kNoMatrix, 0);
-  HIPCHK(h, launch_pack(P, h->photons, h->rgb32, h->comp[k], h->stream));
+  if (!h->pack_fresh) {  // the stream does not end with a march that packed comp[k]
+    stream_op(h);
+    // the buffer must be free of the all-reduce issued two passes ago
+    HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[k], 0));
+    MarchParams P = make_params(h, kNoMatrix, 0);
+    HIPCHK(h, launch_pack(P, h->photons, h->rgb32, h->comp[k], h->stream));
+  }
+  stream_op(h);
   HIPCHK(h, hipEventRecord(h->comp_ready[k], h->stream));
   HIPCHK(h, hipStreamWaitEvent(h->comm_stream, h->comp_ready[k], 0));
   if (int rc = comm_call(h, ncclAllReduce(h->comp[k], h->comp[k], (size_t)h->R * h->R * 4,
@@ -1849,7 +1943,7 @@ int vptmcm_comm_gather_bands(vptmcm* h, float* rgb) {
   // a -0.0 pixel (-0 + +0 = +0).
   const size_t n = (size_t)h->R * h->R * 3;
   float* sum = reinterpret_cast<float*>(h->comp[h->comp_next]);  // R*R float4 >= R*R*3 floats
-  h->done_pending = false;
+  stream_op(h);
   HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[h->comp_next], 0));
   HIPCHK(h, hipMemcpyAsync(sum, h->rgb32, n * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(h, hipEventRecord(h->comp_ready[h->comp_next], h->stream));

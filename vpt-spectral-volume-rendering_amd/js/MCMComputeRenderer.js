@@ -16,7 +16,7 @@ const { PropertyBag } = require('./PropertyBag');
 const { mvpInverse } = require('./Camera');
 const { native, f32bits } = require('./MCMSpectralComputeRenderer');
 
-const LAYOUTS = { linear: 0, corner8: 1, brick8: 2 };
+const LAYOUTS = { linear: 0, corner8: 1, brick8: 2, column4: 3 };
 const RENDERER_RGB = 1;
 const RESET_ON = ['extinction', 'anisotropy', 'bounces', 'transferFunction'];  // js:70-75
 

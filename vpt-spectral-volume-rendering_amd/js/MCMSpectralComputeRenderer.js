@@ -36,7 +36,7 @@ function native() {
   return addon;
 }
 
-const LAYOUTS = { linear: 0, corner8: 1, brick8: 2 };
+const LAYOUTS = { linear: 0, corner8: 1, brick8: 2, column4: 3 };
 const TRANSPORTS = { peer: 0, rccl: 1 };  // vptmcm_config::group_transport
 const RESET_ON = ['extinction', 'anisotropy', 'bounces', 'materialTransferFunction',
   'spectrumRepresentation', 'lightEditor'];  // js:116-125

@@ -16,7 +16,7 @@ PKG = Path(__file__).resolve().parents[2]
 LIB_DIR = PKG / "lib"
 
 OK, EINVAL, EHIP, ESTATE, ENOMEM, ECOMM = 0, -1, -2, -3, -4, -5
-LAYOUT_LINEAR, LAYOUT_CORNER8, LAYOUT_BRICK8 = 0, 1, 2
+LAYOUT_LINEAR, LAYOUT_CORNER8, LAYOUT_BRICK8, LAYOUT_COLUMN4 = 0, 1, 2, 3
 RENDERER_SPECTRAL, RENDERER_RGB = 0, 1
 PHOTON_RGB_BYTES = 64
 PHOTON_BYTES = 144

@@ -12,6 +12,7 @@ Single node only, which is all the benchmark uses.
 """
 from __future__ import annotations
 
+import atexit
 import os
 import tempfile
 import time
@@ -108,26 +109,65 @@ def default_timeout_s() -> float:
     return (ms if ms > 0 else 120000) / 1e3
 
 
+def _proc_start(pid: int) -> str | None:
+    """The process's start time in clock ticks since boot (/proc/<pid>/stat
+    field 22), or None if no such process: with the pid it names one process
+    for the boot's lifetime, whatever pids the kernel reuses."""
+    try:
+        stat = Path(f"/proc/{pid}/stat").read_text()
+    except OSError:
+        return None
+    return stat[stat.rindex(")") + 2:].split()[19]
+
+
+def _marker(key: str) -> bytes:
+    pid = os.getpid()
+    return f"{key}\n{pid}\n{_proc_start(pid)}".encode()
+
+
+def marker_alive(path: Path, key: str) -> bool:
+    """A join marker of this job key whose writer is still running (same pid
+    and start time): a marker left by a rank that timed out or crashed, or by
+    an earlier job with the same key, does not count as a live peer."""
+    try:
+        k, pid, start = path.read_text().split("\n")
+    except (OSError, ValueError):
+        return False
+    return k == key and pid.isdigit() and start != "None" and _proc_start(int(pid)) == start
+
+
+def _unlink(p: Path) -> None:
+    try:
+        p.unlink()
+    except FileNotFoundError:
+        pass
+
+
 def join(rank: int, world: int, key: str | None = None, timeout_s: float | None = None) -> None:
     """All-ranks-present barrier ahead of RCCL: every rank publishes a join
-    marker, then waits until all `world` markers of this job key exist. RCCL's
-    bootstrap is entered only once every peer is known to be alive (a
-    communicator whose peer never arrives blocks inside RCCL's bootstrap, and
-    its abort can block too). A rank that does not arrive within
-    the bound ends every other rank here with RendezvousError (ECOMM)."""
+    marker (job key, pid, process start time), then waits until all `world`
+    markers of this job key name running processes. RCCL's bootstrap is entered
+    only once every peer is known to be alive (a communicator whose peer never
+    arrives blocks inside RCCL's bootstrap, and its abort can block too;
+    DESIGN.md §6). A rank that does not arrive within the bound ends every
+    other rank here with RendezvousError (ECOMM). A rank removes its own marker
+    when it fails here and when its process exits, so a stale marker never
+    stands in for a live peer of a later job with the same key."""
     key = key or job_key()
     timeout_s = default_timeout_s() if timeout_s is None else timeout_s
     mine = join_path(key, rank)
     tmp = mine.with_name(mine.name + f".{os.getpid()}.tmp")
-    tmp.write_bytes(key.encode())
+    tmp.write_bytes(_marker(key))
     os.replace(tmp, mine)
+    atexit.register(_unlink, mine)
     deadline = time.monotonic() + timeout_s
     missing = list(range(world))
     while True:
-        missing = [r for r in missing if not join_path(key, r).exists()]
+        missing = [r for r in missing if not marker_alive(join_path(key, r), key)]
         if not missing:
             return
         if time.monotonic() >= deadline:
+            _unlink(mine)
             raise RendezvousError(f"rendezvous: rank {rank} of {world}: rank(s) {missing} never joined "
                                   f"within {timeout_s:g} s (job key {key}); no communicator was created")
         time.sleep(0.01)
@@ -138,7 +178,4 @@ def cleanup(key: str | None = None, world: int = 0) -> None:
     rank has passed the communicator's first barrier)."""
     key = key or job_key()
     for p in [uid_path(key)] + [join_path(key, r) for r in range(world)]:
-        try:
-            p.unlink()
-        except FileNotFoundError:
-            pass
+        _unlink(p)
