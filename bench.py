@@ -62,7 +62,7 @@ def parse():
     ap.add_argument("--volume", type=int, default=512)
     ap.add_argument("--photon-steps", type=int, default=8, help="S: steps per pass")
     ap.add_argument("--extinction", type=float, default=32.0)
-    ap.add_argument("--layout", choices=["corner8", "brick8", "column4", "linear"], default="corner8")
+    ap.add_argument("--layout", choices=["corner8", "brick8", "column4", "linear"], default="column4")
     ap.add_argument("--tf", choices=["spectral", "grey", "zero", "materials", "materials_const"],
                     default="spectral", help="TF (non-spectral: analysis only)")
     ap.add_argument("--bins", default="12", help="spectrum bin layout (non-12: analysis only)")

@@ -159,7 +159,7 @@ test('addon loads; renderer construction fails loudly without a GPU', () => {
 });
 
 test('createDevice: an ordinal or a device list', () => {
-  assert.deepStrictEqual(V.createDevice(3), { ordinal: 3, layout: 'corner8' });
+  assert.deepStrictEqual(V.createDevice(3), { ordinal: 3, layout: 'column4' });
   assert.deepStrictEqual(V.createDevice([0, 1, 2], 'brick8'), { devices: [0, 1, 2], layout: 'brick8', transport: 'peer' });
   assert.deepStrictEqual(V.createDevice([4, 5], 'corner8', 'rccl').transport, 'rccl');
 });

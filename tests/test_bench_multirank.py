@@ -127,7 +127,7 @@ def test_bench_two_ranks_driver_command_line(tmp_path, world):
     uids = {e[1] for lg in logs for e in lg if e[0] == "comm_init"}
     assert len(uids) == 1, "ranks must share rank 0's unique id"
     for r, lg in enumerate(logs):
-        assert ["create", 16, r, 1] in lg  # one GPU per local rank
+        assert ["create", 16, r, 3] in lg  # one GPU per local rank (COLUMN4, the default layout)
         t = [e[0] for e in lg].index("timing")
         after = lg[t + 1:]
         c1 = [e[0] for e in after].index("composite")
@@ -254,7 +254,7 @@ def test_bench_gpus4_without_launcher_is_one_device_list_handle(tmp_path, transp
     assert rec["cpu_baseline"] is None and rec["unfused"] is None
     log = json.loads((tmp_path / "log.json").read_text())
     creates = [e for e in log if e[0].startswith("create")]
-    assert creates == [["create_group", 16, [0, 1, 2, 3], 0 if transport == "peer" else 1, 1]]
+    assert creates == [["create_group", 16, [0, 1, 2, 3], 0 if transport == "peer" else 1, 3]]
     assert not [e for e in log if e[0] in ("comm_init", "allreduce")]
     t = [e[0] for e in log].index("timing")
     after = [e[0] for e in log[t + 1:]]

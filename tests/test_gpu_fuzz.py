@@ -1,6 +1,6 @@
 """Randomised GPU parity: seeded random configurations of every input the march
 reads — resolution (incl. R not a multiple of 8), ragged volume shapes, all
-three layouts, random / few-row / many-row TFs with constant or varying
+four layouts, random / few-row / many-row TFs with constant or varying
 anisotropy, random bin layouts (uneven, duplicate and unsorted boundaries,
 random CMF coefficients), random light SPD and direction (incl. isotropic),
 extinction over three decades plus 0 and 1e4, bounces, steps, depth of field and random camera
@@ -95,7 +95,8 @@ def _draw(k):
     rng = np.random.default_rng(1000 + k)
     R = int(rng.choice([8, 16, 24, 40, 48, 64, 72, 96, 128, 200, 256])) + (int(rng.integers(1, 8)) if rng.random() < 0.3 else 0)
     shape = tuple(int(x) for x in rng.integers(1, 72, 3)) if rng.random() < 0.4 else (48, 48, 48)
-    layout = int(rng.choice([vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_LINEAR, vptmcm.LAYOUT_BRICK8]))
+    layout = int(rng.choice([vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_LINEAR, vptmcm.LAYOUT_BRICK8,
+                             vptmcm.LAYOUT_COLUMN4]))
     spec_what, spec = _spectrum(rng)
     tf_what, tf = _tf(rng)
     iso = rng.random() < 0.2
@@ -289,7 +290,8 @@ _MODE_INPUTS = {
 # layout template -> (layout, force 64-bit offsets: VPTMCM_MARCH_VARIANT=8)
 _TEMPLATES = {0: (vptmcm.LAYOUT_LINEAR, False), 1: (vptmcm.LAYOUT_CORNER8, False),
               2: (vptmcm.LAYOUT_CORNER8, True), 3: (vptmcm.LAYOUT_BRICK8, False),
-              4: (vptmcm.LAYOUT_BRICK8, True)}
+              4: (vptmcm.LAYOUT_BRICK8, True), 5: (vptmcm.LAYOUT_COLUMN4, False),
+              6: (vptmcm.LAYOUT_COLUMN4, True)}
 
 
 def test_mode_template_coverage(monkeypatch):
@@ -342,5 +344,5 @@ def test_mode_template_coverage(monkeypatch):
                 assert_rgba_equal(gpu.read_rgba16f(), want, what + " fused")
                 assert_rgb32_equal(gpu.read_rgb(), rgb, what + " fused")
             HIT.add((mode, tpl))
-    print(f"forced {len(forced)} of 40 pairs: {forced}")
-    assert len(HIT) == 40
+    print(f"forced {len(forced)} of {8 * len(_TEMPLATES)} pairs: {forced}")
+    assert len(HIT) == 8 * len(_TEMPLATES)

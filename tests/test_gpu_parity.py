@@ -931,7 +931,8 @@ def test_brick8_ragged_volume_bitexact(shape):
     gpu.close()
 
 
-def test_c5_1024_volume_streamed_rows_against_oracle():
+@pytest.mark.parametrize("layout,tpl", [(vptmcm.LAYOUT_CORNER8, 2), (vptmcm.LAYOUT_COLUMN4, 6)])
+def test_c5_1024_volume_streamed_rows_against_oracle(layout, tpl):
     """C5 on one GPU: the 1024^3 fBm volume (seed 1024) streamed into HBM in
     64-slice blocks (WebGPUVolume.readModality's per-placement upload), CORNER8
     cells > 4 GiB (the 64-bit gather template); R = 512, two fused passes; a
@@ -939,7 +940,7 @@ def test_c5_1024_volume_streamed_rows_against_oracle():
     row-restricted run, and the whole frame satisfies the running-mean bounds."""
     n, R = 1024, 512
     vol = cf.fbm_volume(n, 1024)
-    gpu = vptmcm.Renderer(R, device=0)
+    gpu = vptmcm.Renderer(R, device=0, layout=layout)
     gpu.volume_blocks(vol.shape, (((0, 0, z), vol[z:z + 64]) for z in range(0, n, 64)))
     cpu = orc.Oracle(R)
     spec, tf = cf.spectrum_buffer("12"), cf.tf_spectral()
@@ -956,6 +957,7 @@ def test_c5_1024_volume_streamed_rows_against_oracle():
     gpu.reset(mvp, seeds[0])
     cpu.reset(mvp, seeds[0], nthreads=16)
     gpu.render_passes(mvp, seeds[1:])
+    assert gpu.last_launch()["tpl"] == tpl  # cells over 4 GiB: the 64-bit gather
     rows = (224, 264)
     for s in seeds[1:]:
         rgb, want = cpu.render(mvp, s, nthreads=16, rows=rows)
@@ -977,27 +979,29 @@ def test_c5_1024_volume_streamed_rows_against_oracle():
     gpu.close()
 
 
+@pytest.mark.parametrize("layout,tpl", [(vptmcm.LAYOUT_COLUMN4, 5), (vptmcm.LAYOUT_CORNER8, 1)])
 @pytest.mark.parametrize("dark", ["0", "1"])
-def test_c3_driver_shaped_launch_bitexact(dark, monkeypatch):
+def test_c3_driver_shaped_launch_bitexact(dark, layout, tpl, monkeypatch):
     """The benchmarked launch shape itself: BASELINE C3
     (512^3 fBm seed 512, spectral TF, R = 512, S = 8, 12 bins, extinction 32,
     default camera) from a reset, the driver's 5 warm-up passes as one launch,
     then its timed `--steps 20` region as ONE 20-pass fused launch (the FAST
-    MODE 2 kernel on CORNER8), with the bench's own seed stream: photons, the
+    MODE 2 kernel on COLUMN4, the bench's default layout, and on CORNER8), with the
+    bench's own seed stream: photons, the
     fp32 image and the rgba16f image bit-exact against the oracle, with the
     dark-background chain (the default: background waves the light never
     reaches run the draw chain alone) and without it (VPTMCM_DARK=0)."""
     monkeypatch.setenv("VPTMCM_DARK", dark)
     R, S = 512, 8
     vol, tf, mvp = cf.fbm_volume(512, 512, nthreads=8), cf.tf_spectral(), cf.default_mvp_inverse()
-    gpu, cpu = make_pair(R, vol, tf, ext=32.0, steps=S)
+    gpu, cpu = make_pair(R, vol, tf, ext=32.0, steps=S, layout=layout)
     seeds = cf.seed_stream(1 + 5 + 20, start=0, rank=0)  # bench.py's stream at N = 1
     gpu.reset(mvp, seeds[0])
     cpu.reset(mvp, seeds[0], nthreads=16)
     gpu.render_passes(mvp, seeds[1:6])
     gpu.render_passes(mvp, seeds[6:26])
     info = gpu.last_launch()
-    assert (info["passes"], info["mode"], info["tpl"], info["spec"]) == (20, 2, 1, True), info
+    assert (info["passes"], info["mode"], info["tpl"], info["spec"]) == (20, 2, tpl, True), info
     for s in seeds[1:]:
         rgb, want = cpu.render(mvp, s, nthreads=16)
     assert_photons_equal(gpu.read_photons(), cpu.photons, "C3 20-pass launch")
@@ -1020,7 +1024,7 @@ def test_c3_bench_settled_state_driver_launch_rows_bitexact():
     whole frame's sample counts are those of the settled state."""
     R, S = 512, 8
     vol, tf, mvp = cf.fbm_volume(512, 512, nthreads=8), cf.tf_spectral(), cf.default_mvp_inverse()
-    gpu, cpu = make_pair(R, vol, tf, ext=32.0, steps=S)
+    gpu, cpu = make_pair(R, vol, tf, ext=32.0, steps=S, layout=vptmcm.LAYOUT_COLUMN4)  # the bench's layout
     seeds = cf.seed_stream(1 + 5 + 20, start=0, rank=0)  # bench.py's stream at N = 1
     sseeds = cf.seed_stream(32, start=1 << 20, rank=0)    # bench.py's clock-settling seeds
     gpu.reset(mvp, seeds[0])
@@ -1030,7 +1034,7 @@ def test_c3_bench_settled_state_driver_launch_rows_bitexact():
     gpu.render_passes(mvp, seeds[1:6])
     gpu.render_passes(mvp, seeds[6:26])
     info = gpu.last_launch()
-    assert (info["passes"], info["mode"], info["tpl"], info["spec"]) == (20, 2, 1, True), info
+    assert (info["passes"], info["mode"], info["tpl"], info["spec"]) == (20, 2, 5, True), info
     rows = (248, 264)
     for _ in range(320):
         for s in sseeds:

@@ -35,7 +35,8 @@ def same_words(a, b):
     return (a == b) | (np.isnan(fa) & np.isnan(fb))
 
 
-@pytest.mark.parametrize("layout", [vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_LINEAR, vptmcm.LAYOUT_BRICK8])
+@pytest.mark.parametrize("layout", [vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_LINEAR, vptmcm.LAYOUT_BRICK8,
+                                    vptmcm.LAYOUT_COLUMN4])
 @pytest.mark.parametrize("tfk,aniso,ext,env", [("default", 0.0, 1.0, (255, 255, 255, 255)),
                                                ("ramp", 0.6, 24.0, (255, 255, 255, 255)),
                                                ("odd", -0.4, 8.0, (200, 150, 90, 255)),

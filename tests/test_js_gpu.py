@@ -88,7 +88,8 @@ def test_js_render_calls_fuse(tmp_path, render_passes):
 
 
 @pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
-@pytest.mark.parametrize("layout,stream", [("corner8", True), ("linear", False), ("brick8", True)])
+@pytest.mark.parametrize("layout,stream", [("corner8", True), ("linear", False), ("brick8", True),
+                                           ("column4", True), ("column4", False)])
 def test_js_renderer_bitexact(tmp_path, layout, stream):
     vol, tf = cf.sphere_in_cube(64), cf.tf_spectral()
     ph, rgba, seeds, used = run_case(tmp_path, vol, tf, layout=layout, stream=stream)

@@ -77,6 +77,14 @@ for s in $STEPS; do
   diag)  # a diagnostic script: DIAG=tools/<script>.py
     timeout -k 10 300 python ${DIAG} > $OUT/diag.jsonl 2> $OUT/diag.err
     rc=$?; echo "diag rc=$rc" | tee -a $OUT/status.txt; cat $OUT/diag.jsonl; fault $rc && exit $rc ;;
+  commab)  # the one-rank RCCL composite path (VPTMCM_BENCH_FORCE_COMM=1), round-4 library vs the current one
+    for lib in ${COMM_LIBS:-r04 cur r04 cur r04 cur}; do
+      if [ $lib = cur ]; then unset VPTMCM_LIB; else export VPTMCM_LIB=$lib; fi
+      VPTMCM_BENCH_FORCE_COMM=1 timeout -k 10 300 python bench.py --steps 64 --warmup 64 --cpu-seconds 0 --per-pass-steps 128 > $OUT/comm_$lib.json 2>> $OUT/commab.err
+      rc=$?; unset VPTMCM_LIB; [ $rc -ne 0 ] && { echo "commab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      python3 -c "import json; d=json.load(open('$OUT/comm_$lib.json')); p=d['per_pass_allreduce']; print(json.dumps({'lib': '$lib', 'value': d['value'], 'ms_per_step': d['ms_per_step'], 'per_pass_us': round(p['ms_per_step']*1e3, 2), 'per_pass_value': p['value']}))" >> $OUT/commab.jsonl
+    done
+    echo "commab rc=0" | tee -a $OUT/status.txt; cat $OUT/commab.jsonl ;;
   flagab)  # the driver's command, alternating the completion signal off (VPTMCM_DONE_FLAG=0) and on
     for f in ${FLAG_CASES:-0 1 0 1 0 1 0 1 0 1}; do
       VPTMCM_DONE_FLAG=$f timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 > $OUT/flag_$f.json 2>> $OUT/flagab.err

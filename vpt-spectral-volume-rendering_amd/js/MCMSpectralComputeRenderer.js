@@ -94,7 +94,7 @@ class MCMSpectralComputeRenderer extends PropertyBag {
   }
 
   _createNative() {
-    const layout = LAYOUTS[this._device.layout || 'corner8'];
+    const layout = LAYOUTS[this._device.layout || 'column4'];
     if (layout === undefined) throw new Error(`unknown volume layout '${this._device.layout}'`);
     const ordinal = this._device.ordinal !== undefined ? this._device.ordinal : -1;
     const devs = this._device.devices;

@@ -15,7 +15,7 @@ const mat4 = require('./mat4');
 // or a list of ordinals for one renderer driving several GPUs (a
 // photon-parallel replica per GPU, composited on the first; transport 'peer'
 // or 'rccl', include/vptmcm.h).
-function createDevice(ordinal = 0, layout = 'corner8', transport = 'peer') {
+function createDevice(ordinal = 0, layout = 'column4', transport = 'peer') {
   if (Array.isArray(ordinal)) return { devices: ordinal.slice(), layout, transport };
   return { ordinal, layout };
 }
