@@ -692,58 +692,36 @@ def _expected_schedule(table: np.ndarray, n_tiles: int, xcd_by_xcd: bool = False
     tiles, background tiles], each class ascending; slot q = k*4G + lb*4 + j
     goes to wave 4j + ((k + j) & 3) of hardware block lb (consecutive blocks
     rotate over the XCDs), or of block unswizzle(lb) with round 2's XCD-by-XCD
-    order (variant bit 7). The volume class is taken from the table's own bit 31.
-    Dark-first deal (one chunk, SIMD pairs, some background tile dark last
-    launch: bit 29): the background tiles [dark ascending, then the others]
-    fill [the slots beside pairs (group 2-3, positions < pairs)] then [the
-    other CUs' background slots (group 1-3, positions >= pairs)]."""
+    order (variant bit 7). The volume class is taken from the table's own bit 31."""
     G = table.size // 16
     used = table != 0xFFFFFFFF
     words = table[used]
     tiles = words & 0x1FFFFFFF
     vol = np.zeros(n_tiles, bool)
     vol[tiles[(words >> 31) == 1]] = True
-    dark = np.zeros(n_tiles, bool)
-    dark[tiles[((words >> 29) & 1) == 1]] = True
     nv = int(vol.sum())
-    pairs = max(nv - 4 * G, 0)
-    lone = 4 * G - pairs if pairs < 4 * G else 0
     slots = {}
     for q, t in enumerate(np.flatnonzero(vol)):
         slots[int(t)] = q
-    bg = np.flatnonzero(~vol)
-    if n_tiles <= 4096 and pairs > 0 and lone > 0 and dark.any():
-        for r, t in enumerate(np.concatenate([bg[dark[bg]], bg[~dark[bg]]])):
-            if r < 2 * pairs:
-                g = r // pairs
-                slots[int(t)] = (2 + g) * 4 * G + (r - g * pairs)
-            else:
-                r2 = r - 2 * pairs
-                g = r2 // lone
-                slots[int(t)] = (1 + g) * 4 * G + pairs + (r2 - g * lone)
-    else:
-        for r, t in enumerate(bg):
-            slots[int(t)] = nv + r
+    for r, t in enumerate(np.flatnonzero(~vol)):
+        slots[int(t)] = nv + r
     exp = np.full(table.size, 0xFFFFFFFF, np.uint32)
     for t, q in slots.items():
         k, rem = divmod(q, 4 * G)
         lb, j = divmod(rem, 4)
         b = _xcd_unswizzle(lb, G) if xcd_by_xcd else lb
-        exp[b * 16 + 4 * j + ((k + j) & 3)] = t | (int(vol[t]) << 31) | (int(dark[t]) << 29)
+        exp[b * 16 + 4 * j + ((k + j) & 3)] = t | (int(vol[t]) << 31)
     return exp
 
 
-@pytest.mark.parametrize("R,variant,dark", [(256, "0", "1"), (512, "0", "1"), (512, "128", "1"), (1024, "0", "1"),
-                                            (256, "0", "2"), (512, "0", "2")])
-def test_tile_schedule_is_the_latin_square_deal(R, variant, dark, monkeypatch):
+@pytest.mark.parametrize("R,variant", [(256, "0"), (512, "0"), (512, "128"), (1024, "0")])
+def test_tile_schedule_is_the_latin_square_deal(R, variant, monkeypatch):
     """N2, checked directly: after each launch every tile ran on exactly one
     wave slot, volume tiles first, dealt over the slots exactly as
     schedule_tile's ballot / prefix scan intends (vptmcm_debug_schedule), in
     the XCD round-robin slot order and in round 2's XCD-by-XCD one (variant
-    bit 7); a camera change re-deals it. dark = 2 (VPTMCM_DARK): the
-    dark-first deal of the background tiles."""
+    bit 7); a camera change re-deals it."""
     monkeypatch.setenv("VPTMCM_MARCH_VARIANT", variant)
-    monkeypatch.setenv("VPTMCM_DARK", dark)
     gpu = vptmcm.Renderer(R, device=0)
     assert (gpu.debug_schedule() == 0xFFFFFFFF).all()  # fresh handle: no launch yet
     gpu.set_volume(cf.fbm_volume(128, 77))

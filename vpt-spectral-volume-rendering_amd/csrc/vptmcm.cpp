@@ -834,17 +834,26 @@ static int group_alloc(vptmcm* h, const int32_t* devs, uint32_t n) {
   HIPCHK(h, hipEventRecord(h->grp_done, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->group_transport == VPTMCM_GROUP_PEER) {
+    // both directions between devices[0] and each peer: the peer's stream
+    // pushes its pack into devices[0]'s memory (peer -> devices[0]), and
+    // devices[0] reads nothing of the peers' but keeps the historical access
+    auto enable = [&](int from, int to) -> int {
+      int can = 0;
+      HIPCHK(h, hipDeviceCanAccessPeer(&can, from, to));
+      if (!can) return VPTMCM_OK;  // hipMemcpyPeerAsync then stages through the host
+      HIPCHK(h, hipSetDevice(from));
+      const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+        FAIL(h, VPTMCM_EHIP, "hipDeviceEnablePeerAccess(%d -> %d): %s", from, to, hipGetErrorString(e));
+      (void)hipGetLastError();  // clear an already-enabled status
+      return VPTMCM_OK;
+    };
     for (uint32_t k = 1; k < n; k++) {
       if (devs[k] == h->device) continue;
-      int can = 0;
-      HIPCHK(h, hipDeviceCanAccessPeer(&can, h->device, devs[k]));
-      if (!can) continue;  // hipMemcpyPeerAsync then stages through the host
-      const hipError_t e = hipDeviceEnablePeerAccess(devs[k], 0);
-      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
-        FAIL(h, VPTMCM_EHIP, "hipDeviceEnablePeerAccess(%d -> %d): %s", h->device, devs[k],
-             hipGetErrorString(e));
-      (void)hipGetLastError();  // clear an already-enabled status
+      if (int rc2 = enable(h->device, devs[k])) return rc2;
+      if (int rc2 = enable(devs[k], h->device)) return rc2;
     }
+    HIPCHK(h, hipSetDevice(h->device));
   } else {
     h->grp_comms.assign(n, nullptr);
     std::vector<int> dl(devs, devs + n);
