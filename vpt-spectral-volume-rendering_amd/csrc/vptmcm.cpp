@@ -1082,9 +1082,16 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   if (const char* v = getenv("VPTMCM_DONE_FLAG")) h->done_on = v[0] != '0';
   CK(hipMalloc(&h->done_ctr, sizeof(uint32_t)));
   CK(hipMemsetAsync(h->done_ctr, 0, sizeof(uint32_t), h->stream));
-  CK(hipHostMalloc(&h->done_host, sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
-  *h->done_host = 0u;
-  CK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->done_dev), h->done_host, 0));
+  // the flag word in fine-grained host memory; without it, synchronize waits
+  // for the stream (the signal is an optimisation, never a requirement)
+  if (hipHostMalloc(&h->done_host, sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped) ==
+          hipSuccess &&
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&h->done_dev), h->done_host, 0) == hipSuccess) {
+    *h->done_host = 0u;
+  } else {
+    (void)hipGetLastError();
+    h->done_on = false;
+  }
   if (h->kind == VPTMCM_RENDERER_RGB) {  // WebGPUAbstractComputeRenderer.js:23-28
     static const uint8_t kDefaultTf[8] = {255, 0, 0, 0, 255, 0, 0, 255};
     if (vptmcm_set_transfer_function(h, kDefaultTf, 2, 1)) return fail(VPTMCM_EHIP);
