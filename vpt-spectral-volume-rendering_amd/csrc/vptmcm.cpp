@@ -590,10 +590,9 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
     HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[h->comp_next], 0));
     T.pack = h->comp[h->comp_next];
   }
-  if (signal) {  // every block of the grid counts once
-    h->done_total += tile_blocks(P, kMarchBlock);
-    P.done_target = h->done_total;
-    P.done_seq = ++h->done_seq;
+  if (signal) {  // every block of the grid counts once (committed below, once launched)
+    P.done_target = h->done_total + tile_blocks(P, kMarchBlock);
+    P.done_seq = h->done_seq + 1u;
     T.done_ctr = h->done_ctr;
     T.done_flag = h->done_dev;
   }
@@ -609,6 +608,10 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   h->march_launches++;
   h->sched_cur = c ^ 1u;
   h->grp_dirty = true;
+  if (signal) {
+    h->done_total = P.done_target;
+    h->done_seq = P.done_seq;
+  }
   h->done_pending = signal;
   h->pack_fresh = pack;
   return VPTMCM_OK;
@@ -1792,15 +1795,20 @@ int vptmcm_comm_init(vptmcm* h, const uint8_t* uid, int nranks, int rank) {
   auto job = std::make_shared<InitJob>();
   comm_trace("comm_init: ncclCommInitRank nranks=%d rank=%d (helper thread)", nranks, rank);
   const int dev = h->device;
-  std::thread th([job, id, nranks, rank, dev]() {
-    ncclComm_t c = nullptr;
-    (void)hipSetDevice(dev);
-    const ncclResult_t r = ncclCommInitRank(&c, nranks, id, rank);
-    job->comm = c;
-    job->r = r;
-    int running = 0;
-    if (!job->state.compare_exchange_strong(running, 1) && c) (void)ncclCommAbort(c);  // abandoned
-  });
+  std::thread th;
+  try {
+    th = std::thread([job, id, nranks, rank, dev]() {
+      ncclComm_t c = nullptr;
+      (void)hipSetDevice(dev);
+      const ncclResult_t r = ncclCommInitRank(&c, nranks, id, rank);
+      job->comm = c;
+      job->r = r;
+      int running = 0;
+      if (!job->state.compare_exchange_strong(running, 1) && c) (void)ncclCommAbort(c);  // abandoned
+    });
+  } catch (const std::exception& e) {
+    FAIL(h, VPTMCM_ECOMM, "comm_init: cannot start the initialisation thread: %s", e.what());
+  }
   const int64_t t0 = now_ms();
   while (job->state.load() == 0 && now_ms() - t0 <= h->comm_timeout_ms)
     std::this_thread::sleep_for(std::chrono::microseconds(500));
