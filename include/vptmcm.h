@@ -266,7 +266,8 @@ int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out
  * from it are upper bounds) and the launch count since the last enable, and
  * synchronises. */
 int vptmcm_enable_kernel_timing(vptmcm* h, int enable);
-/* A device-list handle reports the longest replica's region. */
+/* A device-list handle times replica 0 (devices[0]) only: every replica runs
+ * the same launches, and untimed launches enqueue faster. */
 int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches);
 
 /* ---- multi-GPU (photon-parallel replicas, RCCL over xGMI) ----------------- */

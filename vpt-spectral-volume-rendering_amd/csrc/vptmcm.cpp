@@ -1718,25 +1718,15 @@ static int kernel_time_one(vptmcm* h, double* total_ms, uint64_t* launches) {
   return VPTMCM_OK;
 }
 
-// A device-list handle: the longest replica's region (its launches counted
-// once: every replica runs the same launches).
+// A device-list handle times replica 0 only (vptmcm_enable_kernel_timing):
+// every replica runs the same launches, and each timed launch carries event
+// stamps that add ≈ 2–4 µs to its enqueue, i.e. to the skew between the first
+// and the last replica's start when one host thread forwards the launch.
 int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
   if (check_handle(h)) return VPTMCM_EINVAL;
-  if (!total_ms || !launches) FAIL(h, VPTMCM_EINVAL, "kernel_time: null output");
-  double mx = 0.0;
-  uint64_t n0 = 0;
-  int rc = for_replicas(h, [&](vptmcm* c) {
-    double ms = 0.0;
-    uint64_t n = 0;
-    if (int r = kernel_time_one(c, &ms, &n)) return r;
-    if (c == h) n0 = n;
-    mx = ms > mx ? ms : mx;
-    return VPTMCM_OK;
-  });
-  if (rc) return rc;
-  *total_ms = mx;
-  *launches = n0;
-  return VPTMCM_OK;
+  for (vptmcm* c : h->peers)  // their queued passes launch, as for any observation
+    if (int rc = flush_renders(c)) return rc;
+  return kernel_time_one(h, total_ms, launches);
 }
 
 // ------------------------------------------------------------------ multi-GPU
@@ -2171,7 +2161,7 @@ int vptmcm_synchronize(vptmcm* h) {
 
 int vptmcm_enable_kernel_timing(vptmcm* h, int enable) {
   if (check_handle(h)) return VPTMCM_EINVAL;
-  return for_replicas(h, [&](vptmcm* c) { return enable_kernel_timing_one(c, enable); });
+  return enable_kernel_timing_one(h, enable);  // replica 0 only (see vptmcm_kernel_time)
 }
 
 int vptmcm_composite(vptmcm* h) {
