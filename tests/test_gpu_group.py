@@ -86,13 +86,16 @@ def test_group_of_one_is_the_single_device_renderer():
     gpu.close()
 
 
-@pytest.mark.parametrize("n_rep", [2, 3])
-def test_group_replicas_composite_bitexact(n_rep):
+@pytest.mark.parametrize("n_rep,threads", [(2, "1"), (3, "1"), (3, "0"), (8, "1")])
+def test_group_replicas_composite_bitexact(n_rep, threads, monkeypatch):
     """N replicas on one GPU (devices = [0] * N): replica k marches with rank
     k's seed stream (the stream bench.py gives rank k, configs.seed_bits), the
     render target, the fp32 image and the tone mapper see the composite, and
     every output is bit-exact against N oracle replicas composited in replica
-    order. Replica 0's photons are the handle's photons."""
+    order. Replica 0's photons are the handle's photons. Forwarded operations
+    run on the per-replica worker threads, or serially on the caller's thread
+    with VPTMCM_GROUP_THREADS=0: the same bits."""
+    monkeypatch.setenv("VPTMCM_GROUP_THREADS", threads)
     R, vol, tf, mvp = 96, cf.fbm_volume(64, 32, nthreads=8), cf.tf_spectral(), cf.golden_mvp("orbit")
     base = cf.seed_stream(6, start=0)
     g = vptmcm.Renderer(R, devices=[0] * n_rep)

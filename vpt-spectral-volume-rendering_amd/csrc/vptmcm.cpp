@@ -12,12 +12,14 @@
 #include <cfloat>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <utility>
@@ -34,6 +36,30 @@ thread_local std::string g_create_error;
 
 struct EventPair {
   hipEvent_t beg = nullptr, end = nullptr;
+};
+
+// One forwarded operation of a device-list handle, type-erased for a worker.
+struct ReplicaJob {
+  int (*call)(const void*, vptmcm*) = nullptr;
+  const void* f = nullptr;
+};
+
+// The worker thread of one peer replica of a device-list handle: every
+// forwarded operation (ingest, render_passes, reset, the composite's pack and
+// push, synchronize) runs on all replicas at once, each replica's host work
+// and enqueue on its own thread, instead of one replica after another from the
+// caller's thread. Posting is a counter bump; an idle worker spins for the
+// handle's sync_spin_us and then sleeps on the condition variable.
+struct ReplicaWorker {
+  vptmcm* c = nullptr;
+  std::thread th;
+  std::mutex m;
+  std::condition_variable cv;
+  std::atomic<uint64_t> posted{0}, finished{0};
+  std::atomic<bool> quit{false};
+  ReplicaJob job;
+  int rc = 0;
+  int64_t spin_us = 0;
 };
 
 }  // namespace
@@ -170,6 +196,9 @@ struct vptmcm {
   hipEvent_t grp_packed = nullptr; // this replica's pack is complete
   hipEvent_t grp_done = nullptr;   // replica 0: the last composite has read every pack
   std::vector<ncclComm_t> grp_comms;  // RCCL transport: one communicator per replica (InitAll)
+  // replica 0: one worker thread per peer (VPTMCM_GROUP_THREADS=0: none, the
+  // operations run serially on the caller's thread)
+  std::vector<std::unique_ptr<ReplicaWorker>> workers;
 
   std::string err;
 };
@@ -763,27 +792,124 @@ uint32_t pcg_host(uint32_t v) {
 // same photons.
 uint32_t replica_seed(uint32_t s, uint32_t k) { return k ? pcg_host(s ^ (k * 0x9E3779B9u)) : s; }
 
-// Run the same single-replica operation on every peer replica of a
-// device-list handle; a peer's failure is reported on h, naming the replica.
-template <class F>
-int for_peers(vptmcm* h, F&& f) {
-  for (vptmcm* c : h->peers) {
-    const int rc = f(c);
-    if (rc != VPTMCM_OK) {
-      h->err = "replica " + std::to_string(c->replica) + " (device " + std::to_string(c->device) +
-               "): " + c->err;
-      return rc;
-    }
-  }
-  return VPTMCM_OK;
+inline void cpu_relax() {
+#if defined(__x86_64__)
+  __builtin_ia32_pause();
+#endif
 }
 
-// Replica 0 (h) and its peers, in replica order.
-template <class F>
-int for_replicas(vptmcm* h, F&& f) {
-  if (int rc = f(h)) return rc;
-  return for_peers(h, f);
+void worker_main(ReplicaWorker* w) {
+  uint64_t seen = 0;
+  for (;;) {
+    const int64_t t0 = now_us();
+    uint64_t p;
+    while ((p = w->posted.load(std::memory_order_acquire)) == seen) {
+      if (w->quit.load(std::memory_order_acquire)) return;
+      if (now_us() - t0 > w->spin_us) {
+        std::unique_lock<std::mutex> lk(w->m);
+        w->cv.wait(lk, [&] {
+          return w->posted.load(std::memory_order_acquire) != seen || w->quit.load(std::memory_order_acquire);
+        });
+      } else {
+        cpu_relax();
+      }
+    }
+    seen = p;
+    w->rc = w->job.call(w->job.f, w->c);
+    w->finished.store(seen, std::memory_order_release);
+  }
 }
+
+void post(ReplicaWorker* w, const ReplicaJob& job) {
+  w->job = job;
+  {
+    std::lock_guard<std::mutex> lk(w->m);
+    w->posted.store(w->posted.load(std::memory_order_relaxed) + 1, std::memory_order_release);
+  }
+  w->cv.notify_one();
+}
+
+// Wait for the worker's last job: spin, then sleep in short slices (an
+// ingest job is milliseconds of host-to-device copy).
+int await(ReplicaWorker* w, int64_t spin_us) {
+  const uint64_t want = w->posted.load(std::memory_order_relaxed);
+  const int64_t t0 = now_us();
+  while (w->finished.load(std::memory_order_acquire) != want) {
+    if (now_us() - t0 > spin_us)
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    else
+      cpu_relax();
+  }
+  return w->rc;
+}
+
+void start_workers(vptmcm* h) {
+  for (vptmcm* c : h->peers) {
+    auto w = std::make_unique<ReplicaWorker>();
+    w->c = c;
+    w->spin_us = std::max<int64_t>(h->sync_spin_us, 0);
+    w->th = std::thread(worker_main, w.get());
+    h->workers.push_back(std::move(w));
+  }
+}
+
+void stop_workers(vptmcm* h) {
+  for (auto& w : h->workers) {
+    {
+      std::lock_guard<std::mutex> lk(w->m);
+      w->quit.store(true, std::memory_order_release);
+    }
+    w->cv.notify_one();
+  }
+  for (auto& w : h->workers)
+    if (w->th.joinable()) w->th.join();
+  h->workers.clear();
+}
+
+// A peer's failure is reported on h, naming the replica.
+int peer_failed(vptmcm* h, const vptmcm* c, int rc) {
+  h->err = "replica " + std::to_string(c->replica) + " (device " + std::to_string(c->device) + "): " + c->err;
+  return rc;
+}
+
+// Run the same single-replica operation on replica 0 (h, when self) and every
+// peer of a device-list handle: on the peers' worker threads with h's part on
+// the caller's thread, all at once, or one after another without workers. The
+// operation must touch only its own replica (and read shared inputs). Every
+// replica runs it; the first failure in replica order is the result.
+template <class F>
+int run_replicas(vptmcm* h, bool self, const F& f) {
+  if (h->workers.empty()) {
+    if (self)
+      if (int rc = f(h)) return rc;
+    for (vptmcm* c : h->peers)
+      if (int rc = f(c)) return peer_failed(h, c, rc);
+    return VPTMCM_OK;
+  }
+  ReplicaJob job;
+  job.call = [](const void* p, vptmcm* c) { return (*static_cast<const F*>(p))(c); };
+  job.f = &f;
+  for (auto& w : h->workers) post(w.get(), job);
+  const int rc0 = self ? f(h) : VPTMCM_OK;
+  int first = VPTMCM_OK;
+  const vptmcm* bad = nullptr;
+  for (auto& w : h->workers) {
+    const int rc = await(w.get(), h->sync_spin_us);
+    if (rc && !bad) {
+      first = rc;
+      bad = w->c;
+    }
+  }
+  if (rc0) return rc0;
+  return bad ? peer_failed(h, bad, first) : VPTMCM_OK;
+}
+
+template <class F>
+int for_peers(vptmcm* h, const F& f) { return run_replicas(h, false, f); }
+
+// Replica 0 (h) and its peers.
+template <class F>
+int for_replicas(vptmcm* h, const F& f) { return run_replicas(h, true, f); }
 
 bool composited(const vptmcm* h) { return !h->peers.empty(); }
 
@@ -923,6 +1049,8 @@ static int create_group(const vptmcm_config* cfg, vptmcm** out) {
   if (n > 1 || h->group_transport == VPTMCM_GROUP_RCCL) {
     if ((rc = group_alloc(h, cfg->devices, n))) return fail(rc, "vptmcm_create: " + h->err);
   }
+  const char* threads = getenv("VPTMCM_GROUP_THREADS");
+  if (n > 1 && !(threads && threads[0] == '0')) start_workers(h);
   *out = h;
   return VPTMCM_OK;
 }
@@ -1107,6 +1235,7 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
 
 void vptmcm_destroy(vptmcm* h) {
   if (!h) return;
+  stop_workers(h);
   // Replicas first: their streams may feed this one's composite (they hold no
   // communicator, so their waits are plain stream waits).
   for (vptmcm* c : h->peers) {
@@ -1724,8 +1853,8 @@ static int kernel_time_one(vptmcm* h, double* total_ms, uint64_t* launches) {
 // and the last replica's start when one host thread forwards the launch.
 int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches) {
   if (check_handle(h)) return VPTMCM_EINVAL;
-  for (vptmcm* c : h->peers)  // their queued passes launch, as for any observation
-    if (int rc = flush_renders(c)) return rc;
+  // their queued passes launch, as for any observation
+  if (int rc = for_peers(h, [](vptmcm* c) { return flush_renders(c); })) return rc;
   return kernel_time_one(h, total_ms, launches);
 }
 
@@ -2147,10 +2276,15 @@ int vptmcm_render_passes(vptmcm* h, const float* mvp, const uint32_t* seeds, uin
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (h->peers.empty()) return render_passes_one(h, mvp, seeds, n);
   if (!seeds && n) FAIL(h, VPTMCM_EINVAL, "render_passes: null argument");
-  std::vector<uint32_t> rs(n);
   return for_replicas(h, [&](vptmcm* c) {
-    for (uint32_t k = 0; k < n; k++) rs[k] = replica_seed(seeds[k], c->replica);
-    return render_passes_one(c, mvp, rs.data(), n);
+    uint32_t rs[kMaxFusedPasses];
+    if (n == 0) return render_passes_one(c, mvp, rs, 0);
+    for (uint32_t k0 = 0; k0 < n; k0 += kMaxFusedPasses) {
+      const uint32_t m = std::min<uint32_t>(n - k0, kMaxFusedPasses);
+      for (uint32_t k = 0; k < m; k++) rs[k] = replica_seed(seeds[k0 + k], c->replica);
+      if (int rc = render_passes_one(c, mvp, rs, m)) return rc;
+    }
+    return VPTMCM_OK;
   });
 }
 
