@@ -82,7 +82,10 @@ typedef struct vptmcm_config {
      * handle holds N photon-parallel replicas, replica k on devices[k] with the
      * seed stream of rank k (seed bits s -> s for k = 0, pcg(s ^ k*0x9E3779B9)
      * otherwise; the same streams as N one-GPU processes). Every input goes to
-     * every replica; render/reset run on all of them; the render target
+     * every replica; render/reset run on all of them (N > 1: each peer
+     * replica's share on a worker thread the handle owns, replica 0's on the
+     * calling thread, all at once; VPTMCM_GROUP_THREADS=0 forwards serially
+     * on the calling thread); the render target
      * (read_rgba16f, read_rgb, tonemap) is the composite sum(rgb*n)/sum(n) over
      * the replicas, computed on devices[0] (N = 1: the replica's own image,
      * bit for bit). read/write_photons and the diagnostics see replica 0. The
