@@ -326,9 +326,7 @@ def main():
         the display could show). Returns the pass count of every march launch."""
         launches, done = [], 0
         if composite is None and F == 32:
-            # one call: the library launches it in 32-pass launches, the ones
-            # before the last balancing their tails across launch boundaries
-            # (DESIGN.md §5, cross-launch balancing); the last completes every tile
+            # one call: the library launches it in 32-pass launches
             r.render_passes(mvp, seeds[first:first + count])
             return [min(32, count - k) for k in range(0, count, 32)]
         while done < count:

@@ -26,8 +26,7 @@
     __builtin_amdgcn_s_waitcnt(0x0F70);   \
     TL_MARK(k);                           \
   } while (0)
-// extra (non-zero): word 6 instead of the probe time (carry launches: the
-// tile's passes to do << 16 | passes done << 8 | owing)
+// extra (non-zero): word 6 instead of the probe time (a caller-defined word)
 #define TL_END(out, tile, entered, extra)                                                \
   do {                                                                                   \
     TL_MARK_WAIT(4);                                                                     \
