@@ -8,6 +8,8 @@ matrices (incl. a camera inside the volume) — against the oracle, bit for bit,
 through unfused and fused (queued) passes. Each case prints its draw, so a
 failure names the configuration that exposed it.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -18,7 +20,10 @@ from test_gpu_parity import assert_photons_equal, assert_rgb32_equal, assert_rgb
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = 96
+# VPTMCM_FUZZ_CASES / VPTMCM_FUZZ_BASE: a longer campaign over fresh draws
+# (tools/fuzz_campaign.sh; the suite's defaults are 96 cases from base 0)
+N_CASES = int(os.environ.get("VPTMCM_FUZZ_CASES", "96"))
+BASE = int(os.environ.get("VPTMCM_FUZZ_BASE", "0"))
 # (MODE, layout template) pairs the random cases' fused launches ran
 # (vptmcm_debug_last_launch); test_mode_template_coverage forces the rest
 HIT = set()
@@ -92,7 +97,7 @@ def _tf(rng):
 
 
 def _draw(k):
-    rng = np.random.default_rng(1000 + k)
+    rng = np.random.default_rng(1000 + BASE + k)
     R = int(rng.choice([8, 16, 24, 40, 48, 64, 72, 96, 128, 200, 256])) + (int(rng.integers(1, 8)) if rng.random() < 0.3 else 0)
     shape = tuple(int(x) for x in rng.integers(1, 72, 3)) if rng.random() < 0.4 else (48, 48, 48)
     layout = int(rng.choice([vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_LINEAR, vptmcm.LAYOUT_BRICK8,
@@ -142,7 +147,7 @@ def test_random_configuration_bitexact(k):
         gpu.set_params(**params)
         cpu.volume, cpu.tf, cpu.light, cpu.light_dir = vol, tf, spd, ld
         cpu.params.update(**params)
-        seeds = cf.seed_stream(6, start=10 * k)
+        seeds = cf.seed_stream(6, start=10 * (BASE + k))
         gpu.reset(mvp, seeds[0])
         cpu.reset(mvp, seeds[0], nthreads=16)
         assert_photons_equal(gpu.read_photons(), cpu.photons, what + " reset")
@@ -174,7 +179,7 @@ def test_random_configuration_rgb_bitexact(k):
     rgba8 TF image (random width/height; the kernel samples row 0), a random
     environment colour and a random anisotropy."""
     R, shape, layout, _, _, _, _, params, mvp, vol_seed, what = _draw(k)
-    rng = np.random.default_rng(5000 + k)
+    rng = np.random.default_rng(5000 + BASE + k)
     tf = rng.integers(0, 256, (int(rng.integers(1, 4)), int(rng.integers(2, 300)), 4), dtype=np.uint8)
     env = tuple(int(x) for x in rng.integers(0, 256, 4))
     aniso = float(np.float32(rng.uniform(-0.95, 0.95)))
@@ -191,7 +196,7 @@ def test_random_configuration_rgb_bitexact(k):
         gpu.set_params(**params)
         cpu.volume, cpu.tf, cpu.env = vol, tf, np.array(env, np.uint8)
         cpu.params.update(**params)
-        seeds = cf.seed_stream(6, start=10 * k + 3)
+        seeds = cf.seed_stream(6, start=10 * (BASE + k) + 3)
         gpu.reset(mvp, seeds[0])
         cpu.reset(mvp, seeds[0])
         assert _same_words(gpu.read_photons(), cpu.photons).all(), what + " reset"
@@ -227,9 +232,9 @@ def test_random_bands_bitexact(k):
     8-row tiles; the last band ends at R, which need not be a multiple of 8), one
     handle per band; every band's rows equal the oracle's full frame and the band
     images sum to the oracle's fp32 image, bit for bit."""
-    draw = _draw(200 + k)
+    draw = _draw(200 + k)  # (BASE applies inside _draw)
     R, mvp, what = draw[0], draw[8], draw[10]
-    rng = np.random.default_rng(7000 + k)
+    rng = np.random.default_rng(7000 + BASE + k)
     tiles = (R + 7) // 8
     cuts = sorted(set(int(c) * 8 for c in rng.integers(1, tiles, int(rng.integers(0, 4))))) if tiles > 1 else []
     edges = [0] + cuts + [R]
@@ -243,7 +248,7 @@ def test_random_bands_bitexact(k):
             _setup_spectral(g, orc.Oracle(R), draw)
         for g, (y0, y1) in zip(gpus, bands):
             g.set_band(y0, y1)
-        seeds = cf.seed_stream(5, start=10 * k + 7)
+        seeds = cf.seed_stream(5, start=10 * (BASE + k) + 7)
         cpu.reset(mvp, seeds[0], nthreads=16)
         for s in seeds[1:]:
             rgb, want = cpu.render(mvp, s, nthreads=16)
