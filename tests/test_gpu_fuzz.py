@@ -271,6 +271,51 @@ def test_random_bands_bitexact(k):
             g.close()
 
 
+@pytest.mark.parametrize("k", range(max(1, N_CASES // 8)))
+def test_random_group_composite_bitexact(k):
+    """Device-list handles under random draws: 2-8 replicas on device 0 (every
+    forwarded call on the replicas' worker threads), replica j on rank j's seed
+    stream; replica 0's photons, the composite's fp32 and rgba16float images and
+    its sample counts bit for bit against the oracle replicas composited in
+    replica order (tests/test_gpu_group.py's numpy restatement of k_composite)."""
+    from test_gpu_group import _composite
+    R, shape, layout, spec, tf, ld, spd, params, mvp, vol_seed, what = _draw(400 + k)
+    rng = np.random.default_rng(9000 + BASE + k)
+    n_rep = int(rng.integers(2, 9))
+    what = f"group x{n_rep} {what}"
+    print(what)
+    vol = _volume(shape, vol_seed)
+    start = 10 * (BASE + k) + 9
+    seeds = cf.seed_stream(5, start=start)
+    with vptmcm.Renderer(R, devices=[0] * n_rep, layout=layout) as g:
+        g.set_spectrum(spec)
+        g.set_volume(vol)
+        g.set_material_tf(tf)
+        g.set_light(spd, ld)
+        g.set_params(**params)
+        g.reset(mvp, seeds[0])
+        g.render(mvp, seeds[1])
+        g.read_rgb()  # a composite between passes: an unfused launch, then a fused one
+        g.render_passes(mvp, seeds[2:])
+        reps = []
+        for j in range(n_rep):
+            o = orc.Oracle(R)
+            o.set_spectrum(spec)
+            o.volume, o.tf, o.light, o.light_dir = vol, tf, spd, ld
+            o.params.update(**params)
+            rs = cf.seed_stream(5, start=start, rank=j)
+            o.reset(mvp, rs[0], nthreads=16)
+            for s_ in rs[1:]:
+                rgb, _ = o.render(mvp, s_, nthreads=16)
+            reps.append((o, rgb))
+        assert_photons_equal(g.read_photons(), reps[0][0].photons, what + " replica 0")
+        want_rgb, want_rgba, want_n = _composite(reps)
+        q, crgb, n = g.read_composite_all()
+        assert np.array_equal(n, want_n), what + " counts"
+        assert_rgb32_equal(crgb, want_rgb, what + " composite fp32")
+        assert_rgba_equal(q, want_rgba, what + " composite rgba16f")
+
+
 def _close_bins():
     """3 bins whose inner boundaries (500.1, 500.15 nm) put two distinct
     thresholds in one cell of the wavelength-bin table: the table is refused and
