@@ -843,13 +843,20 @@ int await(ReplicaWorker* w, int64_t spin_us) {
   return w->rc;
 }
 
+void stop_workers(vptmcm* h);
+
+// Without every worker (thread creation failed) the handle forwards serially.
 void start_workers(vptmcm* h) {
-  for (vptmcm* c : h->peers) {
-    auto w = std::make_unique<ReplicaWorker>();
-    w->c = c;
-    w->spin_us = std::max<int64_t>(h->sync_spin_us, 0);
-    w->th = std::thread(worker_main, w.get());
-    h->workers.push_back(std::move(w));
+  try {
+    for (vptmcm* c : h->peers) {
+      auto w = std::make_unique<ReplicaWorker>();
+      w->c = c;
+      w->spin_us = std::max<int64_t>(h->sync_spin_us, 0);
+      w->th = std::thread(worker_main, w.get());
+      h->workers.push_back(std::move(w));
+    }
+  } catch (...) {
+    stop_workers(h);
   }
 }
 
