@@ -1652,6 +1652,7 @@ static int synchronize_one(vptmcm* h) {
     const int64_t t0 = now_us();
     for (uint32_t k = 0;; k++) {
       if (*f == h->done_seq) {
+        std::atomic_thread_fence(std::memory_order_acquire);  // the march's stores before the flag
         done = true;
         break;
       }
