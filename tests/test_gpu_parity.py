@@ -1032,6 +1032,42 @@ def test_c3_bench_settled_state_driver_launch_rows_bitexact():
     gpu.close()
 
 
+def test_c3_bench_default_region_rows_bitexact():
+    """The state the default bench line times (`python bench.py`: 10,240
+    clock-settling passes, 4,096 warm-up passes, then the 1,024 timed passes,
+    all in 32-pass launches): a 16-row band through the cube bit-exact against
+    the oracle's row-restricted run of all 15,361 passes."""
+    R, S = 512, 8
+    vol, tf, mvp = cf.fbm_volume(512, 512, nthreads=8), cf.tf_spectral(), cf.default_mvp_inverse()
+    gpu, cpu = make_pair(R, vol, tf, ext=32.0, steps=S, layout=vptmcm.LAYOUT_COLUMN4)
+    W, K = 4096, 1024
+    seeds = cf.seed_stream(1 + W + K, start=0, rank=0)
+    sseeds = cf.seed_stream(32, start=1 << 20, rank=0)
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0], nthreads=16)
+    for _ in range(320):
+        gpu.render_passes(mvp, sseeds)
+    gpu.render_passes(mvp, seeds[1:1 + W])
+    gpu.render_passes(mvp, seeds[1 + W:])
+    info = gpu.last_launch()
+    assert (info["passes"], info["mode"], info["tpl"]) == (32, 2, 5), info
+    rows = (256, 272)
+    for _ in range(320):
+        for s in sseeds:
+            cpu.render(mvp, s, nthreads=16, rows=rows)
+    for s in seeds[1:]:
+        rgb, want = cpu.render(mvp, s, nthreads=16, rows=rows)
+    y0, y1 = rows
+    got = gpu.read_photons().reshape(R, R, -1)
+    exp = cpu.photons.reshape(R, R, -1)
+    assert_photons_equal(got[y0:y1].reshape(-1, got.shape[-1]), exp[y0:y1].reshape(-1, exp.shape[-1]),
+                         "C3 default bench region")
+    assert_rgb32_equal(gpu.read_rgb()[y0:y1], rgb[y0:y1], "C3 default bench region")
+    assert_rgba_equal(gpu.read_rgba16f()[y0:y1], want[y0:y1], "C3 default bench region")
+    assert np.median(got[y0:y1, :, 7]) > 1500
+    gpu.close()
+
+
 @pytest.mark.parametrize("layout", [vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_BRICK8])
 def test_queued_renders_matrix_change_and_inputs(layout):
     """render() calls queue passes that launch as fused marches: a render()
