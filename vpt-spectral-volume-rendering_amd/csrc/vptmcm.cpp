@@ -1032,26 +1032,55 @@ static int create_group(const vptmcm_config* cfg, vptmcm** out) {
         return VPTMCM_EINVAL;
       }
   }
-  vptmcm_config one = *cfg;
-  one.n_devices = 0;
-  one.device = cfg->devices[0];
-  vptmcm* h = nullptr;
-  int rc = vptmcm_create(&one, &h);
-  if (rc) return rc;
+  // The replicas' handles are created at once, the peers on threads of their
+  // own (each device's runtime initialisation and allocations overlap), replica
+  // 0 on the caller's thread; then checked in replica order.
+  struct Made {
+    vptmcm* h = nullptr;
+    int rc = VPTMCM_OK;
+    std::string err;
+  };
+  std::vector<Made> made(n);
+  auto make = [&](uint32_t k) {
+    vptmcm_config one = *cfg;
+    one.n_devices = 0;
+    one.device = cfg->devices[k];
+    made[k].rc = vptmcm_create(&one, &made[k].h);
+    if (made[k].rc) made[k].err = g_create_error;  // thread-local: copied out here
+  };
+  std::vector<std::thread> makers;
+  for (uint32_t k = 1; k < n; k++) {
+    try {
+      makers.emplace_back(make, k);
+    } catch (...) {
+      make(k);  // no thread: create it here
+    }
+  }
+  make(0);
+  for (auto& t : makers) t.join();
+  int rc = VPTMCM_OK;
+  std::string msg;
+  for (uint32_t k = 0; k < n && !rc; k++)
+    if (made[k].rc) {
+      rc = made[k].rc;
+      msg = k ? "replica " + std::to_string(k) + ": " + made[k].err : made[k].err;
+    }
+  if (rc) {
+    for (auto& m : made) vptmcm_destroy(m.h);
+    g_create_error = msg;
+    return rc;
+  }
+  vptmcm* h = made[0].h;
   h->grouped = true;
   h->group_transport = cfg->group_transport;
-  auto fail = [&](int code, const std::string& msg) {
+  auto fail = [&](int code, const std::string& m) {
     vptmcm_destroy(h);
-    g_create_error = msg;
+    g_create_error = m;
     return code;
   };
   for (uint32_t k = 1; k < n; k++) {
-    one.device = cfg->devices[k];
-    vptmcm* c = nullptr;
-    rc = vptmcm_create(&one, &c);
-    if (rc) return fail(rc, "replica " + std::to_string(k) + ": " + g_create_error);
-    c->replica = k;
-    h->peers.push_back(c);
+    made[k].h->replica = k;
+    h->peers.push_back(made[k].h);
   }
   if (n > 1 || h->group_transport == VPTMCM_GROUP_RCCL) {
     if ((rc = group_alloc(h, cfg->devices, n))) return fail(rc, "vptmcm_create: " + h->err);
@@ -1159,13 +1188,14 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
       return fail(VPTMCM_EINVAL);
     }
     h->device = cfg->device;
-    // VPTMCM_SYNC_SPIN=1 (analysis): host waits spin instead of yielding
-    if (const char* v = getenv("VPTMCM_SYNC_SPIN"))
-      if (v[0] == '1') (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
     if (hipSetDevice(h->device) != hipSuccess) {
       h->err = "vptmcm_create: hipSetDevice failed";
       return fail(VPTMCM_EHIP);
     }
+    // VPTMCM_SYNC_SPIN=1 (analysis): host waits on this device spin instead of
+    // yielding (the flags of the calling thread's current device: set after it)
+    if (const char* v = getenv("VPTMCM_SYNC_SPIN"))
+      if (v[0] == '1') (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
   } else {
     (void)hipGetDevice(&h->device);
   }
