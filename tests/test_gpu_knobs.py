@@ -19,6 +19,7 @@ KNOBS = [("VPTMCM_MARCH_VARIANT", str(b)) for b in (1, 2, 4, 8, 16, 32, 64, 128)
     ("VPTMCM_MARCH_VARIANT", "255"),
     ("VPTMCM_DARK", "0"),
     ("VPTMCM_DONE_FLAG", "0"),
+    ("VPTMCM_SCHED_CACHE", "0"),
     ("VPTMCM_TIME_STOP", "0"),
     ("VPTMCM_TIME_BEGIN", "marker"),
     ("VPTMCM_SYNC_SPIN_US", "0"),

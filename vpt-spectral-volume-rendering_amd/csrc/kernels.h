@@ -45,6 +45,14 @@ struct TileSched {
   // (rgb * n, n) per pixel of the launch's last pass (k_pack's values, written
   // with the image; the cross-rank composite's buffer), or null
   float4* pack;
+  // Deal reuse: a wave whose tile's flag changed writes the launch's
+  // MarchParams::launch_seq to changed_out; the next launch reads it as
+  // changed_in (the two words alternate like the flag rows). A launch whose
+  // predecessor changed no flag deals exactly what that launch dealt (the
+  // deal is a function of the flags alone), so it takes each slot's tile from
+  // prev instead of running the schedule.
+  const uint32_t* changed_in;
+  uint32_t* changed_out;
 };
 // Flag byte of a tile (written by each launch for the next one's schedule):
 // bit 0 its wave entered the volume.

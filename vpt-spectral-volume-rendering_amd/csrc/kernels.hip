@@ -396,6 +396,24 @@ __device__ __forceinline__ const __attribute__((address_space(4))) float* cmf_ta
                                                                offsetof(MarchParams, xb)) / 4);
 }
 
+// Deal reuse bookkeeping at a wave's end (TileSched::changed_out): the launch
+// number and the word's address re-read from the kernarg segment through an
+// opaque pointer, so neither stays live in SGPRs across the march.
+constexpr uint32_t kKargMarch = sizeof(PassSeeds);  // MarchParams follows PassSeeds
+constexpr uint32_t kKargSched = (kKargMarch + (uint32_t)sizeof(MarchParams) + 7u) & ~7u;
+static_assert(alignof(MarchParams) <= 8 && alignof(TileSched) == 8 && kKargMarch % 8 == 0,
+              "kernel arguments laid out at their natural alignment: PassSeeds, MarchParams, TileSched");
+__device__ __forceinline__ void note_flag_change(uint32_t flag, bool hot0) {
+  if (flag == (hot0 ? kFlagVolume : 0u)) return;
+  auto k = (const __attribute__((address_space(4))) uint8_t*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(k));
+  const uint32_t seq = *(const __attribute__((address_space(4))) uint32_t*)(k + kKargMarch +
+                                                                           offsetof(MarchParams, launch_seq));
+  uint32_t* out = *(uint32_t* const __attribute__((address_space(4)))*)(k + kKargSched +
+                                                                         offsetof(TileSched, changed_out));
+  *out = seq;
+}
+
 // A pixel centre outside the robust-miss box or beyond one of the hull edges
 // (MarchParams::rb_edge; unused edges never qualify).
 __device__ __forceinline__ bool robust_pixel(const MarchParams& P, float sx, float sy) {
@@ -491,7 +509,15 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   bool hot0;  // the tile entered the volume last launch (its wave is a long one)
   bool have = false;  // p already holds this tile's state (the slot's tile did not change)
   if (P.sched != 1u) {
-    const uint32_t s = __builtin_amdgcn_readfirstlane(schedule_tile(P, f0, T.flags_in, s_red, s_tile));
+    // the previous launch changed no tile's flag: its deal stands (a uniform
+    // branch: every block reads the same word)
+    bool reuse = false;
+    if (P.sched_reuse != 0u) {
+      const auto cw = (const __attribute__((address_space(4))) uint32_t*)T.changed_in;
+      reuse = cw[0] != P.launch_seq - 1u;
+    }
+    const uint32_t s = reuse ? prev
+                             : __builtin_amdgcn_readfirstlane(schedule_tile(P, f0, T.flags_in, s_red, s_tile));
     tile = s == 0xffffffffu ? s : s & kSlotTileMask;
     hot0 = s != 0xffffffffu && (s >> 31) != 0u;
     have = hot0 && s == prev;
@@ -550,7 +576,11 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   TL_MARK_WAIT(2);
   if (!live || PS.n == 0u) {
     // an idle out-of-band tile (or a launch of no pass): its flag carries over
-    if (tile < P.n_tiles && lane == 0u) T.flags_out[tile] = (live && hot0) ? kFlagVolume : 0u;
+    if (tile < P.n_tiles && lane == 0u) {
+      const uint32_t nf = (live && hot0) ? kFlagVolume : 0u;
+      T.flags_out[tile] = nf;
+      note_flag_change(nf, hot0);
+    }
     signal_done(P, T, &s_done);
     return;
   }
@@ -948,7 +978,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   for (int b = 0; b < kMaxBins; b++)
     if (NBF || !VPT_NB_ZERO || (uint32_t)b < P.nb) ph[(kRad0 + b) * S + i] = p.rad[b];
 
-  if (lane == 0u) T.flags_out[tile] = entered;  // the next launch's schedule
+  if (lane == 0u) {  // the next launch's schedule
+    T.flags_out[tile] = entered;
+    note_flag_change(entered, hot0);
+  }
   signal_done(P, T, &s_done);
   STAMP_END(rgb32, tile, entered);
   TL_END(rgb32, tile, entered, 0u);
@@ -1021,19 +1054,28 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
   __shared__ float4 s_tf[kRgbTfMax];
   __shared__ uint32_t s_red[64];
   __shared__ uint32_t s_tile[16];
-  // the SIMD-balanced tile schedule and volume-wave priority of k_march
+  // the SIMD-balanced tile schedule and volume-wave priority of k_march, and
+  // its reuse of the previous launch's deal (TileSched::changed_in)
   uint32_t tile;
   bool hot = true;
   if (P.sched != 1u) {
-    const uint32_t s = __builtin_amdgcn_readfirstlane(
-        schedule_tile(P, sched_flags_first(T.flags_in), T.flags_in, s_red, s_tile));
-    tile = s == 0xffffffffu ? s : s & 0x7fffffffu;
+    const uint32_t slot = blockIdx.x * 16u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t prev = ((const __attribute__((address_space(4))) uint32_t*)T.prev)[slot];
+    bool reuse = false;
+    if (P.sched_reuse != 0u)
+      reuse = ((const __attribute__((address_space(4))) uint32_t*)T.changed_in)[0] != P.launch_seq - 1u;
+    const uint32_t s = reuse ? prev
+                             : __builtin_amdgcn_readfirstlane(
+                                   schedule_tile(P, sched_flags_first(T.flags_in), T.flags_in, s_red, s_tile));
+    if ((threadIdx.x & 63u) == 0u && s != prev) T.prev[slot] = s;
+    tile = s == 0xffffffffu ? s : s & kSlotTileMask;
     hot = s != 0xffffffffu && (s >> 31) != 0u;
   } else {
     tile = xcd_swizzle(blockIdx.x, gridDim.x) * (kMarchBlock / 64) +
            __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (tile >= P.n_tiles) tile = 0xffffffffu;
   }
+  const bool hot0 = hot;  // the tile's flag as this launch found it
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t x = (tile % P.tiles_x) * 8u + (lane & 7u);
   const uint32_t y = (tile / P.tiles_x) * 8u + (lane >> 3);
@@ -1053,7 +1095,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
   for (uint32_t k = threadIdx.x; k < P.tf_w; k += kMarchBlock) s_tf[k] = tf[k];
   __syncthreads();
   if (!live) {
-    if (tile < P.n_tiles && lane == 0u) T.flags_out[tile] = 0u;  // an idle out-of-band tile
+    if (tile < P.n_tiles && lane == 0u) {  // an idle out-of-band tile
+      T.flags_out[tile] = 0u;
+      note_flag_change(0u, hot0);
+    }
     return;
   }
 
@@ -1188,7 +1233,10 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
                                tr.x, tr.y, tr.z, rad.x, rad.y, rad.z};
 #pragma unroll
   for (uint32_t k = 0; k < kRgbPlanes; k++) ph[k * S + i] = w[k];
-  if (lane == 0u) T.flags_out[tile] = entered ? 1u : 0u;  // the next launch's schedule
+  if (lane == 0u) {  // the next launch's schedule
+    T.flags_out[tile] = entered ? 1u : 0u;
+    note_flag_change(entered ? 1u : 0u, hot0);
+  }
 }
 
 // --------------------------------------------------------- volume relayout

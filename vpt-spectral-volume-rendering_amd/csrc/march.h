@@ -124,6 +124,11 @@ struct MarchParams {
   // Completion signal (TileSched::done_ctr / done_flag): the cumulative wave
   // count after this launch and the value its last wave writes to the flag.
   uint32_t done_target, done_seq;
+  // The handle's march launch count including this one, and whether this
+  // launch may keep the previous launch's tile deal (TileSched::changed_in):
+  // 1 unless the host touched the schedule state since (first launch,
+  // VPTMCM_SCHED_CACHE=0).
+  uint32_t launch_seq, sched_reuse;
 };
 constexpr uint32_t kBinLutCells = 1024u;
 constexpr uint32_t kBinLutShift = 22u;

@@ -104,6 +104,8 @@ struct vptmcm {
   uint8_t* sched = nullptr;    // tile schedule flags: [2][sched_flag_bytes(n_tiles)]
   uint32_t* sched_prev = nullptr;  // each wave slot's last scheduled tile (TileSched::prev)
   uint32_t sched_cur = 0;      // which flag row the next march reads
+  uint32_t* sched_changed = nullptr;  // [2] TileSched::changed_in / changed_out, alternating
+  bool sched_cache = true;     // VPTMCM_SCHED_CACHE=0: every launch runs the schedule
   uint32_t dark = 1;           // MarchParams::dark: 1 the dark-background chain, 0 off (VPTMCM_DARK)
 
   float spectrum[VPTMCM_SPECTRUM_FLOATS] = {};
@@ -612,7 +614,12 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   if (h->timing && h->time_stop) ee = h->region.end;
   const uint8_t* vol = h->layout != kLayoutLinear ? (const uint8_t*)h->vol_c8 : h->vol_lin;
   const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
-  TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev, nullptr, nullptr, nullptr};
+  TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev, nullptr, nullptr, nullptr,
+              h->sched_changed + c, h->sched_changed + (c ^ 1u)};
+  // the previous launch's deal may stand unless this is the handle's first
+  // launch (only launches touch the schedule state)
+  P.launch_seq = (uint32_t)(h->march_launches + 1u);
+  P.sched_reuse = (h->sched_cache && h->march_launches > 0u) ? 1u : 0u;
   const bool signal = h->done_on && h->kind == VPTMCM_RENDERER_SPECTRAL;
   const bool pack = h->comm && h->kind == VPTMCM_RENDERER_SPECTRAL && h->band_y0 == 0 && h->band_y1 == h->R;
   if (pack) {  // the buffer is free once the all-reduce issued two composites ago is done
@@ -1246,8 +1253,11 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   CK(hipMemsetAsync(h->sched, 0, 2 * (size_t)sched_flag_bytes(h->n_tiles), h->stream));
   CK(hipMalloc(&h->sched_prev, sched_slot_words(h->n_tiles) * sizeof(uint32_t)));
   CK(hipMemsetAsync(h->sched_prev, 0xff, sched_slot_words(h->n_tiles) * sizeof(uint32_t), h->stream));
+  CK(hipMalloc(&h->sched_changed, 2 * sizeof(uint32_t)));
+  CK(hipMemsetAsync(h->sched_changed, 0, 2 * sizeof(uint32_t), h->stream));
   if (const char* v = getenv("VPTMCM_DARK")) h->dark = v[0] == '0' ? 0u : 1u;
   if (const char* v = getenv("VPTMCM_DONE_FLAG")) h->done_on = v[0] != '0';
+  if (const char* v = getenv("VPTMCM_SCHED_CACHE")) h->sched_cache = v[0] != '0';
   CK(hipMalloc(&h->done_ctr, sizeof(uint32_t)));
   CK(hipMemsetAsync(h->done_ctr, 0, sizeof(uint32_t), h->stream));
   // the flag word in fine-grained host memory; without it, synchronize waits
@@ -1340,6 +1350,7 @@ void vptmcm_destroy(vptmcm* h) {
   if (h->light) (void)hipFree(h->light);
   if (h->sched) (void)hipFree(h->sched);
   if (h->sched_prev) (void)hipFree(h->sched_prev);
+  if (h->sched_changed) (void)hipFree(h->sched_changed);
   if (h->done_ctr) (void)hipFree(h->done_ctr);
   if (h->done_host) (void)hipHostFree(h->done_host);
   if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
