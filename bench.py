@@ -222,6 +222,25 @@ def group_devices(n: int) -> list:
     return devs
 
 
+TF_DESC = {"spectral": "spectral TF (HG g=0.702)", "grey": "grey TF", "zero": "zero TF",
+           "materials": "UI-like materials TF (varying anisotropy)",
+           "materials_const": "UI-like materials TF (constant anisotropy)"}
+
+
+def volume_seed(n: int) -> int:
+    """BASELINE.md's fBm seeds: C3's 512^3 volume seed 512, C5's 1024^3 seed 1024."""
+    return 512 if n == 512 else n
+
+
+def config_name(volume: int, n_gpus: int) -> str:
+    """The BASELINE.json config a line measures (C3 / C4: 512^3 on 1 / N GPUs; C5: 1024^3)."""
+    if volume == 512:
+        return "C4" if n_gpus > 1 else "C3"
+    if volume == 1024:
+        return "C5" if n_gpus > 1 else "C5 (one GPU)"
+    return "custom"
+
+
 def main():
     a = parse()
     rank, world, local = rendezvous.env_world()
@@ -241,7 +260,7 @@ def main():
 
     # ---- inputs (synthetic)
     t = time.perf_counter()
-    vol = cf.fbm_volume(a.volume, 512 if a.volume == 512 else a.volume)
+    vol = cf.fbm_volume(a.volume, volume_seed(a.volume))
     gen_s = time.perf_counter() - t
     tf = {"spectral": cf.tf_spectral, "grey": cf.tf_grey, "zero": cf.tf_zero,
           "materials": lambda: cf.tf_materials(True),
@@ -591,9 +610,9 @@ def main():
             "ms_per_step": round(el_max * 1e3 / a.steps, 5), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {
-                "workload": f"C{'4' if n_gpus > 1 else '3'}: {a.volume}^3 fBm volume (seed 512), spectral TF "
-                            f"(HG g=0.702), R={R}, S={S}, {a.bins} bins, extinction {a.extinction}, "
-                            f"{a.camera} camera",
+                "workload": f"{config_name(a.volume, n_gpus)}: {a.volume}^3 fBm volume (seed "
+                            f"{volume_seed(a.volume)}), {TF_DESC.get(a.tf, a.tf + ' TF')}, R={R}, S={S}, "
+                            f"{a.bins} bins, extinction {a.extinction}, {a.camera} camera",
                 "resolution": R, "photon_steps_per_pass": S, "volume": a.volume,
                 "volume_layout": a.layout, "passes_per_launch": ppl,
                 "clock_settle_ms": round(settle_ms, 1), "clock_settle_passes": settle_passes,

@@ -121,7 +121,7 @@ def test_bench_two_ranks_driver_command_line(tmp_path, world):
     assert all("RCCL version" in o[1] for o in outs)
     rec = json.loads(line[0])
     assert rec["n_gpus"] == world and rec["steps"] == 20 and rec["warmup"] == 5
-    assert rec["value"] > 0 and rec["config"]["workload"].startswith("C4")
+    assert rec["value"] > 0 and rec["config"]["workload"].startswith("custom: 16^3")
     assert rec["per_pass_allreduce"]["steps"] == 64 and rec["per_pass_allreduce"]["value"] > 0
     logs = [json.loads((tmp_path / f"log{r}.json").read_text()) for r in range(world)]
     uids = {e[1] for lg in logs for e in lg if e[0] == "comm_init"}
@@ -247,7 +247,7 @@ def test_bench_gpus4_without_launcher_is_one_device_list_handle(tmp_path, transp
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     rec = json.loads(lines[0])
-    assert rec["n_gpus"] == 4 and rec["config"]["workload"].startswith("C4")
+    assert rec["n_gpus"] == 4 and rec["config"]["workload"].startswith("custom: 16^3")
     assert rec["config"]["devices"] == [0, 1, 2, 3]
     assert rec["config"]["composite_transport"] == {"peer": "peer-push", "rccl": "rccl-reduce"}[transport]
     assert "one process" in rec["config"]["parallelism"] and "x4" in rec["config"]["parallelism"]
