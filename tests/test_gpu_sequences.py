@@ -1,0 +1,137 @@
+"""Random operation sequences on one renderer against the oracle.
+
+The other parity tests fix a short script per handle (reset, a few passes, a
+read); the library, though, carries state from launch to launch: queued
+render() passes fused into one launch at the next observation, the tile
+schedule's flags and the deal kept while they do not change, the completion
+signal, parameter and table changes flushing the queue first. Here each case
+drives one handle through a seeded random sequence of 20-50 operations —
+render, render_passes of 1-40 passes, camera switches between three matrices,
+reset, extinction / bounces / steps / blur changes, a new TF, light or bin
+layout, and reads — with the oracle mirroring every operation in the same
+order; every read compares the photons (and, after a pass, both images) bit
+for bit. VPTMCM_SEQ_CASES / VPTMCM_SEQ_BASE: a longer campaign over fresh
+sequences (tools/fuzz_campaign.sh runs them with the random-configuration
+tests)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as orc
+import vptmcm
+from vptmcm import configs as cf
+from test_gpu_fuzz import _perspective_inverse, _spectrum, _tf, _volume
+from test_gpu_parity import assert_photons_equal, assert_rgb32_equal, assert_rgba_equal
+
+pytestmark = pytest.mark.gpu
+
+N_SEQ = int(os.environ.get("VPTMCM_SEQ_CASES", "8"))
+BASE = int(os.environ.get("VPTMCM_SEQ_BASE", "0"))
+_OPS = ["render", "passes", "camera", "reset", "params", "tf", "light", "spectrum", "read"]
+_P = [0.22, 0.2, 0.12, 0.06, 0.1, 0.05, 0.05, 0.05, 0.15]
+
+
+def _light(rng):
+    iso = rng.random() < 0.2
+    ld = np.zeros(3, np.float32) if iso else rng.normal(size=3).astype(np.float32)
+    spd = (np.full(256, 100, np.uint8) if rng.random() < 0.5
+           else rng.integers(0, 256, 256, dtype=np.uint8))
+    return spd, ld
+
+
+def _params(rng):
+    ext = float(np.float32(10 ** rng.uniform(-0.3, 2.2)))
+    ext = {0: 0.0}.get(int(rng.integers(0, 25)), ext)
+    return dict(extinction=ext, bounces=int(rng.integers(0, 11)), steps=int(rng.integers(0, 17)),
+                blur=float(np.float32(rng.uniform(0, 0.3))) if rng.random() < 0.15 else 0.0)
+
+
+@pytest.mark.parametrize("k", range(N_SEQ))
+def test_random_operation_sequence_bitexact(k):
+    rng = np.random.default_rng(50000 + BASE + k)
+    R = int(rng.choice([16, 24, 40, 64, 72, 96])) + (int(rng.integers(1, 8)) if rng.random() < 0.25 else 0)
+    layout = int(rng.choice([vptmcm.LAYOUT_LINEAR, vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_BRICK8,
+                             vptmcm.LAYOUT_COLUMN4]))
+    shape = tuple(int(x) for x in rng.integers(8, 64, 3)) if rng.random() < 0.4 else (48, 48, 48)
+    vol = _volume(shape, int(rng.integers(0, 1 << 16)))
+    mvps = [cf.default_mvp_inverse()] + [_perspective_inverse(rng, inside=rng.random() < 0.2)
+                                         for _ in range(2)]
+    seeds = iter(cf.seed_stream(2000, start=5000 * (BASE + k)).tolist())
+    log = [f"case {k}: R={R} layout={layout} vol={shape}"]
+    with vptmcm.Renderer(R, device=0, layout=layout) as gpu:
+        cpu = orc.Oracle(R)
+        _, spec = _spectrum(rng)
+        _, tf = _tf(rng)
+        spd, ld = _light(rng)
+        params = _params(rng)
+        gpu.set_spectrum(spec)
+        cpu.set_spectrum(spec)
+        gpu.set_volume(vol)
+        cpu.volume = vol
+        gpu.set_material_tf(tf)
+        cpu.tf = tf
+        gpu.set_light(spd, ld)
+        cpu.light, cpu.light_dir = spd, ld
+        gpu.set_params(**params)
+        cpu.params.update(**params)
+        cam = 0
+        s = next(seeds)
+        gpu.reset(mvps[cam], s)
+        cpu.reset(mvps[cam], s, nthreads=16)
+        img = None  # the oracle's last pass images (None right after a reset)
+
+        def check(what):
+            where = " / ".join(log[-6:])
+            assert_photons_equal(gpu.read_photons(), cpu.photons, f"{what}: {where}")
+            if img is not None:
+                assert_rgb32_equal(gpu.read_rgb(), img[0], f"{what}: {where}")
+                assert_rgba_equal(gpu.read_rgba16f(), img[1], f"{what}: {where}")
+
+        for step in range(int(rng.integers(20, 51))):
+            op = _OPS[int(rng.choice(len(_OPS), p=_P))]
+            if op == "render":
+                s = next(seeds)
+                gpu.render(mvps[cam], s)
+                img = cpu.render(mvps[cam], s, nthreads=16)
+                log.append(f"render cam {cam}")
+            elif op == "passes":
+                n = int(rng.integers(1, 41))
+                ss = [next(seeds) for _ in range(n)]
+                gpu.render_passes(mvps[cam], ss)
+                for s in ss:
+                    img = cpu.render(mvps[cam], s, nthreads=16)
+                log.append(f"{n} passes cam {cam}")
+            elif op == "camera":
+                cam = int(rng.integers(0, 3))
+                log.append(f"camera {cam}")
+            elif op == "reset":
+                s = next(seeds)
+                gpu.reset(mvps[cam], s)
+                cpu.reset(mvps[cam], s, nthreads=16)
+                img = None
+                log.append(f"reset cam {cam}")
+            elif op == "params":
+                params = _params(rng)
+                gpu.set_params(**params)
+                cpu.params.update(**params)
+                log.append(f"params {params}")
+            elif op == "tf":
+                what, tf = _tf(rng)
+                gpu.set_material_tf(tf)
+                cpu.tf = tf
+                log.append(f"tf {what}")
+            elif op == "light":
+                spd, ld = _light(rng)
+                gpu.set_light(spd, ld)
+                cpu.light, cpu.light_dir = spd, ld
+                log.append("light")
+            elif op == "spectrum":
+                what, spec = _spectrum(rng)
+                gpu.set_spectrum(spec)
+                cpu.set_spectrum(spec)
+                log.append(f"spectrum {what}")
+            else:
+                check(f"step {step}")
+                log.append("read")
+        check("end")
