@@ -135,3 +135,112 @@ def test_random_operation_sequence_bitexact(k):
                 check(f"step {step}")
                 log.append("read")
         check("end")
+
+
+def _replica_seed(s: int, j: int) -> int:
+    """vptmcm.cpp replica_seed: replica j's seed bits for replica 0's s."""
+    return s if j == 0 else cf.pcg((s ^ ((j * 0x9E3779B9) & 0xFFFFFFFF)) & 0xFFFFFFFF)
+
+
+@pytest.mark.parametrize("k", range(max(1, N_SEQ // 2)))
+def test_random_group_sequence_bitexact(k):
+    """The same random sequences through a device-list handle of 2-4 replicas
+    on device 0 (worker threads forwarding every call, replica j on its own
+    seed stream), with explicit composites among the operations: every read
+    compares replica 0's photons and the composite's fp32 and rgba16float
+    images and sample counts with oracle replicas composited in replica order."""
+    from test_gpu_group import _composite
+    rng = np.random.default_rng(70000 + BASE + k)
+    n_rep = int(rng.integers(2, 5))
+    R = int(rng.choice([16, 24, 40, 64])) + (int(rng.integers(1, 8)) if rng.random() < 0.25 else 0)
+    layout = int(rng.choice([vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_COLUMN4, vptmcm.LAYOUT_BRICK8]))
+    vol = _volume((48, 48, 48), int(rng.integers(0, 1 << 16)))
+    mvps = [cf.default_mvp_inverse()] + [_perspective_inverse(rng) for _ in range(2)]
+    seeds = iter(cf.seed_stream(2000, start=5000 * (BASE + k) + 17).tolist())
+    log = [f"group case {k}: x{n_rep} R={R} layout={layout}"]
+    with vptmcm.Renderer(R, devices=[0] * n_rep, layout=layout) as g:
+        cpus = [orc.Oracle(R) for _ in range(n_rep)]
+        _, spec = _spectrum(rng)
+        _, tf = _tf(rng)
+        spd, ld = _light(rng)
+        params = _params(rng)
+        g.set_spectrum(spec)
+        g.set_volume(vol)
+        g.set_material_tf(tf)
+        g.set_light(spd, ld)
+        g.set_params(**params)
+        for c in cpus:
+            c.set_spectrum(spec)
+            c.volume, c.tf, c.light, c.light_dir = vol, tf, spd, ld
+            c.params.update(**params)
+        cam = 0
+
+        def each(fn):
+            return [fn(j, c) for j, c in enumerate(cpus)]
+
+        s = next(seeds)
+        g.reset(mvps[cam], s)
+        each(lambda j, c: c.reset(mvps[cam], _replica_seed(s, j), nthreads=16))
+        imgs = None
+
+        def check(what):
+            where = " / ".join(log[-6:])
+            assert_photons_equal(g.read_photons(), cpus[0].photons, f"{what}: {where}")
+            if imgs is not None:
+                want_rgb, want_rgba, want_n = _composite([(c, im[0]) for c, im in zip(cpus, imgs)])
+                q, rgb, n = g.read_composite_all()
+                assert np.array_equal(n, want_n), f"{what} counts: {where}"
+                assert_rgb32_equal(rgb, want_rgb, f"{what}: {where}")
+                assert_rgba_equal(q, want_rgba, f"{what}: {where}")
+
+        for step in range(int(rng.integers(15, 36))):
+            op = _OPS[int(rng.choice(len(_OPS), p=_P))]
+            if op == "render":
+                s = next(seeds)
+                g.render(mvps[cam], s)
+                imgs = each(lambda j, c: c.render(mvps[cam], _replica_seed(s, j), nthreads=16))
+                log.append(f"render cam {cam}")
+            elif op == "passes":
+                ss = [next(seeds) for _ in range(int(rng.integers(1, 41)))]
+                g.render_passes(mvps[cam], ss)
+                for s in ss:
+                    imgs = each(lambda j, c: c.render(mvps[cam], _replica_seed(s, j), nthreads=16))
+                if rng.random() < 0.3:
+                    g.composite()  # asynchronous, right after the frame
+                log.append(f"{len(ss)} passes cam {cam}")
+            elif op == "camera":
+                cam = int(rng.integers(0, 3))
+                log.append(f"camera {cam}")
+            elif op == "reset":
+                s = next(seeds)
+                g.reset(mvps[cam], s)
+                each(lambda j, c: c.reset(mvps[cam], _replica_seed(s, j), nthreads=16))
+                imgs = None
+                log.append(f"reset cam {cam}")
+            elif op == "params":
+                params = _params(rng)
+                g.set_params(**params)
+                each(lambda j, c: c.params.update(**params))
+                log.append(f"params {params}")
+            elif op == "tf":
+                what, tf = _tf(rng)
+                g.set_material_tf(tf)
+                for c in cpus:
+                    c.tf = tf
+                log.append(f"tf {what}")
+            elif op == "light":
+                spd, ld = _light(rng)
+                g.set_light(spd, ld)
+                for c in cpus:
+                    c.light, c.light_dir = spd, ld
+                log.append("light")
+            elif op == "spectrum":
+                what, spec = _spectrum(rng)
+                g.set_spectrum(spec)
+                for c in cpus:
+                    c.set_spectrum(spec)
+                log.append(f"spectrum {what}")
+            else:
+                check(f"step {step}")
+                log.append("read")
+        check("end")
