@@ -244,3 +244,94 @@ def test_random_group_sequence_bitexact(k):
                 check(f"step {step}")
                 log.append("read")
         check("end")
+
+
+@pytest.mark.parametrize("k", range(max(1, N_SEQ // 2)))
+def test_random_rgb_sequence_bitexact(k):
+    """The RGB sibling ('mcm-compute') through random sequences: render,
+    render_passes, camera switches, reset, extinction / anisotropy / bounces /
+    steps changes, a new rgba8 TF image or environment colour, reads (photon
+    words and the rgba16float image bit for bit, NaN == NaN)."""
+    from test_gpu_fuzz import _same_words
+    rng = np.random.default_rng(90000 + BASE + k)
+    R = int(rng.choice([16, 24, 40, 64])) + (int(rng.integers(1, 8)) if rng.random() < 0.25 else 0)
+    layout = int(rng.choice([vptmcm.LAYOUT_LINEAR, vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_BRICK8,
+                             vptmcm.LAYOUT_COLUMN4]))
+    vol = _volume((48, 48, 48), int(rng.integers(0, 1 << 16)))
+    mvps = [cf.default_mvp_inverse()] + [_perspective_inverse(rng) for _ in range(2)]
+    seeds = iter(cf.seed_stream(2000, start=5000 * (BASE + k) + 29).tolist())
+    log = [f"rgb case {k}: R={R} layout={layout}"]
+
+    def tf_img():
+        return rng.integers(0, 256, (int(rng.integers(1, 4)), int(rng.integers(2, 300)), 4), dtype=np.uint8)
+
+    def rgb_params():
+        p = _params(rng)
+        return dict(extinction=p["extinction"], anisotropy=float(np.float32(rng.uniform(-0.95, 0.95))),
+                    bounces=p["bounces"], steps=p["steps"])
+
+    with vptmcm.Renderer(R, device=0, layout=layout, renderer=vptmcm.RENDERER_RGB) as gpu:
+        cpu = orc.OracleRGB(R)
+        tf, env, params = tf_img(), tuple(int(x) for x in rng.integers(0, 256, 4)), rgb_params()
+        gpu.set_transfer_function(tf)
+        gpu.set_environment(env)
+        gpu.set_volume(vol)
+        gpu.set_params(**params)
+        cpu.volume, cpu.tf, cpu.env = vol, tf, np.array(env, np.uint8)
+        cpu.params.update(**params)
+        cam = 0
+        s = next(seeds)
+        gpu.reset(mvps[cam], s)
+        cpu.reset(mvps[cam], s)
+        want = None
+
+        def check(what):
+            where = " / ".join(log[-6:])
+            ok = _same_words(gpu.read_photons(), cpu.photons)
+            assert ok.all(), f"{what}: {int((~ok).sum())} photon words differ: {where}"
+            if want is not None:
+                assert np.array_equal(gpu.read_rgba16f(), want), f"{what}: image differs: {where}"
+
+        ops = ["render", "passes", "camera", "reset", "params", "tf", "env", "read"]
+        probs = [0.24, 0.22, 0.12, 0.06, 0.1, 0.05, 0.05, 0.16]
+        for step in range(int(rng.integers(15, 41))):
+            op = ops[int(rng.choice(len(ops), p=probs))]
+            if op == "render":
+                s = next(seeds)
+                gpu.render(mvps[cam], s)
+                _, want = cpu.render(mvps[cam], s)
+                log.append(f"render cam {cam}")
+            elif op == "passes":
+                ss = [next(seeds) for _ in range(int(rng.integers(1, 41)))]
+                gpu.render_passes(mvps[cam], ss)
+                for s in ss:
+                    _, want = cpu.render(mvps[cam], s)
+                log.append(f"{len(ss)} passes cam {cam}")
+            elif op == "camera":
+                cam = int(rng.integers(0, 3))
+                log.append(f"camera {cam}")
+            elif op == "reset":
+                s = next(seeds)
+                gpu.reset(mvps[cam], s)
+                cpu.reset(mvps[cam], s)
+                want = None
+                log.append(f"reset cam {cam}")
+            elif op == "params":
+                params = rgb_params()
+                gpu.set_params(**params)
+                cpu.params.update(**params)
+                log.append(f"params {params}")
+            elif op == "tf":
+                tf = tf_img()
+                gpu.set_transfer_function(tf)
+                cpu.tf = tf
+                log.append(f"tf {tf.shape}")
+            elif op == "env":
+                env = tuple(int(x) for x in rng.integers(0, 256, 4))
+                gpu.set_environment(env)
+                cpu.env = np.array(env, np.uint8)
+                log.append(f"env {env}")
+            else:
+                check(f"step {step}")
+                log.append("read")
+        check("end")
