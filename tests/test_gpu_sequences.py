@@ -335,3 +335,112 @@ def test_random_rgb_sequence_bitexact(k):
                 check(f"step {step}")
                 log.append("read")
         check("end")
+
+
+@pytest.mark.parametrize("k", range(max(1, N_SEQ // 2)))
+def test_random_band_sequence_bitexact(k):
+    """Mode B bands changing mid-sequence (vptmcm_set_band: reset and render
+    touch only the band's rows, every other photon is left as it was): random
+    sequences of render, render_passes, camera switches, reset, band changes
+    (whole 8-row tiles, the last band ending at R) and parameter changes; every
+    read compares the whole photon buffer and the rows the last pass rendered
+    with the oracle's row-restricted run."""
+    rng = np.random.default_rng(110000 + BASE + k)
+    R = int(rng.choice([24, 40, 64, 72])) + (int(rng.integers(1, 8)) if rng.random() < 0.3 else 0)
+    layout = int(rng.choice([vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_COLUMN4, vptmcm.LAYOUT_BRICK8]))
+    vol = _volume((48, 48, 48), int(rng.integers(0, 1 << 16)))
+    mvps = [cf.default_mvp_inverse()] + [_perspective_inverse(rng) for _ in range(2)]
+    seeds = iter(cf.seed_stream(2000, start=5000 * (BASE + k) + 41).tolist())
+    tiles = (R + 7) // 8
+    log = [f"band case {k}: R={R} layout={layout}"]
+
+    def new_band():
+        if rng.random() < 0.2:
+            return 0, R
+        a = int(rng.integers(0, tiles))
+        b = int(rng.integers(a + 1, tiles + 1))
+        return 8 * a, min(R, 8 * b)
+
+    with vptmcm.Renderer(R, device=0, layout=layout) as gpu:
+        cpu = orc.Oracle(R)
+        _, spec = _spectrum(rng)
+        _, tf = _tf(rng)
+        spd, ld = _light(rng)
+        params = _params(rng)
+        gpu.set_spectrum(spec)
+        cpu.set_spectrum(spec)
+        gpu.set_volume(vol)
+        cpu.volume = vol
+        gpu.set_material_tf(tf)
+        cpu.tf = tf
+        gpu.set_light(spd, ld)
+        cpu.light, cpu.light_dir = spd, ld
+        gpu.set_params(**params)
+        cpu.params.update(**params)
+        band = (0, R)
+        cam = 0
+
+        def reset_both(s):
+            gpu.reset(mvps[cam], s)
+            keep = cpu.photons.copy()
+            cpu.reset(mvps[cam], s, nthreads=16)
+            rows = np.zeros((R, R), bool)
+            rows[band[0]:band[1]] = True
+            cpu.photons[~rows.reshape(-1)] = keep[~rows.reshape(-1)]
+
+        reset_both(next(seeds))
+        img = None
+        # per image row: 1 = the last pass's row (compare with img), 2 = zero
+        # (fp32 rows outside a band set since), 0 = not modelled (an older pass)
+        fp_rows = np.zeros(R, np.int8)
+        q_rows = np.zeros(R, bool)  # rgba16f rows of the last pass (band changes leave them)
+
+        def check(what):
+            where = " / ".join(log[-6:])
+            assert_photons_equal(gpu.read_photons(), cpu.photons, f"{what}: {where}")
+            got = gpu.read_rgb()
+            assert not got[fp_rows == 2].any(), f"{what}: fp32 rows zeroed by a band change: {where}"
+            if img is not None:
+                assert_rgb32_equal(got[fp_rows == 1], img[0][fp_rows == 1], f"{what}: {where}")
+                assert_rgba_equal(gpu.read_rgba16f()[q_rows], img[1][q_rows], f"{what}: {where}")
+
+        ops = ["render", "passes", "camera", "reset", "band", "params", "read"]
+        probs = [0.22, 0.2, 0.1, 0.1, 0.13, 0.08, 0.17]
+        for step in range(int(rng.integers(15, 41))):
+            op = ops[int(rng.choice(len(ops), p=probs))]
+            if op in ("render", "passes"):
+                ss = ([next(seeds)] if op == "render"
+                      else [next(seeds) for _ in range(int(rng.integers(1, 41)))])
+                if op == "render":
+                    gpu.render(mvps[cam], ss[0])
+                else:
+                    gpu.render_passes(mvps[cam], ss)
+                for s in ss:
+                    img = cpu.render(mvps[cam], s, nthreads=16, rows=band)
+                fp_rows[fp_rows == 1] = 0
+                fp_rows[band[0]:band[1]] = 1
+                q_rows[:] = False
+                q_rows[band[0]:band[1]] = True
+                log.append(f"{len(ss)} pass(es) cam {cam} band {band}")
+            elif op == "camera":
+                cam = int(rng.integers(0, 3))
+                log.append(f"camera {cam}")
+            elif op == "reset":
+                reset_both(next(seeds))
+                img = None
+                log.append(f"reset cam {cam} band {band}")
+            elif op == "band":
+                band = new_band()
+                gpu.set_band(*band)
+                fp_rows[:band[0]] = 2
+                fp_rows[band[1]:] = 2
+                log.append(f"band {band}")
+            elif op == "params":
+                params = _params(rng)
+                gpu.set_params(**params)
+                cpu.params.update(**params)
+                log.append(f"params {params}")
+            else:
+                check(f"step {step}")
+                log.append("read")
+        check("end")
