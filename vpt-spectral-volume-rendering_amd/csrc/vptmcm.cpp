@@ -48,8 +48,9 @@ struct ReplicaJob {
 // forwarded operation (ingest, render_passes, reset, the composite's pack and
 // push, synchronize) runs on all replicas at once, each replica's host work
 // and enqueue on its own thread, instead of one replica after another from the
-// caller's thread. Posting is a counter bump; an idle worker spins for the
-// handle's sync_spin_us and then sleeps on the condition variable.
+// caller's thread. Posting is a counter bump; an idle worker spins for up to
+// 200 us (the handle's sync_spin_us if shorter) and then sleeps on the
+// condition variable.
 struct ReplicaWorker {
   vptmcm* c = nullptr;
   std::thread th;
@@ -858,7 +859,10 @@ void start_workers(vptmcm* h) {
     for (vptmcm* c : h->peers) {
       auto w = std::make_unique<ReplicaWorker>();
       w->c = c;
-      w->spin_us = std::max<int64_t>(h->sync_spin_us, 0);
+      // an idle worker spins briefly (back-to-back forwarded calls: render_passes
+      // then synchronize) and then sleeps, so a display loop does not keep N
+      // cores busy between frames
+      w->spin_us = std::min<int64_t>(std::max<int64_t>(h->sync_spin_us, 0), 200);
       w->th = std::thread(worker_main, w.get());
       h->workers.push_back(std::move(w));
     }
