@@ -823,7 +823,12 @@ void worker_main(ReplicaWorker* w) {
       }
     }
     seen = p;
-    w->rc = w->job.call(w->job.f, w->c);
+    try {
+      w->rc = w->job.call(w->job.f, w->c);
+    } catch (...) {  // nothing may escape a thread (std::terminate)
+      w->c->err = "internal: exception in a replica's worker thread";
+      w->rc = VPTMCM_ENOMEM;
+    }
     w->finished.store(seen, std::memory_order_release);
   }
 }
@@ -1056,8 +1061,13 @@ static int create_group(const vptmcm_config* cfg, vptmcm** out) {
     vptmcm_config one = *cfg;
     one.n_devices = 0;
     one.device = cfg->devices[k];
-    made[k].rc = vptmcm_create(&one, &made[k].h);
-    if (made[k].rc) made[k].err = g_create_error;  // thread-local: copied out here
+    try {
+      made[k].rc = vptmcm_create(&one, &made[k].h);
+      if (made[k].rc) made[k].err = g_create_error;  // thread-local: copied out here
+    } catch (...) {  // nothing may escape a thread (std::terminate)
+      made[k].rc = VPTMCM_ENOMEM;
+      made[k].err = "vptmcm_create: out of host memory";
+    }
   };
   std::vector<std::thread> makers;
   for (uint32_t k = 1; k < n; k++) {
