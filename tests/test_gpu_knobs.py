@@ -29,10 +29,18 @@ KNOBS = [("VPTMCM_MARCH_VARIANT", str(b)) for b in (1, 2, 4, 8, 16, 32, 64, 128)
 ]
 
 
-def _run(layout, tf, spec, with_oracle=False):
+def _run(layout, tf, spec, with_oracle=False, devices=None):
     R = 64
     vol = cf.fbm_volume(48, 21, nthreads=8)
     gpu, cpu = make_pair(R, vol, tf, spec=spec, ext=24.0, layout=layout)
+    if devices is not None:  # the same inputs behind a device-list handle
+        gpu.close()
+        gpu = vptmcm.Renderer(R, layout=layout, devices=devices)
+        gpu.set_spectrum(cf.spectrum_buffer(spec))
+        gpu.set_volume(vol)
+        gpu.set_material_tf(tf)
+        gpu.set_light(cpu.light, cpu.light_dir)
+        gpu.set_params(extinction=24.0, bounces=8, steps=8)
     m1, m2 = cf.golden_mvp("orbit"), cf.default_mvp_inverse()
     seeds = cf.seed_stream(14, start=3)
     gpu.enable_kernel_timing(True)
@@ -57,7 +65,8 @@ def _run(layout, tf, spec, with_oracle=False):
     return got
 
 
-@pytest.mark.parametrize("layout,tfname,spec", [(vptmcm.LAYOUT_CORNER8, "spectral", "12"),
+@pytest.mark.parametrize("layout,tfname,spec", [(vptmcm.LAYOUT_COLUMN4, "spectral", "12"),
+                                                (vptmcm.LAYOUT_CORNER8, "spectral", "12"),
                                                 (vptmcm.LAYOUT_BRICK8, "materials", "8_uneven")])
 def test_every_knob_leaves_the_bits(layout, tfname, spec, monkeypatch):
     tf = cf.tf_spectral() if tfname == "spectral" else cf.tf_materials(True)
@@ -69,6 +78,31 @@ def test_every_knob_leaves_the_bits(layout, tfname, spec, monkeypatch):
         got = _run(layout, tf, spec)
         monkeypatch.delenv(var)
         what = f"{var}={val}"
+        assert_photons_equal(got[0], base[0], what)
+        assert_rgb32_equal(got[1], base[1], what)
+        assert_rgba_equal(got[2], base[2], what)
+
+
+def test_every_knob_leaves_the_bits_device_list(monkeypatch):
+    """The same sweep on a device-list handle of three replicas (device 0
+    repeated; the default COLUMN4 layout and PEER transport), with
+    VPTMCM_GROUP_THREADS=0 (serial forwarding) among the knobs: replica 0's
+    photons, the composite's fp32 and rgba16f images equal the knob-free run's.
+    Replica 0's photons also equal the single-device handle's (the knob-free
+    single run is pinned to the oracle above)."""
+    tf = cf.tf_spectral()
+    knobs = KNOBS + [("VPTMCM_GROUP_THREADS", "0")]
+    for var, _ in knobs:
+        monkeypatch.delenv(var, raising=False)
+    single = _run(vptmcm.LAYOUT_COLUMN4, tf, "12", with_oracle=True)
+    base = _run(vptmcm.LAYOUT_COLUMN4, tf, "12", devices=[0, 0, 0])
+    assert_photons_equal(base[0], single[0], "device list replica 0 vs single handle")
+    assert not np.array_equal(base[2], single[2])  # the target is the 3-replica composite
+    for var, val in knobs:
+        monkeypatch.setenv(var, val)
+        got = _run(vptmcm.LAYOUT_COLUMN4, tf, "12", devices=[0, 0, 0])
+        monkeypatch.delenv(var)
+        what = f"device list, {var}={val}"
         assert_photons_equal(got[0], base[0], what)
         assert_rgb32_equal(got[1], base[1], what)
         assert_rgba_equal(got[2], base[2], what)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-segment cycle breakdown of the march's volume steps (experiment build).
 
-Runs the bench workload (C3) on lib/libvptmcm_<variant>.so built with
+Runs the bench workload (C3) on build/variants/libvptmcm_<variant>.so built with
 -DVPT_STAMP=1 (tools/variants.py stamp='-DVPT_STAMP=1'), settles the clock with
 fused launches, then runs ONE one-pass launch whose waves write their
 s_memtime segment sums into the fp32 image buffer (tile * 8 + k, see k_march).

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Timeline of a march launch, per wave (experiment build, never the product).
 
-Runs the bench workload (C3) on lib/libvptmcm_<variant>.so built with
+Runs the bench workload (C3) on build/variants/libvptmcm_<variant>.so built with
 -DVPT_STAMP=2 (tools/variants.py tl='-DVPT_STAMP=2'): every wave writes the
 100 MHz s_memrealtime at five points of the launch into the fp32 image buffer
 (csrc/stamp.h): entry, tile scheduled, LDS filled + photon state resident, pass

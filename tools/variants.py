@@ -3,7 +3,7 @@
 
     python tools/variants.py name1='-DFOO=1' name2='-fno-slp-vectorize' ...
 
-Each variant is lib/libvptmcm_<name>.so, compiled from the same sources as the
+Each variant is build/variants/libvptmcm_<name>.so (outside the shipped package), compiled from the same sources as the
 product with the extra flags appended; bench.py / tests select one with
 VPTMCM_LIB=<name> (tools/sweep.sh lines 'VPTMCM_LIB=<name>;<bench args>').
 Variants are experiments only: the product library is always libvptmcm.so.
@@ -20,7 +20,7 @@ import build as B  # noqa: E402
 
 def one(spec: str) -> Path:
     name, _, flags = spec.partition("=")
-    out = B.LIB / f"libvptmcm_{name}.so"
+    out = B.VARIANTS / f"libvptmcm_{name}.so"
     srcs = [B.CSRC / "kernels.hip", B.CSRC / "vptmcm.cpp"]
     B._run(["/opt/rocm/bin/hipcc", *B.HIP_FLAGS, *shlex.split(flags), "-shared",
             f"-I{REPO / 'include'}", *srcs, "-o", out, "-lrccl", f"-L{B.ROCM / 'lib'}",
@@ -29,7 +29,7 @@ def one(spec: str) -> Path:
 
 
 if __name__ == "__main__":
-    B.LIB.mkdir(parents=True, exist_ok=True)
+    B.VARIANTS.mkdir(parents=True, exist_ok=True)
     with ThreadPoolExecutor(4) as ex:
         for p in ex.map(one, sys.argv[1:]):
             print(p)

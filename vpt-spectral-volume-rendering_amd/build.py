@@ -19,6 +19,8 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 REPO = PKG.parent
 LIB = PKG / "lib"
+# tools/variants.py A/B builds: outside the package, so lib/ holds the product only
+VARIANTS = REPO / "build" / "variants"
 CSRC = PKG / "csrc"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = "gfx950"
@@ -92,7 +94,16 @@ def build_oracle(force: bool = False) -> Path:
     return odir / "liboracle.so"
 
 
+def clean_stale_variants() -> None:
+    """lib/ holds the product library only: A/B builds that older rounds left
+    there (libvptmcm_<name>.so) are removed (variants now live in build/variants/)."""
+    for p in LIB.glob("libvptmcm_*.so"):
+        print(f"remove stale variant {p}", flush=True)
+        p.unlink()
+
+
 def build_all(force: bool = False) -> None:
+    clean_stale_variants()
     build_hip(force)
     build_synth(force)
     build_napi(force)

@@ -28,6 +28,10 @@
 #include "../../include/vptmcm.h"
 #include "kernels.h"
 
+#ifndef VPT_STAMP
+#define VPT_STAMP 0  // measurement builds (csrc/stamp.h) set it for both sources
+#endif
+
 using namespace vpt;
 
 namespace {
@@ -154,6 +158,17 @@ struct vptmcm {
   // buffer without a k_pack launch.
   bool pack_fresh = false;
   MarchLaunchInfo last_launch{};
+  // The camera's robust-miss region (robust_region: a double-precision matrix
+  // inverse and the projected hull) for the last matrix seen: a progressive
+  // renderer re-sends one camera every pass, so launches reuse it instead of
+  // recomputing it (keyed on the matrix bits and 1/R, the only inputs).
+  struct RobustCache {
+    bool valid = false, ok = false;
+    float m[16];
+    float ir = 0.0f;
+    float rb[4];
+    float edge[kRbEdges][3];
+  } robust_cache;
 
   // multi-GPU
   ncclComm_t comm = nullptr;
@@ -347,7 +362,23 @@ bool robust_region(const float* m32, float ir, float rb[4], float (*edge)[3]) {
 // Uniform preparation shared by render and reset (wgsl:8-18, js:295-312).
 // Everything derived here is computed in IEEE f32 exactly as the kernel
 // would compute it per lane (host SSE arithmetic, no contraction).
-MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
+// robust_region of (mvp, ir) through the handle's one-entry cache.
+bool robust_cached(vptmcm* h, const float* mvp, float ir, float rb[4], float (*edge)[3]) {
+  if (mvp == kNoMatrix) return robust_region(mvp, ir, rb, edge);  // the packs' launches: keep the camera's entry
+  auto& c = h->robust_cache;
+  if (!c.valid || memcmp(c.m, mvp, sizeof c.m) != 0 || memcmp(&c.ir, &ir, sizeof ir) != 0) {
+    c.valid = false;
+    c.ok = robust_region(mvp, ir, c.rb, c.edge);
+    memcpy(c.m, mvp, sizeof c.m);
+    c.ir = ir;
+    c.valid = true;
+  }
+  memcpy(rb, c.rb, sizeof c.rb);
+  memcpy(edge, c.edge, sizeof c.edge);
+  return c.ok;
+}
+
+MarchParams make_params(vptmcm* h, const float* mvp, uint32_t seed) {
   MarchParams P;
   memset(&P, 0, sizeof P);
   memcpy(P.m, mvp, sizeof P.m);
@@ -426,7 +457,7 @@ MarchParams make_params(const vptmcm* h, const float* mvp, uint32_t seed) {
   for (int k = 0; k < 4; k++) P.env[k] = h->env[k];
   float rb[4];
   P.robust = (P.blur == 0.0f && P.rcp_extinction > 0.0f && std::isfinite(P.rcp_extinction) &&
-              robust_region(mvp, P.inv_res[0], rb, P.rb_edge)) ? 1u : 0u;
+              robust_cached(h, mvp, P.inv_res[0], rb, P.rb_edge)) ? 1u : 0u;
   if (!P.robust)
     for (int e = 0; e < kRbEdges; e++) P.rb_edge[e][0] = P.rb_edge[e][1] = 0.0f, P.rb_edge[e][2] = FLT_MAX;
   if (P.robust) {
@@ -470,6 +501,15 @@ int check_handle(vptmcm* h) { return h ? VPTMCM_OK : VPTMCM_EINVAL; }
 void stream_op(vptmcm* h) {
   h->done_pending = false;
   h->pack_fresh = false;
+}
+
+// The handle's stream for enqueueing anything but the march itself: every
+// such enqueue names the stream through this helper, so the completion flag
+// and the packed composite buffer can only stand while a march really is the
+// stream's last work (the march launch in do_march is the one raw use).
+hipStream_t enq(vptmcm* h) {
+  stream_op(h);
+  return h->stream;
 }
 
 // MarchParams::bins_lut (march MODE 6 / 7): the wavelength bin as a step
@@ -540,7 +580,7 @@ int build_bin_lut(vptmcm* h) {
   for (uint64_t v = 0; v < (1ull << 32); v += 0x10001ull)
     if (lut_bin(v) != bin_rule(v)) return VPTMCM_OK;
   HIPCHK(h, hipMemcpyAsync(h->bin_lut, h->bin_lut_host, sizeof h->bin_lut_host,
-                           hipMemcpyHostToDevice, h->stream));
+                           hipMemcpyHostToDevice, enq(h)));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->bin_lut_ok = true;
   return VPTMCM_OK;
@@ -556,7 +596,7 @@ int time_slot(vptmcm* h, hipEvent_t* beg) {
     HIPCHK(h, hipEventCreateWithFlags(&h->region.end, hipEventDisableSystemFence));
   }
   if (h->launches++ == 0) {
-    if (h->time_begin_marker) HIPCHK(h, hipEventRecord(h->region.beg, h->stream));
+    if (h->time_begin_marker) HIPCHK(h, hipEventRecord(h->region.beg, enq(h)));
     else *beg = h->region.beg;
   }
   h->region_closed = false;
@@ -570,7 +610,7 @@ int time_close(vptmcm* h) {
     h->region_closed = true;
     return VPTMCM_OK;
   }
-  HIPCHK(h, hipEventRecord(h->region.end, h->stream));
+  HIPCHK(h, hipEventRecord(h->region.end, enq(h)));
   h->region_closed = true;
   stream_op(h);  // work behind the signalling march
   return VPTMCM_OK;
@@ -588,11 +628,11 @@ int flush_relayout(vptmcm* h) {
     // quads [z0, z1 + 1), clipped to the column's D + 2
     const uint32_t z1 = std::min(h->vol_c1[2] + 1u, h->D + 2u);
     const uint32_t nq[3] = {n[0], n[1], z1 - h->vol_c0[2]};
-    HIPCHK(h, launch_column4(h->vol_lin, h->W, h->H, h->D, h->vol_c8, h->stream, h->vol_c0, nq));
+    HIPCHK(h, launch_column4(h->vol_lin, h->W, h->H, h->D, h->vol_c8, enq(h), h->vol_c0, nq));
     return VPTMCM_OK;
   }
   HIPCHK(h, launch_corner8(h->vol_lin, h->W, h->H, h->D, brick ? (h->W + kBrickCells) / kBrickCells : 0u,
-                           brick ? (h->H + kBrickCells) / kBrickCells : 0u, h->vol_c8, h->stream,
+                           brick ? (h->H + kBrickCells) / kBrickCells : 0u, h->vol_c8, enq(h),
                            h->vol_c0, n));
   return VPTMCM_OK;
 }
@@ -622,9 +662,12 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   P.launch_seq = (uint32_t)(h->march_launches + 1u);
   P.sched_reuse = (h->sched_cache && h->march_launches > 0u) ? 1u : 0u;
   const bool signal = h->done_on && h->kind == VPTMCM_RENDERER_SPECTRAL;
-  const bool pack = h->comm && h->kind == VPTMCM_RENDERER_SPECTRAL && h->band_y0 == 0 && h->band_y1 == h->R;
+  // (measurement builds, VPT_STAMP != 0, store neither rgb32 nor the pack: the
+  // all-reduce then runs k_pack, whose inputs are as invalid as those builds' results)
+  const bool pack = !VPT_STAMP && h->comm && h->kind == VPTMCM_RENDERER_SPECTRAL && h->band_y0 == 0 &&
+                    h->band_y1 == h->R;
   if (pack) {  // the buffer is free once the all-reduce issued two composites ago is done
-    HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[h->comp_next], 0));
+    HIPCHK(h, hipStreamWaitEvent(enq(h), h->comp_done[h->comp_next], 0));
     T.pack = h->comp[h->comp_next];
   }
   if (signal) {  // every block of the grid counts once (committed below, once launched)
@@ -891,7 +934,10 @@ void stop_workers(vptmcm* h) {
 
 // A peer's failure is reported on h, naming the replica.
 int peer_failed(vptmcm* h, const vptmcm* c, int rc) {
-  h->err = "replica " + std::to_string(c->replica) + " (device " + std::to_string(c->device) + "): " + c->err;
+  try {
+    h->err = "replica " + std::to_string(c->replica) + " (device " + std::to_string(c->device) + "): " + c->err;
+  } catch (...) {  // out of host memory for the message: the code still says what failed
+  }
   return rc;
 }
 
@@ -900,20 +946,34 @@ int peer_failed(vptmcm* h, const vptmcm* c, int rc) {
 // the caller's thread, all at once, or one after another without workers. The
 // operation must touch only its own replica (and read shared inputs). Every
 // replica runs it; the first failure in replica order is the result.
+// f runs under a catch-all on every thread: an exception (std::bad_alloc from
+// an error message's formatting) becomes an error code instead of unwinding
+// the caller's stack while workers still call through &f, or escaping through
+// the C ABI; every worker is awaited before this returns.
+template <class F>
+int guarded(vptmcm* c, const F& f) {
+  try {
+    return f(c);
+  } catch (...) {
+    c->err = "internal: exception in a forwarded operation";
+    return VPTMCM_ENOMEM;
+  }
+}
+
 template <class F>
 int run_replicas(vptmcm* h, bool self, const F& f) {
   if (h->workers.empty()) {
     if (self)
-      if (int rc = f(h)) return rc;
+      if (int rc = guarded(h, f)) return rc;
     for (vptmcm* c : h->peers)
-      if (int rc = f(c)) return peer_failed(h, c, rc);
+      if (int rc = guarded(c, f)) return peer_failed(h, c, rc);
     return VPTMCM_OK;
   }
   ReplicaJob job;
   job.call = [](const void* p, vptmcm* c) { return (*static_cast<const F*>(p))(c); };
   job.f = &f;
   for (auto& w : h->workers) post(w.get(), job);
-  const int rc0 = self ? f(h) : VPTMCM_OK;
+  const int rc0 = self ? guarded(h, f) : VPTMCM_OK;
   int first = VPTMCM_OK;
   const vptmcm* bad = nullptr;
   for (auto& w : h->workers) {
@@ -979,11 +1039,11 @@ static int group_alloc(vptmcm* h, const int32_t* devs, uint32_t n) {
   const size_t slots = h->group_transport == VPTMCM_GROUP_RCCL ? 1 : n - 1;
   if (slots) HIPCHK(h, hipMalloc(&h->grp_gather, slots * npx * sizeof(float4)));
   HIPCHK(h, hipMalloc(&h->grp_rgb32, npx * 3 * sizeof(float)));
-  HIPCHK(h, hipMemsetAsync(h->grp_rgb32, 0, npx * 3 * sizeof(float), h->stream));
+  HIPCHK(h, hipMemsetAsync(h->grp_rgb32, 0, npx * 3 * sizeof(float), enq(h)));
   HIPCHK(h, hipMalloc(&h->grp_rgba, npx * 4 * sizeof(uint16_t)));
-  HIPCHK(h, hipMemsetAsync(h->grp_rgba, 0, npx * 4 * sizeof(uint16_t), h->stream));
+  HIPCHK(h, hipMemsetAsync(h->grp_rgba, 0, npx * 4 * sizeof(uint16_t), enq(h)));
   HIPCHK(h, hipEventCreateWithFlags(&h->grp_done, hipEventDisableTiming));
-  HIPCHK(h, hipEventRecord(h->grp_done, h->stream));
+  HIPCHK(h, hipEventRecord(h->grp_done, enq(h)));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->group_transport == VPTMCM_GROUP_PEER) {
     // both directions between devices[0] and each peer: the peer's stream
@@ -1127,13 +1187,13 @@ static int group_composite(vptmcm* h) {
     HIPCHK(c, hipSetDevice(c->device));
     stream_op(c);  // the pack follows the march on this stream
     // the last composite has read this replica's pack (and its slot on devices[0])
-    HIPCHK(c, hipStreamWaitEvent(c->stream, h->grp_done, 0));
+    HIPCHK(c, hipStreamWaitEvent(enq(c), h->grp_done, 0));
     const MarchParams P = make_params(c, kNoMatrix, 0);
-    HIPCHK(c, launch_pack(P, c->photons, c->rgb32, c->grp_pack, c->stream));
+    HIPCHK(c, launch_pack(P, c->photons, c->rgb32, c->grp_pack, enq(c)));
     if (peer && c != h)
       HIPCHK(c, hipMemcpyPeerAsync(h->grp_gather + (size_t)(c->replica - 1) * npx, h->device, c->grp_pack,
-                                   c->device, bytes, c->stream));
-    HIPCHK(c, hipEventRecord(c->grp_packed, c->stream));
+                                   c->device, bytes, enq(c)));
+    HIPCHK(c, hipEventRecord(c->grp_packed, enq(c)));
     return VPTMCM_OK;
   });
   if (rc) return rc;
@@ -1145,7 +1205,7 @@ static int group_composite(vptmcm* h) {
     for (uint32_t k = 0; k < n && r == ncclSuccess; k++) {
       vptmcm* c = k ? h->peers[k - 1] : h;
       r = ncclReduce(c->grp_pack, k ? c->grp_pack : h->grp_gather, npx * 4, ncclFloat32, ncclSum, 0,
-                     h->grp_comms[k], c->stream);
+                     h->grp_comms[k], enq(c));
     }
     const ncclResult_t re = ncclGroupEnd();
     if (r != ncclSuccess || re != ncclSuccess)
@@ -1158,12 +1218,12 @@ static int group_composite(vptmcm* h) {
     S.n = n;
     S.p[0] = h->grp_pack;
     for (uint32_t k = 1; k < n; k++) {  // every peer's push has landed
-      HIPCHK(h, hipStreamWaitEvent(h->stream, h->peers[k - 1]->grp_packed, 0));
+      HIPCHK(h, hipStreamWaitEvent(enq(h), h->peers[k - 1]->grp_packed, 0));
       S.p[k] = h->grp_gather + (size_t)(k - 1) * npx;
     }
   }
-  HIPCHK(h, launch_composite(S, (uint32_t)npx, h->grp_rgb32, h->grp_rgba, nullptr, h->stream));
-  HIPCHK(h, hipEventRecord(h->grp_done, h->stream));
+  HIPCHK(h, launch_composite(S, (uint32_t)npx, h->grp_rgb32, h->grp_rgba, nullptr, enq(h)));
+  HIPCHK(h, hipEventRecord(h->grp_done, enq(h)));
   h->grp_dirty = false;
   return VPTMCM_OK;
 }
@@ -1243,37 +1303,37 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   } while (0)
   CK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   CK(hipMalloc(&h->photons, (size_t)kNumPlanes * h->npad * sizeof(float)));
-  CK(hipMemsetAsync(h->photons, 0, (size_t)kNumPlanes * h->npad * sizeof(float), h->stream));
+  CK(hipMemsetAsync(h->photons, 0, (size_t)kNumPlanes * h->npad * sizeof(float), enq(h)));
   CK(hipMalloc(&h->rgba, (size_t)h->R * h->R * 4 * sizeof(uint16_t)));
-  CK(hipMemsetAsync(h->rgba, 0, (size_t)h->R * h->R * 4 * sizeof(uint16_t), h->stream));
+  CK(hipMemsetAsync(h->rgba, 0, (size_t)h->R * h->R * 4 * sizeof(uint16_t), enq(h)));
   CK(hipMalloc(&h->rgb32, (size_t)h->R * h->R * 3 * sizeof(float)));
-  CK(hipMemsetAsync(h->rgb32, 0, (size_t)h->R * h->R * 3 * sizeof(float), h->stream));
+  CK(hipMemsetAsync(h->rgb32, 0, (size_t)h->R * h->R * 3 * sizeof(float), enq(h)));
   CK(hipMalloc(&h->tf_rg, 65536 * sizeof(uint16_t)));
-  CK(hipMemsetAsync(h->tf_rg, 0, 65536 * sizeof(uint16_t), h->stream));  // zero texture, js:85
+  CK(hipMemsetAsync(h->tf_rg, 0, 65536 * sizeof(uint16_t), enq(h)));  // zero texture, js:85
   CK(hipMalloc(&h->tf_b4, kTfCells * kTfCells * sizeof(uint32_t)));
-  CK(hipMemsetAsync(h->tf_b4, 0, kTfCells * kTfCells * sizeof(uint32_t), h->stream));
+  CK(hipMemsetAsync(h->tf_b4, 0, kTfCells * kTfCells * sizeof(uint32_t), enq(h)));
   CK(hipMalloc(&h->tf_brow, 256));
-  CK(hipMemsetAsync(h->tf_brow, 0, 256, h->stream));
+  CK(hipMemsetAsync(h->tf_brow, 0, 256, enq(h)));
   CK(hipMalloc(&h->tf_rows, kTfRowsMax * 256 * sizeof(uint32_t)));
-  CK(hipMemsetAsync(h->tf_rows, 0, kTfRowsMax * 256 * sizeof(uint32_t), h->stream));
+  CK(hipMemsetAsync(h->tf_rows, 0, kTfRowsMax * 256 * sizeof(uint32_t), enq(h)));
   CK(hipMalloc(&h->bin_lut, sizeof h->bin_lut_host));
-  CK(hipMemsetAsync(h->bin_lut, 0, sizeof h->bin_lut_host, h->stream));
+  CK(hipMemsetAsync(h->bin_lut, 0, sizeof h->bin_lut_host, enq(h)));
   CK(hipMalloc(&h->tf_rowmap, 256));
-  CK(hipMemsetAsync(h->tf_rowmap, 0, 256, h->stream));
+  CK(hipMemsetAsync(h->tf_rowmap, 0, 256, enq(h)));
   CK(hipMalloc(&h->light, 256));
-  CK(hipMemsetAsync(h->light, 0, 256, h->stream));
+  CK(hipMemsetAsync(h->light, 0, 256, enq(h)));
   CK(hipMalloc(&h->tf_rgb, kRgbTfMax * sizeof(float4)));
   CK(hipMalloc(&h->sched, 2 * (size_t)sched_flag_bytes(h->n_tiles)));
-  CK(hipMemsetAsync(h->sched, 0, 2 * (size_t)sched_flag_bytes(h->n_tiles), h->stream));
+  CK(hipMemsetAsync(h->sched, 0, 2 * (size_t)sched_flag_bytes(h->n_tiles), enq(h)));
   CK(hipMalloc(&h->sched_prev, sched_slot_words(h->n_tiles) * sizeof(uint32_t)));
-  CK(hipMemsetAsync(h->sched_prev, 0xff, sched_slot_words(h->n_tiles) * sizeof(uint32_t), h->stream));
+  CK(hipMemsetAsync(h->sched_prev, 0xff, sched_slot_words(h->n_tiles) * sizeof(uint32_t), enq(h)));
   CK(hipMalloc(&h->sched_changed, 2 * sizeof(uint32_t)));
-  CK(hipMemsetAsync(h->sched_changed, 0, 2 * sizeof(uint32_t), h->stream));
+  CK(hipMemsetAsync(h->sched_changed, 0, 2 * sizeof(uint32_t), enq(h)));
   if (const char* v = getenv("VPTMCM_DARK")) h->dark = v[0] == '0' ? 0u : 1u;
   if (const char* v = getenv("VPTMCM_DONE_FLAG")) h->done_on = v[0] != '0';
   if (const char* v = getenv("VPTMCM_SCHED_CACHE")) h->sched_cache = v[0] != '0';
   CK(hipMalloc(&h->done_ctr, sizeof(uint32_t)));
-  CK(hipMemsetAsync(h->done_ctr, 0, sizeof(uint32_t), h->stream));
+  CK(hipMemsetAsync(h->done_ctr, 0, sizeof(uint32_t), enq(h)));
   // the flag word in fine-grained host memory; without it, synchronize waits
   // for the stream (the signal is an optimisation, never a requirement)
   if (hipHostMalloc(&h->done_host, sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped) ==
@@ -1396,7 +1456,7 @@ static int volume_begin_one(vptmcm* h, uint32_t width, uint32_t height, uint32_t
     FAIL(h, VPTMCM_ENOMEM, "volume allocation of %zu bytes failed", n);
   }
   // a fresh texture is zero; the block copies below run on the same stream, after it
-  HIPCHK(h, hipMemsetAsync(h->vol_lin, 0, n, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->vol_lin, 0, n, enq(h)));
   if (h->layout != kLayoutLinear) {
     // CORNER8: (W+1)(H+1)(D+1) cells in raster order; BRICK8: the same cells
     // in 4x4x4-cell bricks (the brick grid rounds each edge up to whole bricks)
@@ -1418,7 +1478,7 @@ static int volume_begin_one(vptmcm* h, uint32_t width, uint32_t height, uint32_t
            brick ? "brick8" : col ? "column4" : "corner8",
            ncell * 8);
     }
-    HIPCHK(h, hipMemsetAsync(h->vol_c8, 0, ncell * 8, h->stream));
+    HIPCHK(h, hipMemsetAsync(h->vol_c8, 0, ncell * 8, enq(h)));
   }
   h->W = width;
   h->H = height;
@@ -1444,7 +1504,7 @@ static int volume_write_block_one(vptmcm* h, const uint8_t* data, uint32_t x, ui
   // returning (the caller keeps the block buffer).
   if (bw == h->W && bh == h->H && x == 0 && y == 0) {  // whole slices: one contiguous copy
     HIPCHK(h, hipMemcpyAsync(h->vol_lin + (size_t)z * h->W * h->H, data, (size_t)bw * bh * bd,
-                             hipMemcpyHostToDevice, h->stream));
+                             hipMemcpyHostToDevice, enq(h)));
   } else {
     hipMemcpy3DParms p;
     memset(&p, 0, sizeof p);
@@ -1453,7 +1513,7 @@ static int volume_write_block_one(vptmcm* h, const uint8_t* data, uint32_t x, ui
     p.dstPos = make_hipPos(x, y, z);
     p.extent = make_hipExtent(bw, bh, bd);
     p.kind = hipMemcpyHostToDevice;
-    HIPCHK(h, hipMemcpy3DAsync(&p, h->stream));
+    HIPCHK(h, hipMemcpy3DAsync(&p, enq(h)));
   }
   if (h->layout != kLayoutLinear) {
     // the cells whose 8 corners include a voxel of the block, x .. x + bw per
@@ -1516,8 +1576,8 @@ static int set_material_tf_one(vptmcm* h, const uint8_t* rgba) {
       b4[(size_t)cr * kTfCells + cc] =
           bch(r0, c0) | (bch(r0, c1) << 8) | (bch(r1, c0) << 16) | (bch(r1, c1) << 24);
     }
-  HIPCHK(h, hipMemcpyAsync(h->tf_rg, rg.data(), rg.size() * 2, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(h->tf_b4, b4.data(), b4.size() * 4, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->tf_rg, rg.data(), rg.size() * 2, hipMemcpyHostToDevice, enq(h)));
+  HIPCHK(h, hipMemcpyAsync(h->tf_b4, b4.data(), b4.size() * 4, hipMemcpyHostToDevice, enq(h)));
   // column-invariant anisotropy (the UI's per-material constant case): exact row table
   uint8_t brow[256];
   uint32_t inv = 1;
@@ -1526,7 +1586,7 @@ static int set_material_tf_one(vptmcm* h, const uint8_t* rgba) {
     for (int c = 1; c < 256 && inv; c++)
       if (bch(r, c) != brow[r]) inv = 0;
   }
-  HIPCHK(h, hipMemcpyAsync(h->tf_brow, brow, 256, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->tf_brow, brow, 256, hipMemcpyHostToDevice, enq(h)));
   h->b_rows = inv;
   // Distinct density rows over (albedo, alpha, anisotropy): a UI TF paints one
   // material's wavelength arrays into every row of a density range
@@ -1556,8 +1616,8 @@ static int set_material_tf_one(vptmcm* h, const uint8_t* rgba) {
   h->tf_dedup = n_rows <= kTfRowsMax ? 1u : 0u;
   if (h->tf_dedup) {
     HIPCHK(h, hipMemcpyAsync(h->tf_rows, rows.data(), rows.size() * sizeof(uint32_t),
-                             hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipMemcpyAsync(h->tf_rowmap, rowmap, 256, hipMemcpyHostToDevice, h->stream));
+                             hipMemcpyHostToDevice, enq(h)));
+    HIPCHK(h, hipMemcpyAsync(h->tf_rowmap, rowmap, 256, hipMemcpyHostToDevice, enq(h)));
   }
   HIPCHK(h, hipStreamSynchronize(h->stream));  // the host copies are freed on return
   return VPTMCM_OK;
@@ -1570,7 +1630,7 @@ static int set_light_one(vptmcm* h, const uint8_t* spd, const float dir[3]) {
   HIPCHK(h, hipSetDevice(h->device));
   memcpy(h->light_host, spd, 256);
   memcpy(h->light_dir, dir, sizeof h->light_dir);
-  HIPCHK(h, hipMemcpyAsync(h->light, h->light_host, 256, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->light, h->light_host, 256, hipMemcpyHostToDevice, enq(h)));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return VPTMCM_OK;
 }
@@ -1604,7 +1664,7 @@ static int set_transfer_function_one(vptmcm* h, const uint8_t* rgba, uint32_t wi
                          (float)t[3] * kInv255);
   }
   HIPCHK(h, hipMemcpyAsync(h->tf_rgb, row.data(), width * sizeof(float4), hipMemcpyHostToDevice,
-                           h->stream));
+                           enq(h)));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->tf_rgb_w = width;
   return VPTMCM_OK;
@@ -1630,9 +1690,9 @@ static int set_band_one(vptmcm* h, uint32_t y0, uint32_t y1) {
   h->band_y1 = y1;
   stream_op(h);
   const size_t row = (size_t)h->R * 3 * sizeof(float);
-  if (y0 > 0) HIPCHK(h, hipMemsetAsync(h->rgb32, 0, y0 * row, h->stream));
+  if (y0 > 0) HIPCHK(h, hipMemsetAsync(h->rgb32, 0, y0 * row, enq(h)));
   if (y1 < h->R)
-    HIPCHK(h, hipMemsetAsync((char*)h->rgb32 + y1 * row, 0, (h->R - y1) * row, h->stream));
+    HIPCHK(h, hipMemsetAsync((char*)h->rgb32 + y1 * row, 0, (h->R - y1) * row, enq(h)));
   h->grp_dirty = true;
   return VPTMCM_OK;
 }
@@ -1659,9 +1719,9 @@ static int reset_one(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   MarchParams P = make_params(h, mvp, seed_bits);
   stream_op(h);
   if (h->kind == VPTMCM_RENDERER_RGB)
-    HIPCHK(h, launch_reset_rgb(P, h->photons, h->stream));
+    HIPCHK(h, launch_reset_rgb(P, h->photons, enq(h)));
   else
-    HIPCHK(h, launch_reset(P, h->photons, h->stream));
+    HIPCHK(h, launch_reset(P, h->photons, enq(h)));
   h->grp_dirty = true;
   return VPTMCM_OK;
 }
@@ -1729,7 +1789,7 @@ int vptmcm_read_rgba16f(vptmcm* h, uint16_t* out) {
     if (int rc = group_composite(h)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipMemcpyAsync(out, composited(h) ? h->grp_rgba : h->rgba, (size_t)h->R * h->R * 8,
-                           hipMemcpyDeviceToHost, h->stream));
+                           hipMemcpyDeviceToHost, enq(h)));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return VPTMCM_OK;
 }
@@ -1742,7 +1802,7 @@ int vptmcm_read_rgb(vptmcm* h, float* out) {
     if (int rc = group_composite(h)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipMemcpyAsync(out, composited(h) ? h->grp_rgb32 : h->rgb32,
-                           (size_t)h->R * h->R * 3 * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+                           (size_t)h->R * h->R * 3 * sizeof(float), hipMemcpyDeviceToHost, enq(h)));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return VPTMCM_OK;
 }
@@ -1756,8 +1816,8 @@ int vptmcm_pack_radiance(vptmcm* h, float* out) {
   float4* d = nullptr;
   HIPCHK(h, hipMalloc(&d, bytes));
   MarchParams P = make_params(h, kNoMatrix, 0);
-  hipError_t e = launch_pack(P, h->photons, h->rgb32, d, h->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(out, d, bytes, hipMemcpyDeviceToHost, h->stream);
+  hipError_t e = launch_pack(P, h->photons, h->rgb32, d, enq(h));
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d, bytes, hipMemcpyDeviceToHost, enq(h));
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   (void)hipFree(d);
   if (e != hipSuccess) FAIL(h, VPTMCM_EHIP, "pack_radiance: %s", hipGetErrorString(e));
@@ -1784,9 +1844,9 @@ int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out
   T.exponent = (float)(-std::log((double)midpoint) / std::log(2.0)) / params[4];
   stream_op(h);
   HIPCHK(h, launch_tonemap_artistic(composited(h) ? h->grp_rgba : h->rgba, (uint32_t)npx, T, h->ldr,
-                                    h->stream));
+                                    enq(h)));
   if (rgba8_out) {
-    HIPCHK(h, hipMemcpyAsync(rgba8_out, h->ldr, npx * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(rgba8_out, h->ldr, npx * 4, hipMemcpyDeviceToHost, enq(h)));
     HIPCHK(h, hipStreamSynchronize(h->stream));
   }
   return VPTMCM_OK;
@@ -1799,7 +1859,7 @@ int vptmcm_read_photons(vptmcm* h, void* out) {
   HIPCHK(h, hipSetDevice(h->device));
   std::vector<uint32_t> planes((size_t)kNumPlanes * h->npad);
   HIPCHK(h, hipMemcpyAsync(planes.data(), h->photons, planes.size() * 4, hipMemcpyDeviceToHost,
-                           h->stream));
+                           enq(h)));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   uint32_t* o = static_cast<uint32_t*>(out);
   if (h->kind == VPTMCM_RENDERER_RGB) {  // struct Photon, Photon.wgsl: 64-B stride
@@ -1869,7 +1929,7 @@ int vptmcm_write_photons(vptmcm* h, const void* in) {
       for (int b = 0; b < kMaxBins; b++) planes[(kRad0 + b) * (size_t)h->npad + i] = w[10 + b];
     }
   HIPCHK(h, hipMemcpyAsync(h->photons, planes.data(), planes.size() * 4, hipMemcpyHostToDevice,
-                           h->stream));
+                           enq(h)));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->grp_dirty = true;
   return VPTMCM_OK;
@@ -1886,8 +1946,8 @@ static int enable_kernel_timing_one(vptmcm* h, int enable) {
   if (h->timing && !h->region.beg) {  // created and first recorded here, outside the region they time
     HIPCHK(h, hipEventCreateWithFlags(&h->region.beg, hipEventDisableSystemFence));
     HIPCHK(h, hipEventCreateWithFlags(&h->region.end, hipEventDisableSystemFence));
-    HIPCHK(h, hipEventRecord(h->region.beg, h->stream));
-    HIPCHK(h, hipEventRecord(h->region.end, h->stream));
+    HIPCHK(h, hipEventRecord(h->region.beg, enq(h)));
+    HIPCHK(h, hipEventRecord(h->region.end, enq(h)));
     HIPCHK(h, hipStreamSynchronize(h->stream));
   }
   h->launches = 0;
@@ -2037,12 +2097,12 @@ int vptmcm_comm_allreduce_radiance(vptmcm* h) {
   if (!h->pack_fresh) {  // the stream does not end with a march that packed comp[k]
     stream_op(h);
     // the buffer must be free of the all-reduce issued two passes ago
-    HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[k], 0));
+    HIPCHK(h, hipStreamWaitEvent(enq(h), h->comp_done[k], 0));
     MarchParams P = make_params(h, kNoMatrix, 0);
-    HIPCHK(h, launch_pack(P, h->photons, h->rgb32, h->comp[k], h->stream));
+    HIPCHK(h, launch_pack(P, h->photons, h->rgb32, h->comp[k], enq(h)));
   }
   stream_op(h);
-  HIPCHK(h, hipEventRecord(h->comp_ready[k], h->stream));
+  HIPCHK(h, hipEventRecord(h->comp_ready[k], enq(h)));
   HIPCHK(h, hipStreamWaitEvent(h->comm_stream, h->comp_ready[k], 0));
   if (int rc = comm_call(h, ncclAllReduce(h->comp[k], h->comp[k], (size_t)h->R * h->R * 4,
                                           ncclFloat32, ncclSum, h->comm, h->comm_stream),
@@ -2086,15 +2146,15 @@ int vptmcm_read_composite(vptmcm* h, uint16_t* rgba16f, float* rgb, float* count
         for (uint32_t k = 1; k < S.n; k++) S.p[k] = h->grp_gather + (size_t)(k - 1) * npx;
       }
       if (!h->comp_counts) HIPCHK(h, hipMalloc(&h->comp_counts, npx * sizeof(float)));
-      HIPCHK(h, launch_composite(S, (uint32_t)npx, nullptr, nullptr, h->comp_counts, h->stream));
+      HIPCHK(h, launch_composite(S, (uint32_t)npx, nullptr, nullptr, h->comp_counts, enq(h)));
       HIPCHK(h, hipMemcpyAsync(counts, h->comp_counts, npx * sizeof(float), hipMemcpyDeviceToHost,
-                               h->stream));
+                               enq(h)));
     }
     if (rgba16f)
-      HIPCHK(h, hipMemcpyAsync(rgba16f, h->grp_rgba, npx * 8, hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(h, hipMemcpyAsync(rgba16f, h->grp_rgba, npx * 8, hipMemcpyDeviceToHost, enq(h)));
     if (rgb)
       HIPCHK(h, hipMemcpyAsync(rgb, h->grp_rgb32, npx * 3 * sizeof(float), hipMemcpyDeviceToHost,
-                               h->stream));
+                               enq(h)));
     return wait_stream(h, h->stream, "read_composite");
   }
   if (!h->comm || h->comp_last < 0)
@@ -2150,9 +2210,9 @@ int vptmcm_comm_gather_bands(vptmcm* h, float* rgb) {
   const size_t n = (size_t)h->R * h->R * 3;
   float* sum = reinterpret_cast<float*>(h->comp[h->comp_next]);  // R*R float4 >= R*R*3 floats
   stream_op(h);
-  HIPCHK(h, hipStreamWaitEvent(h->stream, h->comp_done[h->comp_next], 0));
-  HIPCHK(h, hipMemcpyAsync(sum, h->rgb32, n * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
-  HIPCHK(h, hipEventRecord(h->comp_ready[h->comp_next], h->stream));
+  HIPCHK(h, hipStreamWaitEvent(enq(h), h->comp_done[h->comp_next], 0));
+  HIPCHK(h, hipMemcpyAsync(sum, h->rgb32, n * sizeof(float), hipMemcpyDeviceToDevice, enq(h)));
+  HIPCHK(h, hipEventRecord(h->comp_ready[h->comp_next], enq(h)));
   HIPCHK(h, hipStreamWaitEvent(h->comm_stream, h->comp_ready[h->comp_next], 0));
   if ((rc = comm_call(h, ncclAllReduce(sum, sum, n, ncclFloat32, ncclSum, h->comm, h->comm_stream),
                       "comm_gather_bands")))
@@ -2209,7 +2269,7 @@ int vptmcm_debug_schedule(vptmcm* h, uint32_t* out, uint32_t n_words, uint32_t* 
   if (n_words < n) FAIL(h, VPTMCM_EINVAL, "debug_schedule: output holds fewer words than slots");
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipMemcpyAsync(out, h->sched_prev, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                           h->stream));
+                           enq(h)));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return VPTMCM_OK;
 }
@@ -2229,7 +2289,7 @@ int vptmcm_debug_eval(vptmcm* h, int fn, const uint32_t* in, uint32_t* out, uint
     FAIL(h, VPTMCM_ENOMEM, "debug_eval: allocation failed");
   }
   hipError_t e = hipMemcpy(din, in, (size_t)n * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = launch_debug_eval(fn, din, dout, n, h->stream);
+  if (e == hipSuccess) e = launch_debug_eval(fn, din, dout, n, enq(h));
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost);
   (void)hipFree(din);
@@ -2248,13 +2308,13 @@ int vptmcm_debug_verify(vptmcm* h, int fn, uint32_t lo, uint64_t count, uint64_t
   uint32_t* dfirst = nullptr;
   HIPCHK(h, hipMalloc(&dbad, sizeof(unsigned long long)));
   HIPCHK(h, hipMalloc(&dfirst, (nfirst ? nfirst : 1) * sizeof(uint32_t)));
-  HIPCHK(h, hipMemsetAsync(dbad, 0, sizeof(unsigned long long), h->stream));
+  HIPCHK(h, hipMemsetAsync(dbad, 0, sizeof(unsigned long long), enq(h)));
   uint64_t done = 0;
   hipError_t e = hipSuccess;
   const MarchParams P = make_params(h, kNoMatrix, 0);  // fn 13 uses the current spectrum
   while (done < count && e == hipSuccess) {  // chunks of 2^31 (u32 range)
     uint64_t chunk = count - done < (1ull << 31) ? count - done : (1ull << 31);
-    e = launch_verify(fn, P, (uint32_t)(lo + done), (uint32_t)chunk, dbad, dfirst, nfirst, h->stream);
+    e = launch_verify(fn, P, (uint32_t)(lo + done), (uint32_t)chunk, dbad, dfirst, nfirst, enq(h));
     done += chunk;
   }
   unsigned long long nb = 0;

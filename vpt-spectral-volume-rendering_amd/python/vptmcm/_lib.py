@@ -14,6 +14,8 @@ import numpy as np
 
 PKG = Path(__file__).resolve().parents[2]
 LIB_DIR = PKG / "lib"
+# A/B and measurement builds (tools/variants.py): never beside the product library
+VARIANT_DIR = PKG.parent / "build" / "variants"
 
 OK, EINVAL, EHIP, ESTATE, ENOMEM, ECOMM = 0, -1, -2, -3, -4, -5
 LAYOUT_LINEAR, LAYOUT_CORNER8, LAYOUT_BRICK8, LAYOUT_COLUMN4 = 0, 1, 2, 3
@@ -63,14 +65,15 @@ _lib = None
 
 
 def lib_path() -> Path:
-    # VPTMCM_LIB=<name> selects lib/libvptmcm_<name>.so: the cost-attribution
-    # builds (exp, exp_stamps; results invalid) and tuning variants built by
-    # tools/variants.py for A/B sweeps (tools only; never the product default)
+    # VPTMCM_LIB=<name> selects build/variants/libvptmcm_<name>.so (outside the
+    # shipped package): the cost-attribution builds (exp, exp_stamps; results
+    # invalid) and tuning variants built by tools/variants.py for A/B sweeps
+    # (tools only; never the product default)
     name = os.environ.get("VPTMCM_LIB", "")
     if name:
         if not name.replace("_", "").isalnum():
             raise ValueError(f"VPTMCM_LIB={name!r}: expected an alphanumeric variant name")
-        return LIB_DIR / f"libvptmcm_{name}.so"
+        return VARIANT_DIR / f"libvptmcm_{name}.so"
     return LIB_DIR / "libvptmcm.so"
 
 
