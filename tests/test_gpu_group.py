@@ -125,6 +125,54 @@ def test_group_replicas_composite_bitexact(n_rep, threads, monkeypatch):
     g.close()
 
 
+def _oracle_replicas_stepwise(R, vol, tf, ext, mvp, n_rep, n_pass, start=0):
+    """N oracle replicas advanced one pass at a time: the composite after each pass."""
+    reps, out = [], []
+    for k in range(n_rep):
+        o = orc.Oracle(R)
+        o.set_spectrum(cf.spectrum_buffer("12"))
+        o.volume, o.tf, o.light, o.light_dir = vol, tf, np.full(256, 100, np.uint8), np.asarray((1, 0, 0), np.float32)
+        o.params.update(extinction=ext, bounces=8, steps=8)
+        reps.append([o, None, cf.seed_stream(n_pass + 1, start=start, rank=k)])
+    for o, _, sd in reps:
+        o.reset(mvp, sd[0], nthreads=16)
+    for p in range(1, n_pass + 1):
+        for r in reps:
+            r[1], _ = r[0].render(mvp, r[2][p], nthreads=16)
+        out.append(_composite([(r[0], r[1]) for r in reps]))
+    return out
+
+
+@pytest.mark.parametrize("R,n_rep", [(64, 3), (16, 3), (40, 8)])
+def test_group_per_pass_composites_bitexact(R, n_rep):
+    """A composite after every pass, issued asynchronously (composite() after
+    each render(), nothing read in between), so consecutive composites
+    alternate the double-buffered packs and overlap the next passes; reads at
+    two points and at the end equal the oracle replicas' composite after that
+    many passes. R = 16 with 3 replicas leaves two of the three pixel shards
+    empty; R = 40 is not a multiple of the 256-pixel shard unit."""
+    vol, tf, mvp = cf.fbm_volume(48, 35, nthreads=8), cf.tf_spectral(), cf.golden_mvp("orbit")
+    n_pass = 7
+    want = _oracle_replicas_stepwise(R, vol, tf, 24.0, mvp, n_rep, n_pass, start=9)
+    base = cf.seed_stream(n_pass + 1, start=9)
+    g = vptmcm.Renderer(R, devices=[0] * n_rep)
+    _setup(g, vol, tf, 24.0)
+    g.reset(mvp, base[0])
+    for p in range(1, n_pass + 1):
+        g.render(mvp, base[p])
+        g.composite()
+        if p in (2, 5):
+            q, crgb, n = g.read_composite_all()
+            assert_rgb32_equal(crgb, want[p - 1][0], f"composite after pass {p}")
+            assert np.array_equal(q, want[p - 1][1]) and np.array_equal(n, want[p - 1][2])
+    g.synchronize()
+    assert_rgb32_equal(g.read_rgb(), want[-1][0], "final composite fp32")
+    assert_rgba_equal(g.read_rgba16f(), want[-1][1], "final composite rgba16f")
+    q, crgb, n = g.read_composite_all()
+    assert np.array_equal(n, want[-1][2])
+    g.close()
+
+
 def test_group_tonemap_reads_the_composite():
     R, vol, tf, mvp = 64, cf.fbm_volume(48, 33, nthreads=8), cf.tf_spectral(), cf.default_mvp_inverse()
     seeds = cf.seed_stream(4, start=0)

@@ -1,0 +1,74 @@
+"""Reads of memory the library never wrote, and accesses outside an allocation
+(the contiguous-allocation episode).
+
+* The guard builds (VPT_GUARD; build/variants/libvptmcm_guard.so with poison
+  byte 0xA5, libvptmcm_guardff.so with 0xFF — NaN as f32): every device
+  allocation and every kernel's LDS poisoned before the library writes it,
+  checked guard zones around every allocation, bounds flags on every volume
+  gather. tests/guard_cases.py runs every layout (ragged volumes), both TF
+  paths, streaming ingest, the sharded device-list composite and the RGB
+  sibling under each build, in a process of its own, bit-exact against the
+  oracle with no guard hit.
+* The product library after the device memory pool has been dirtied: 2 GiB
+  of allocations filled with 0xFF and freed before the handle is created, so
+  its buffers are likely to land on dirty memory; bit-exact again.
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import vptmcm
+from vptmcm import configs as cf
+
+from test_gpu_parity import assert_photons_equal, assert_rgb32_equal, assert_rgba_equal, make_pair
+
+pytestmark = pytest.mark.gpu
+REPO = Path(__file__).resolve().parents[1]
+
+
+@pytest.mark.parametrize("lib", ["guard", "guardff"])
+def test_guard_build_cases_bitexact(lib):
+    so = REPO / "build" / "variants" / f"libvptmcm_{lib}.so"
+    assert so.exists(), f"{so} not built (vpt-spectral-volume-rendering_amd/build.py builds it)"
+    env = dict(os.environ, VPTMCM_LIB=lib)
+    p = subprocess.run([sys.executable, str(REPO / "tests" / "guard_cases.py")], env=env,
+                       capture_output=True, text=True, timeout=600)
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    bad = [x for x in lines if not x["ok"]]
+    assert p.returncode == 0 and not bad and len(lines) >= 14, (p.returncode, bad, p.stderr[-3000:])
+
+
+def test_dirty_device_pool_leaves_the_bits():
+    hip = C.CDLL("/opt/rocm/lib/libamdhip64.so")
+    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+    hip.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+    hip.hipFree.argtypes = [C.c_void_p]
+    assert hip.hipSetDevice(0) == 0
+    ptrs = []
+    for k in range(64):  # 2 GiB in sizes from 1 to 63 MiB, interleaved
+        p = C.c_void_p()
+        assert hip.hipMalloc(C.byref(p), (1 + k) << 20) == 0
+        assert hip.hipMemset(p, 0xFF, (1 + k) << 20) == 0
+        ptrs.append(p)
+    assert hip.hipDeviceSynchronize() == 0
+    for p in ptrs[::2] + ptrs[1::2]:
+        assert hip.hipFree(p) == 0
+    R, vol = 48, np.ascontiguousarray(cf.fbm_volume(48, 45, nthreads=8)[:31, :44, :39])
+    for layout in (vptmcm.LAYOUT_COLUMN4, vptmcm.LAYOUT_CORNER8):
+        gpu, cpu = make_pair(R, vol, cf.tf_spectral(), ext=24.0, layout=layout)
+        mvp, seeds = cf.golden_mvp("orbit"), cf.seed_stream(7, start=2)
+        gpu.reset(mvp, seeds[0])
+        gpu.render_passes(mvp, seeds[1:])
+        cpu.reset(mvp, seeds[0], nthreads=16)
+        for s in seeds[1:]:
+            rgb, rgba = cpu.render(mvp, s, nthreads=16)
+        assert_photons_equal(gpu.read_photons(), cpu.photons, "dirty pool photons")
+        assert_rgb32_equal(gpu.read_rgb(), rgb, "dirty pool rgb32")
+        assert_rgba_equal(gpu.read_rgba16f(), rgba, "dirty pool rgba16f")
+        gpu.close()

@@ -59,6 +59,31 @@ def build_hip(force: bool = False) -> Path:
     return out
 
 
+# Debug builds the GPU tests load (tests/test_gpu_guard.py): guard zones and
+# poisoned allocations / LDS with two poison bytes, volume-gather bounds flags
+# (csrc/kernels.hip, VPT_GUARD). Test infrastructure, never the product.
+GUARD_VARIANTS = {"guard": ["-DVPT_GUARD=1"], "guardff": ["-DVPT_GUARD=1", "-DVPT_POISON=0xFFu"]}
+
+
+def build_guard(force: bool = False) -> list[Path]:
+    from concurrent.futures import ThreadPoolExecutor
+    srcs = [CSRC / "kernels.hip", CSRC / "vptmcm.cpp"]
+    deps = srcs + [CSRC / "kernels.h", CSRC / "march.h", CSRC / "mcm_device.h", CSRC / "stamp.h",
+                   REPO / "include" / "vptmcm.h"]
+    hipcc = shutil.which("hipcc") or str(ROCM / "bin" / "hipcc")
+    VARIANTS.mkdir(parents=True, exist_ok=True)
+
+    def one(item):
+        name, flags = item
+        out = VARIANTS / f"libvptmcm_{name}.so"
+        if force or _stale(out, deps):
+            _run([hipcc, *HIP_FLAGS, *flags, "-shared", f"-I{REPO / 'include'}", *srcs, "-o", out,
+                  "-lrccl", f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}"])
+        return out
+    with ThreadPoolExecutor(len(GUARD_VARIANTS)) as ex:
+        return list(ex.map(one, GUARD_VARIANTS.items()))
+
+
 def build_napi(force: bool = False) -> Path | None:
     out = LIB / "vptmcm_napi.node"
     src = PKG / "napi" / "vptmcm_napi.c"
@@ -103,8 +128,12 @@ def clean_stale_variants() -> None:
 
 
 def build_all(force: bool = False) -> None:
+    from concurrent.futures import ThreadPoolExecutor
     clean_stale_variants()
-    build_hip(force)
+    with ThreadPoolExecutor(2) as ex:  # the product and the guard builds compile at once
+        guard = ex.submit(build_guard, force)
+        build_hip(force)
+        guard.result()
     build_synth(force)
     build_napi(force)
     build_oracle(force)

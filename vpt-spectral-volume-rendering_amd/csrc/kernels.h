@@ -121,16 +121,21 @@ hipError_t launch_column4(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D
                           hipStream_t s, const uint32_t c0[3] = nullptr, const uint32_t n[3] = nullptr);
 hipError_t launch_pack(const MarchParams& P, const float* ph, const float* rgb32, float4* out,
                        hipStream_t s);
-// Multi-replica composite (k_composite): the n source buffers of R^2 (rgb*n, n)
+// Multi-replica composite (k_composite): the n source buffers of npx (rgb*n, n)
 // float4 summed in source order, / sum(n) -> fp32 rgb and rgba16float (either
-// output and counts may be null).
+// output and counts may be null). Sources and outputs may point into a shard
+// of the frame; coherent: system-scope loads / stores, for sources and outputs
+// in other devices' memory (the sharded device-list composite).
 constexpr uint32_t kMaxReplicas = 8;
 struct CompositeSrc {
   const float4* p[kMaxReplicas];
   uint32_t n;
 };
 hipError_t launch_composite(const CompositeSrc& S, uint32_t npx, float* rgb32, uint16_t* rgba,
-                            float* counts, hipStream_t s);
+                            float* counts, hipStream_t s, bool coherent = false);
+// Guard build (VPT_GUARD): the layouts whose volume gathers left the volume
+// allocation since the last call (bit = kTpl*), cleared by the call (0 in the product).
+hipError_t guard_take_oob(uint32_t* out);
 // fn 13 checks bin_of's arithmetic path against the count on the spectrum in P
 hipError_t launch_verify(int fn, const MarchParams& P, uint32_t lo, uint32_t n,
                          unsigned long long* bad, uint32_t* first, uint32_t nfirst, hipStream_t s);

@@ -23,6 +23,45 @@
 
 namespace vpt {
 
+// ------------------------------------------------- guard build (VPT_GUARD)
+// The debug build (-DVPT_GUARD=1, build/variants/libvptmcm_guard*.so; the
+// product has VPT_GUARD 0 and every hook below is empty) looks for reads of
+// memory the library never wrote and accesses outside an allocation: every
+// kernel with LDS fills all of it with the poison byte VPT_POISON before its
+// own first LDS write (an LDS read before a write then sees poison instead of
+// what an earlier kernel left on the CU, and breaks bit-exactness against the
+// oracle); every volume gather checks its byte range against the volume
+// allocation and flags a miss in g_guard_oob (bit = the layout template); the
+// host side poisons every device allocation and brackets it with checked
+// guard zones (vptmcm.cpp, dev_alloc).
+#ifndef VPT_GUARD
+#define VPT_GUARD 0
+#endif
+#ifndef VPT_POISON
+#define VPT_POISON 0xA5u
+#endif
+#if VPT_GUARD
+__device__ uint32_t g_guard_oob;
+#endif
+
+__device__ __forceinline__ void guard_gather(uint32_t L, uint64_t end, uint64_t limit) {
+#if VPT_GUARD
+  if (end > limit) __hip_atomic_fetch_or(&g_guard_oob, 1u << L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+
+// Fill n bytes of LDS at p with the poison byte (all threads of the block;
+// the caller's barrier publishes it). n is a multiple of 4.
+__device__ __forceinline__ void poison_lds(void* p, uint32_t n) {
+#if VPT_GUARD
+  uint32_t* w = static_cast<uint32_t*>(p);
+  for (uint32_t k = threadIdx.x; k < n / 4u; k += blockDim.x) w[k] = (uint32_t)VPT_POISON * 0x01010101u;
+#else
+  (void)p;
+  (void)n;
+#endif
+}
+
 // ------------------------------------------------------------- photon I/O
 __device__ __forceinline__ void load_photon(const float* __restrict__ ph, size_t S, size_t i,
                                             Photon& p) {
@@ -127,6 +166,8 @@ __device__ __forceinline__ VolTap vol_fetch(const MarchParams& P, const uint8_t*
     const uint32_t cz = (uint32_t)(clampi(iz + 1, (int)P.D));
     const uint32_t brick = __umul24(mad_u24(cz >> 2, P.BH, cy >> 2), P.BW) + (cx >> 2);
     const uint32_t inner = brick_inner(cx, cy, cz) << 3;
+    guard_gather(L, (((uint64_t)brick << 9) | inner) + 8u,
+                 (uint64_t)P.BW * P.BH * ((P.D + kBrickCells) / kBrickCells) * 512u);
     uint2 c;
     if constexpr (L == kTplBrick8)
       c = *reinterpret_cast<const uint2*>(vol + ((brick << 9) | inner));
@@ -139,6 +180,8 @@ __device__ __forceinline__ VolTap vol_fetch(const MarchParams& P, const uint8_t*
     const uint32_t cx = (uint32_t)(clampi(ix + 1, (int)P.W));
     const uint32_t cy = (uint32_t)(clampi(iy + 1, (int)P.H));
     const uint32_t cz = (uint32_t)(clampi(iz + 1, (int)P.D));
+    guard_gather(L, (((uint64_t)cy * W1 + cx) * D2 + cz) * 4u + 8u,
+                 ((uint64_t)W1 * (P.H + 1u) * D2 + 1u) / 2u * 8u);
     uint2 c;
     if constexpr (L == kTplColumn4)  // quad index (cy * W1 + cx) * D2 + cz, 32-bit byte offset
       c = load8_a4(vol + ((__umul24(mad_u24(cy, W1, cx), D2) + cz) << 2));
@@ -151,6 +194,7 @@ __device__ __forceinline__ VolTap vol_fetch(const MarchParams& P, const uint8_t*
     uint32_t cx = (uint32_t)(clampi(ix + 1, (int)P.W));
     uint32_t cy = (uint32_t)(clampi(iy + 1, (int)P.H));
     uint32_t cz = (uint32_t)(clampi(iz + 1, (int)P.D));
+    guard_gather(L, (((uint64_t)cz * H1 + cy) * W1 + cx) * 8u + 8u, (uint64_t)W1 * H1 * (P.D + 1u) * 8u);
     uint2 c;
     if constexpr (L == kTplCorner8) {
       // 32-bit byte offset from the SGPR base (u24 multiply-adds, saddr load)
@@ -169,6 +213,8 @@ __device__ __forceinline__ VolTap vol_fetch(const MarchParams& P, const uint8_t*
     uint32_t z0 = clampi(iz, dm), z1 = clampi(iz + 1, dm);
     size_t r00 = ((size_t)z0 * P.H + y0) * P.W, r10 = ((size_t)z0 * P.H + y1) * P.W;
     size_t r01 = ((size_t)z1 * P.H + y0) * P.W, r11 = ((size_t)z1 * P.H + y1) * P.W;
+    guard_gather(L, (uint64_t)std::max(std::max(r00, r10), std::max(r01, r11)) + std::max(x0, x1) + 1u,
+                 (uint64_t)P.W * P.H * P.D);
     t.lo = (uint32_t)vol[r00 + x0] | ((uint32_t)vol[r00 + x1] << 8) |
            ((uint32_t)vol[r10 + x0] << 16) | ((uint32_t)vol[r10 + x1] << 24);
     t.hi = (uint32_t)vol[r01 + x0] | ((uint32_t)vol[r01 + x1] << 8) |
@@ -468,6 +514,17 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __shared__ uint32_t s_red[64];
   __shared__ uint32_t s_tile[16];
   __shared__ uint32_t s_done;  // the block's waves past their stores (signal_done)
+  if (VPT_GUARD) {
+    poison_lds(s_tf4, sizeof s_tf4);
+    poison_lds(s_light, sizeof s_light);
+    poison_lds(s_brow, sizeof s_brow);
+    poison_lds(s_rowmap, sizeof s_rowmap);
+    poison_lds(s_binlut, sizeof s_binlut);
+    poison_lds(s_red, sizeof s_red);
+    poison_lds(s_tile, sizeof s_tile);
+    poison_lds(&s_done, sizeof s_done);
+    __syncthreads();
+  }
   if (threadIdx.x == 0u) s_done = 0u;  // published by the prologue's barriers
 
   TL_DECL();
@@ -1054,6 +1111,12 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
   __shared__ float4 s_tf[kRgbTfMax];
   __shared__ uint32_t s_red[64];
   __shared__ uint32_t s_tile[16];
+  if (VPT_GUARD) {
+    poison_lds(s_tf, sizeof s_tf);
+    poison_lds(s_red, sizeof s_red);
+    poison_lds(s_tile, sizeof s_tile);
+    __syncthreads();
+  }
   // the SIMD-balanced tile schedule and volume-wave priority of k_march, and
   // its reuse of the previous launch's deal (TileSched::changed_in)
   uint32_t tile;
@@ -1316,20 +1379,57 @@ __global__ __launch_bounds__(256) void k_pack(const MarchParams P, const float* 
   out[pix] = make_float4(c[0] * n, c[1] * n, c[2] * n, n);
 }
 
+// Coherent access for the sharded device-list composite (COH): a shard kernel
+// on device K reads the other replicas' packs in their devices' memory and
+// writes its slice of the image into devices[0]'s memory over xGMI. Relaxed
+// system-scope atomic loads / stores (global_load / global_store with sc0 sc1
+// on gfx950) bypass the non-coherent caching of remote lines in K's L2, so
+// the shard sees exactly what each pack kernel left in memory (its event, a
+// system-scope release, precedes the shard kernel's cross-device wait) and its
+// stores reach devices[0]'s memory before its own completion event, whatever
+// the acquire / release scope of the dispatch packets.
+template <bool COH>
+__device__ __forceinline__ float ld_f(const float* p) {
+  if constexpr (COH)
+    return __uint_as_float(__hip_atomic_load(reinterpret_cast<uint32_t*>(const_cast<float*>(p)),
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  else
+    return *p;
+}
+template <bool COH>
+__device__ __forceinline__ float4 ld_f4(const float4* p) {
+  if constexpr (COH) {
+    const float* f = reinterpret_cast<const float*>(p);
+    return make_float4(ld_f<true>(f), ld_f<true>(f + 1), ld_f<true>(f + 2), ld_f<true>(f + 3));
+  } else {
+    return *p;
+  }
+}
+template <bool COH>
+__device__ __forceinline__ void st_u(uint32_t* p, uint32_t v) {
+  if constexpr (COH)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else
+    *p = v;
+}
+
 // The composite of R^2 (rgb*n, n) float4 buffers (k_pack's, one per replica,
 // or one already summed by an RCCL all-reduce / reduce): per pixel the sum over
 // the sources in source order (f32 adds: deterministic for a fixed order), then
 // rgb = sum(rgb*n) / sum(n) with a correctly rounded division (0 where no
 // samples), stored as fp32 and as rgba16float (round-to-nearest-even, alpha 1).
+// The sources and outputs may be offset to a pixel range (a shard); COH: the
+// coherent accesses above (the sharded device-list composite).
+template <bool COH>
 __global__ __launch_bounds__(256) void k_composite(const CompositeSrc S, uint32_t npx,
                                                    float* __restrict__ rgb32,
                                                    uint16_t* __restrict__ rgba,
                                                    float* __restrict__ counts) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= npx) return;
-  float4 s = S.p[0][i];
+  float4 s = ld_f4<COH>(S.p[0] + i);
   for (uint32_t k = 1; k < S.n; k++) {
-    const float4 t = S.p[k][i];
+    const float4 t = ld_f4<COH>(S.p[k] + i);
     s.x += t.x;
     s.y += t.y;
     s.z += t.z;
@@ -1339,17 +1439,17 @@ __global__ __launch_bounds__(256) void k_composite(const CompositeSrc S, uint32_
   const bool any = n > 0.0f;
   const float r = any ? s.x / n : 0.0f, g = any ? s.y / n : 0.0f, b = any ? s.z / n : 0.0f;
   if (rgb32) {
-    rgb32[3u * i] = r;
-    rgb32[3u * i + 1u] = g;
-    rgb32[3u * i + 2u] = b;
+    uint32_t* o = reinterpret_cast<uint32_t*>(rgb32) + 3u * i;
+    st_u<COH>(o, __float_as_uint(r));
+    st_u<COH>(o + 1, __float_as_uint(g));
+    st_u<COH>(o + 2, __float_as_uint(b));
   }
   if (rgba) {
-    uint2 px;
-    px.x = (uint32_t)f2h(r) | ((uint32_t)f2h(g) << 16);
-    px.y = (uint32_t)f2h(b) | (0x3c00u << 16);
-    reinterpret_cast<uint2*>(rgba)[i] = px;
+    uint32_t* o = reinterpret_cast<uint32_t*>(rgba) + 2u * i;
+    st_u<COH>(o, (uint32_t)f2h(r) | ((uint32_t)f2h(g) << 16));
+    st_u<COH>(o + 1, (uint32_t)f2h(b) | (0x3c00u << 16));
   }
-  if (counts) counts[i] = n;
+  if (counts) st_u<COH>(reinterpret_cast<uint32_t*>(counts) + i, __float_as_uint(n));
 }
 
 // ------------------------------------------------------------ tone mapping
@@ -1561,6 +1661,18 @@ hipError_t launch_column4(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D
   return hipGetLastError();
 }
 
+hipError_t guard_take_oob(uint32_t* out) {
+#if VPT_GUARD
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_guard_oob), sizeof(uint32_t));
+  const uint32_t zero = 0u;
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_guard_oob), &zero, sizeof zero);
+  return e;
+#else
+  *out = 0u;
+  return hipSuccess;
+#endif
+}
+
 hipError_t launch_pack(const MarchParams& P, const float* ph, const float* rgb32, float4* out,
                        hipStream_t s) {
   hipLaunchKernelGGL(k_pack, dim3(march_blocks(P)), dim3(kBlock), 0, s, P, ph, rgb32, out);
@@ -1568,10 +1680,15 @@ hipError_t launch_pack(const MarchParams& P, const float* ph, const float* rgb32
 }
 
 hipError_t launch_composite(const CompositeSrc& S, uint32_t npx, float* rgb32, uint16_t* rgba,
-                            float* counts, hipStream_t s) {
+                            float* counts, hipStream_t s, bool coherent) {
   if (npx == 0) return hipSuccess;
   if (S.n < 1 || S.n > kMaxReplicas) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_composite, dim3((npx + 255u) / 256u), dim3(256), 0, s, S, npx, rgb32, rgba, counts);
+  if (coherent)
+    hipLaunchKernelGGL(k_composite<true>, dim3((npx + 255u) / 256u), dim3(256), 0, s, S, npx, rgb32, rgba,
+                       counts);
+  else
+    hipLaunchKernelGGL(k_composite<false>, dim3((npx + 255u) / 256u), dim3(256), 0, s, S, npx, rgb32, rgba,
+                       counts);
   return hipGetLastError();
 }
 

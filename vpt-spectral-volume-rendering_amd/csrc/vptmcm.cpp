@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -31,12 +32,106 @@
 #ifndef VPT_STAMP
 #define VPT_STAMP 0  // measurement builds (csrc/stamp.h) set it for both sources
 #endif
+// Guard build (-DVPT_GUARD=1 for both sources, kernels.hip): every device
+// allocation is filled with the poison byte VPT_POISON (so a read of memory
+// the library never wrote breaks bit-exactness) and bracketed by guard zones
+// of poison that are checked, with the kernels' volume-gather bounds flags,
+// after every launch; a hit fails the call with VPTMCM_EHIP naming it.
+#ifndef VPT_GUARD
+#define VPT_GUARD 0
+#endif
+#ifndef VPT_POISON
+#define VPT_POISON 0xA5u
+#endif
 
 using namespace vpt;
 
 namespace {
 
 thread_local std::string g_create_error;
+
+// ---- device allocations (guard zones in the guard build)
+constexpr size_t kGuardBytes = VPT_GUARD ? 65536 : 0;
+struct GuardAlloc {
+  void* base;
+  size_t bytes;
+};
+std::mutex g_guard_mu;
+std::map<uintptr_t, GuardAlloc>& guard_live() {
+  static std::map<uintptr_t, GuardAlloc> m;
+  return m;
+}
+
+hipError_t dev_alloc_raw(void** p, size_t bytes) {
+  if (!VPT_GUARD) return hipMalloc(p, bytes);
+  void* base = nullptr;
+  hipError_t e = hipMalloc(&base, bytes + 2 * kGuardBytes);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return e;
+  }
+  e = hipMemset(base, (int)VPT_POISON, bytes + 2 * kGuardBytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();  // before any stream of the library touches it
+  if (e != hipSuccess) {
+    (void)hipFree(base);
+    *p = nullptr;
+    return e;
+  }
+  *p = static_cast<char*>(base) + kGuardBytes;
+  std::lock_guard<std::mutex> lk(g_guard_mu);
+  guard_live()[(uintptr_t)*p] = GuardAlloc{base, bytes};
+  return hipSuccess;
+}
+
+template <class T>
+hipError_t dev_alloc(T** p, size_t bytes) {
+  void* v = nullptr;
+  const hipError_t e = dev_alloc_raw(&v, bytes);
+  *p = static_cast<T*>(v);
+  return e;
+}
+
+// The guard zones of one allocation hold nothing but poison (guard build).
+bool guard_intact(uintptr_t user, const GuardAlloc& a) {
+  std::vector<uint8_t> g(kGuardBytes);
+  for (int side = 0; side < 2; side++) {
+    const char* z = side ? reinterpret_cast<const char*>(user) + a.bytes : static_cast<const char*>(a.base);
+    if (hipMemcpy(g.data(), z, kGuardBytes, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    for (uint8_t b : g)
+      if (b != (uint8_t)VPT_POISON) return false;
+  }
+  return true;
+}
+
+// Every live allocation's guard zones: "" when intact, else which one broke.
+std::string guard_scan() {
+  if (!VPT_GUARD) return std::string();
+  std::lock_guard<std::mutex> lk(g_guard_mu);
+  for (const auto& kv : guard_live())
+    if (!guard_intact(kv.first, kv.second)) {
+      char b[128];
+      snprintf(b, sizeof b, "guard zone of the %zu-byte allocation at %p overwritten", kv.second.bytes,
+               (void*)kv.first);
+      return b;
+    }
+  return std::string();
+}
+
+hipError_t dev_free(void* p) {
+  if (!VPT_GUARD || !p) return hipFree(p);
+  GuardAlloc a{nullptr, 0};
+  {
+    std::lock_guard<std::mutex> lk(g_guard_mu);
+    auto it = guard_live().find((uintptr_t)p);
+    if (it == guard_live().end()) return hipFree(p);  // not ours
+    a = it->second;
+    if (!guard_intact(it->first, a))
+      fprintf(stderr, "vptmcm guard: guard zone of the %zu-byte allocation at %p overwritten (at free)\n",
+              a.bytes, p);
+    guard_live().erase(it);
+  }
+  return hipFree(a.base);
+}
 
 struct EventPair {
   hipEvent_t beg = nullptr, end = nullptr;
@@ -207,12 +302,24 @@ struct vptmcm {
   bool grouped = false;            // created from a device list (even of one device)
   uint32_t group_transport = VPTMCM_GROUP_PEER;
   bool grp_dirty = true;           // a march / reset since the last composite
-  float4* grp_pack = nullptr;      // this replica's (rgb*n, n), on its device
-  float4* grp_gather = nullptr;    // replica 0: the peers' packs (PEER) / the reduced sum (RCCL)
+  // this replica's (rgb*n, n) on its device; PEER double-buffers it (composite
+  // j packs into [j & 1]), so a pack never waits for the composite before it
+  float4* grp_pack[2] = {nullptr, nullptr};
+  float4* grp_gather = nullptr;    // replica 0, RCCL: the reduced sum
   float* grp_rgb32 = nullptr;      // replica 0: the composite, fp32
   uint16_t* grp_rgba = nullptr;    // replica 0: the composite, rgba16float
-  hipEvent_t grp_packed = nullptr; // this replica's pack is complete
-  hipEvent_t grp_done = nullptr;   // replica 0: the last composite has read every pack
+  float* grp_counts = nullptr;     // replica 0, PEER: the composite's sum(n)
+  hipEvent_t grp_packed = nullptr; // this replica's pack of the current composite is complete
+  // PEER (sharded): replica k composites pixel shard k of every replica's pack
+  // on its own device, on a stream of its own (its next march does not wait
+  // for the other replicas), writing that slice of the image into devices[0]
+  hipStream_t grp_stream = nullptr;
+  hipEvent_t grp_shard = nullptr;  // this replica's shard of the current composite is written
+  // replica 0: composite j (buffer j & 1) has read every pack and written every
+  // shard; the readers and the pack two composites later wait for it
+  hipEvent_t grp_done[2] = {nullptr, nullptr};
+  uint32_t grp_seq = 0;            // replica 0: composites issued
+  int grp_last = -1;               // replica 0: the buffer of the last composite
   std::vector<ncclComm_t> grp_comms;  // RCCL transport: one communicator per replica (InitAll)
   // replica 0: one worker thread per peer (VPTMCM_GROUP_THREADS=0: none, the
   // operations run serially on the caller's thread)
@@ -495,6 +602,22 @@ MarchParams make_params(vptmcm* h, const float* mvp, uint32_t seed) {
 
 int check_handle(vptmcm* h) { return h ? VPTMCM_OK : VPTMCM_EINVAL; }
 
+// Guard build: after the handle's queued work has finished, no volume gather
+// left the volume allocation and every guard zone still holds poison; the
+// product (VPT_GUARD 0) checks nothing.
+int guard_check(vptmcm* h, const char* where) {
+  if (!VPT_GUARD) return VPTMCM_OK;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (h->grp_stream) HIPCHK(h, hipStreamSynchronize(h->grp_stream));
+  uint32_t oob = 0u;
+  HIPCHK(h, guard_take_oob(&oob));
+  if (oob) FAIL(h, VPTMCM_EHIP, "guard: %s: a volume gather left the volume allocation (templates 0x%x)", where, oob);
+  const std::string g = guard_scan();
+  if (!g.empty()) FAIL(h, VPTMCM_EHIP, "guard: %s: %s", where, g.c_str());
+  return VPTMCM_OK;
+}
+
 // Work other than a march is enqueued on the handle's stream: the stream no
 // longer ends with a signalling march (vptmcm::done_pending) or with one that
 // packed the composite buffer (vptmcm::pack_fresh).
@@ -629,12 +752,12 @@ int flush_relayout(vptmcm* h) {
     const uint32_t z1 = std::min(h->vol_c1[2] + 1u, h->D + 2u);
     const uint32_t nq[3] = {n[0], n[1], z1 - h->vol_c0[2]};
     HIPCHK(h, launch_column4(h->vol_lin, h->W, h->H, h->D, h->vol_c8, enq(h), h->vol_c0, nq));
-    return VPTMCM_OK;
+    return guard_check(h, "relayout");
   }
   HIPCHK(h, launch_corner8(h->vol_lin, h->W, h->H, h->D, brick ? (h->W + kBrickCells) / kBrickCells : 0u,
                            brick ? (h->H + kBrickCells) / kBrickCells : 0u, h->vol_c8, enq(h),
                            h->vol_c0, n));
-  return VPTMCM_OK;
+  return guard_check(h, "relayout");
 }
 
 // One march launch of n <= kMaxFusedPasses passes (seeds) with matrix mvp.
@@ -694,7 +817,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   }
   h->done_pending = signal;
   h->pack_fresh = pack;
-  return VPTMCM_OK;
+  return guard_check(h, "march");
 }
 
 // Launch the queued render() passes (see vptmcm::pend_n) as one march.
@@ -997,8 +1120,8 @@ int for_replicas(vptmcm* h, const F& f) { return run_replicas(h, true, f); }
 bool composited(const vptmcm* h) { return !h->peers.empty(); }
 
 void free_volume(vptmcm* h) {
-  if (h->vol_lin) (void)hipFree(h->vol_lin);
-  if (h->vol_c8) (void)hipFree(h->vol_c8);
+  if (h->vol_lin) (void)dev_free(h->vol_lin);
+  if (h->vol_c8) (void)dev_free(h->vol_c8);
   h->vol_lin = nullptr;
   h->vol_c8 = nullptr;
   h->volume_ready = false;
@@ -1019,52 +1142,60 @@ const char* vptmcm_last_error(const vptmcm* h) {
 
 // ---- device-list handles (vptmcm_config::n_devices)
 
-// The composite's buffers and events: a pack buffer per replica on its device;
-// on devices[0] the peers' packs (PEER) or the reduced sum (RCCL) and the
-// composite image. PEER enables xGMI peer access from devices[0] to each other
-// device (copies then run device to device over the link); RCCL builds one
-// communicator per replica with ncclCommInitAll (one process: no bootstrap
+// The composite's buffers and events. PEER: two pack buffers, a composite
+// stream and a shard event per replica; on devices[0] the composite image and
+// counts; xGMI peer access between EVERY pair of distinct devices (a shard
+// kernel on device k reads every replica's pack and writes devices[0]'s
+// image). RCCL: one pack buffer per replica, the reduced sum on devices[0] and
+// one communicator per replica by ncclCommInitAll (one process: no bootstrap
 // peers that could fail to arrive).
 static int group_alloc(vptmcm* h, const int32_t* devs, uint32_t n) {
   const size_t npx = (size_t)h->R * h->R;
+  const bool peer = h->group_transport == VPTMCM_GROUP_PEER;
   int rc = for_replicas(h, [&](vptmcm* c) {
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipMalloc(&c->grp_pack, npx * sizeof(float4)));
+    for (int k = 0; k < (peer ? 2 : 1); k++) HIPCHK(c, dev_alloc(&c->grp_pack[k], npx * sizeof(float4)));
     HIPCHK(c, hipEventCreateWithFlags(&c->grp_packed, hipEventDisableTiming));
+    if (peer) {
+      HIPCHK(c, hipStreamCreateWithFlags(&c->grp_stream, hipStreamNonBlocking));
+      HIPCHK(c, hipEventCreateWithFlags(&c->grp_shard, hipEventDisableTiming));
+    }
     return VPTMCM_OK;
   });
   if (rc) return rc;
   HIPCHK(h, hipSetDevice(h->device));
-  stream_op(h);
-  const size_t slots = h->group_transport == VPTMCM_GROUP_RCCL ? 1 : n - 1;
-  if (slots) HIPCHK(h, hipMalloc(&h->grp_gather, slots * npx * sizeof(float4)));
-  HIPCHK(h, hipMalloc(&h->grp_rgb32, npx * 3 * sizeof(float)));
+  if (!peer) HIPCHK(h, dev_alloc(&h->grp_gather, npx * sizeof(float4)));
+  HIPCHK(h, dev_alloc(&h->grp_rgb32, npx * 3 * sizeof(float)));
   HIPCHK(h, hipMemsetAsync(h->grp_rgb32, 0, npx * 3 * sizeof(float), enq(h)));
-  HIPCHK(h, hipMalloc(&h->grp_rgba, npx * 4 * sizeof(uint16_t)));
+  HIPCHK(h, dev_alloc(&h->grp_rgba, npx * 4 * sizeof(uint16_t)));
   HIPCHK(h, hipMemsetAsync(h->grp_rgba, 0, npx * 4 * sizeof(uint16_t), enq(h)));
-  HIPCHK(h, hipEventCreateWithFlags(&h->grp_done, hipEventDisableTiming));
-  HIPCHK(h, hipEventRecord(h->grp_done, enq(h)));
+  if (peer) {
+    HIPCHK(h, dev_alloc(&h->grp_counts, npx * sizeof(float)));
+    HIPCHK(h, hipMemsetAsync(h->grp_counts, 0, npx * sizeof(float), enq(h)));
+  }
+  for (int k = 0; k < 2; k++) {
+    HIPCHK(h, hipEventCreateWithFlags(&h->grp_done[k], hipEventDisableTiming));
+    HIPCHK(h, hipEventRecord(h->grp_done[k], enq(h)));
+  }
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  if (h->group_transport == VPTMCM_GROUP_PEER) {
-    // both directions between devices[0] and each peer: the peer's stream
-    // pushes its pack into devices[0]'s memory (peer -> devices[0]), and
-    // devices[0] reads nothing of the peers' but keeps the historical access
-    auto enable = [&](int from, int to) -> int {
-      int can = 0;
-      HIPCHK(h, hipDeviceCanAccessPeer(&can, from, to));
-      if (!can) return VPTMCM_OK;  // hipMemcpyPeerAsync then stages through the host
-      HIPCHK(h, hipSetDevice(from));
-      const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
-      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
-        FAIL(h, VPTMCM_EHIP, "hipDeviceEnablePeerAccess(%d -> %d): %s", from, to, hipGetErrorString(e));
-      (void)hipGetLastError();  // clear an already-enabled status
-      return VPTMCM_OK;
-    };
-    for (uint32_t k = 1; k < n; k++) {
-      if (devs[k] == h->device) continue;
-      if (int rc2 = enable(h->device, devs[k])) return rc2;
-      if (int rc2 = enable(devs[k], h->device)) return rc2;
-    }
+  if (peer) {
+    // every ordered pair of distinct devices (a shard kernel on `from` reads
+    // and writes `to`'s memory); without peer access a kernel cannot reach the
+    // other device at all, so the PEER transport is refused (RCCL remains)
+    for (uint32_t i = 0; i < n; i++)
+      for (uint32_t j = 0; j < n; j++) {
+        if (devs[i] == devs[j]) continue;
+        int can = 0;
+        HIPCHK(h, hipDeviceCanAccessPeer(&can, devs[i], devs[j]));
+        if (!can)
+          FAIL(h, VPTMCM_EINVAL, "devices %d and %d have no peer access: the PEER group transport needs "
+               "it between every pair (use VPTMCM_GROUP_RCCL)", devs[i], devs[j]);
+        HIPCHK(h, hipSetDevice(devs[i]));
+        const hipError_t e = hipDeviceEnablePeerAccess(devs[j], 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+          FAIL(h, VPTMCM_EHIP, "hipDeviceEnablePeerAccess(%d -> %d): %s", devs[i], devs[j], hipGetErrorString(e));
+        (void)hipGetLastError();  // clear an already-enabled status
+      }
     HIPCHK(h, hipSetDevice(h->device));
   } else {
     h->grp_comms.assign(n, nullptr);
@@ -1172,59 +1303,106 @@ static int create_group(const vptmcm_config* cfg, vptmcm** out) {
   return VPTMCM_OK;
 }
 
-// The composite of the current frame over every replica, enqueued on replica
-// 0's stream: each replica packs (rgb*n, n) on its own stream; PEER: each peer
-// then pushes its pack to its slot on devices[0] on its own stream (its own
-// xGMI link, all peers at once; a device copy for a repeated device) and
-// k_composite sums the slots in replica order; RCCL reduces the packs to
-// devices[0] (grouped ncclReduce) and k_composite divides. Asynchronous.
+// Replica k of a device-list handle (0: the handle itself).
+static vptmcm* replica_of(vptmcm* h, uint32_t k) { return k ? h->peers[k - 1] : h; }
+
+// Pixel shard k of N of the PEER composite: [p0, p1), whole 256-pixel blocks
+// of the composite kernel except the last (a shard may be empty for tiny R).
+static void shard_range(size_t npx, uint32_t n, uint32_t k, size_t* p0, size_t* p1) {
+  const size_t step = ((npx + n - 1) / n + 255) / 256 * 256;
+  *p0 = std::min(npx, (size_t)k * step);
+  *p1 = std::min(npx, *p0 + step);
+}
+
+// The composite of the current frame over every replica. Asynchronous: the
+// readers (and synchronize) wait for grp_done[grp_last].
+//
+// PEER (sharded): (1) every replica packs (rgb*n, n) into its buffer j & 1 on
+// its own stream, behind its march (that buffer was last read by composite
+// j - 2: its grp_done); (2) replica k, on its composite stream, waits for
+// every replica's pack and composites pixel shard k of all of them — the
+// sources summed in replica order, the same f32 sums and division as one
+// k_composite over whole buffers — writing that slice of devices[0]'s fp32
+// image, rgba16f image and counts: each device reads 1/N of every pack over
+// its own links at once and writes 1/N of the image to devices[0]; (3)
+// devices[0]'s composite stream waits for every shard and records grp_done.
+// Steps (1) and (2) run on the replicas' worker threads; a step's host
+// enqueue starts once every replica has recorded the previous step's event.
+//
+// RCCL: every replica packs, a grouped ncclReduce sums the packs on
+// devices[0], and k_composite divides there, on replica 0's stream.
 static int group_composite(vptmcm* h) {
   const uint32_t n = 1u + (uint32_t)h->peers.size();
-  const size_t npx = (size_t)h->R * h->R, bytes = npx * sizeof(float4);
+  const size_t npx = (size_t)h->R * h->R;
   const bool peer = h->group_transport == VPTMCM_GROUP_PEER;
+  const uint32_t b = peer ? (h->grp_seq & 1u) : 0u;
+  hipEvent_t prev = h->grp_done[b];
   int rc = for_replicas(h, [&](vptmcm* c) {
     if (int r = flush_renders(c)) return r;
     HIPCHK(c, hipSetDevice(c->device));
-    stream_op(c);  // the pack follows the march on this stream
-    // the last composite has read this replica's pack (and its slot on devices[0])
-    HIPCHK(c, hipStreamWaitEvent(enq(c), h->grp_done, 0));
+    HIPCHK(c, hipStreamWaitEvent(enq(c), prev, 0));  // buffer b is free (and, RCCL, the reduce target)
     const MarchParams P = make_params(c, kNoMatrix, 0);
-    HIPCHK(c, launch_pack(P, c->photons, c->rgb32, c->grp_pack, enq(c)));
-    if (peer && c != h)
-      HIPCHK(c, hipMemcpyPeerAsync(h->grp_gather + (size_t)(c->replica - 1) * npx, h->device, c->grp_pack,
-                                   c->device, bytes, enq(c)));
+    HIPCHK(c, launch_pack(P, c->photons, c->rgb32, c->grp_pack[b], enq(c)));
     HIPCHK(c, hipEventRecord(c->grp_packed, enq(c)));
     return VPTMCM_OK;
   });
   if (rc) return rc;
-  CompositeSrc S;
-  memset(&S, 0, sizeof S);
-  if (h->group_transport == VPTMCM_GROUP_RCCL) {
+  if (peer) {
+    rc = for_replicas(h, [&](vptmcm* c) {
+      HIPCHK(c, hipSetDevice(c->device));
+      // every pack, replica 0's included: its packed event also follows every
+      // read of the previous composite's image enqueued on devices[0]
+      for (uint32_t k = 0; k < n; k++) HIPCHK(c, hipStreamWaitEvent(c->grp_stream, replica_of(h, k)->grp_packed, 0));
+      size_t p0, p1;
+      shard_range(npx, n, c->replica, &p0, &p1);
+      if (p1 > p0) {
+        CompositeSrc S;
+        memset(&S, 0, sizeof S);
+        S.n = n;
+        for (uint32_t k = 0; k < n; k++) S.p[k] = replica_of(h, k)->grp_pack[b] + p0;
+        HIPCHK(c, launch_composite(S, (uint32_t)(p1 - p0), h->grp_rgb32 + 3 * p0, h->grp_rgba + 4 * p0,
+                                   h->grp_counts + p0, c->grp_stream, true));
+      }
+      HIPCHK(c, hipEventRecord(c->grp_shard, c->grp_stream));
+      return VPTMCM_OK;
+    });
+    if (rc) return rc;
+    HIPCHK(h, hipSetDevice(h->device));
+    for (uint32_t k = 1; k < n; k++) HIPCHK(h, hipStreamWaitEvent(h->grp_stream, h->peers[k - 1]->grp_shard, 0));
+    HIPCHK(h, hipEventRecord(h->grp_done[b], h->grp_stream));
+  } else {
     if (ncclGroupStart() != ncclSuccess) FAIL(h, VPTMCM_ECOMM, "composite: ncclGroupStart failed");
     ncclResult_t r = ncclSuccess;
     for (uint32_t k = 0; k < n && r == ncclSuccess; k++) {
-      vptmcm* c = k ? h->peers[k - 1] : h;
-      r = ncclReduce(c->grp_pack, k ? c->grp_pack : h->grp_gather, npx * 4, ncclFloat32, ncclSum, 0,
+      vptmcm* c = replica_of(h, k);
+      r = ncclReduce(c->grp_pack[0], k ? c->grp_pack[0] : h->grp_gather, npx * 4, ncclFloat32, ncclSum, 0,
                      h->grp_comms[k], enq(c));
     }
     const ncclResult_t re = ncclGroupEnd();
     if (r != ncclSuccess || re != ncclSuccess)
       FAIL(h, VPTMCM_ECOMM, "composite: ncclReduce: %s", ncclGetErrorString(r != ncclSuccess ? r : re));
     HIPCHK(h, hipSetDevice(h->device));
+    CompositeSrc S;
+    memset(&S, 0, sizeof S);
     S.n = 1;
     S.p[0] = h->grp_gather;
-  } else {
-    HIPCHK(h, hipSetDevice(h->device));
-    S.n = n;
-    S.p[0] = h->grp_pack;
-    for (uint32_t k = 1; k < n; k++) {  // every peer's push has landed
-      HIPCHK(h, hipStreamWaitEvent(enq(h), h->peers[k - 1]->grp_packed, 0));
-      S.p[k] = h->grp_gather + (size_t)(k - 1) * npx;
-    }
+    HIPCHK(h, launch_composite(S, (uint32_t)npx, h->grp_rgb32, h->grp_rgba, nullptr, enq(h)));
+    HIPCHK(h, hipEventRecord(h->grp_done[b], enq(h)));
   }
-  HIPCHK(h, launch_composite(S, (uint32_t)npx, h->grp_rgb32, h->grp_rgba, nullptr, enq(h)));
-  HIPCHK(h, hipEventRecord(h->grp_done, enq(h)));
+  h->grp_seq++;
+  h->grp_last = (int)b;
   h->grp_dirty = false;
+  if (VPT_GUARD) return for_replicas(h, [&](vptmcm* c) { return guard_check(c, "composite"); });
+  return VPTMCM_OK;
+}
+
+// Before a read of the composite on replica 0's stream: make it if a march or
+// reset ran since the last one, and order the stream behind it.
+static int composite_ready(vptmcm* h) {
+  if (h->grp_dirty || h->grp_last < 0)
+    if (int rc = group_composite(h)) return rc;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamWaitEvent(enq(h), h->grp_done[h->grp_last], 0));
   return VPTMCM_OK;
 }
 
@@ -1302,37 +1480,37 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
     }                                                                \
   } while (0)
   CK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-  CK(hipMalloc(&h->photons, (size_t)kNumPlanes * h->npad * sizeof(float)));
+  CK(dev_alloc(&h->photons, (size_t)kNumPlanes * h->npad * sizeof(float)));
   CK(hipMemsetAsync(h->photons, 0, (size_t)kNumPlanes * h->npad * sizeof(float), enq(h)));
-  CK(hipMalloc(&h->rgba, (size_t)h->R * h->R * 4 * sizeof(uint16_t)));
+  CK(dev_alloc(&h->rgba, (size_t)h->R * h->R * 4 * sizeof(uint16_t)));
   CK(hipMemsetAsync(h->rgba, 0, (size_t)h->R * h->R * 4 * sizeof(uint16_t), enq(h)));
-  CK(hipMalloc(&h->rgb32, (size_t)h->R * h->R * 3 * sizeof(float)));
+  CK(dev_alloc(&h->rgb32, (size_t)h->R * h->R * 3 * sizeof(float)));
   CK(hipMemsetAsync(h->rgb32, 0, (size_t)h->R * h->R * 3 * sizeof(float), enq(h)));
-  CK(hipMalloc(&h->tf_rg, 65536 * sizeof(uint16_t)));
+  CK(dev_alloc(&h->tf_rg, 65536 * sizeof(uint16_t)));
   CK(hipMemsetAsync(h->tf_rg, 0, 65536 * sizeof(uint16_t), enq(h)));  // zero texture, js:85
-  CK(hipMalloc(&h->tf_b4, kTfCells * kTfCells * sizeof(uint32_t)));
+  CK(dev_alloc(&h->tf_b4, kTfCells * kTfCells * sizeof(uint32_t)));
   CK(hipMemsetAsync(h->tf_b4, 0, kTfCells * kTfCells * sizeof(uint32_t), enq(h)));
-  CK(hipMalloc(&h->tf_brow, 256));
+  CK(dev_alloc(&h->tf_brow, 256));
   CK(hipMemsetAsync(h->tf_brow, 0, 256, enq(h)));
-  CK(hipMalloc(&h->tf_rows, kTfRowsMax * 256 * sizeof(uint32_t)));
+  CK(dev_alloc(&h->tf_rows, kTfRowsMax * 256 * sizeof(uint32_t)));
   CK(hipMemsetAsync(h->tf_rows, 0, kTfRowsMax * 256 * sizeof(uint32_t), enq(h)));
-  CK(hipMalloc(&h->bin_lut, sizeof h->bin_lut_host));
+  CK(dev_alloc(&h->bin_lut, sizeof h->bin_lut_host));
   CK(hipMemsetAsync(h->bin_lut, 0, sizeof h->bin_lut_host, enq(h)));
-  CK(hipMalloc(&h->tf_rowmap, 256));
+  CK(dev_alloc(&h->tf_rowmap, 256));
   CK(hipMemsetAsync(h->tf_rowmap, 0, 256, enq(h)));
-  CK(hipMalloc(&h->light, 256));
+  CK(dev_alloc(&h->light, 256));
   CK(hipMemsetAsync(h->light, 0, 256, enq(h)));
-  CK(hipMalloc(&h->tf_rgb, kRgbTfMax * sizeof(float4)));
-  CK(hipMalloc(&h->sched, 2 * (size_t)sched_flag_bytes(h->n_tiles)));
+  CK(dev_alloc(&h->tf_rgb, kRgbTfMax * sizeof(float4)));
+  CK(dev_alloc(&h->sched, 2 * (size_t)sched_flag_bytes(h->n_tiles)));
   CK(hipMemsetAsync(h->sched, 0, 2 * (size_t)sched_flag_bytes(h->n_tiles), enq(h)));
-  CK(hipMalloc(&h->sched_prev, sched_slot_words(h->n_tiles) * sizeof(uint32_t)));
+  CK(dev_alloc(&h->sched_prev, sched_slot_words(h->n_tiles) * sizeof(uint32_t)));
   CK(hipMemsetAsync(h->sched_prev, 0xff, sched_slot_words(h->n_tiles) * sizeof(uint32_t), enq(h)));
-  CK(hipMalloc(&h->sched_changed, 2 * sizeof(uint32_t)));
+  CK(dev_alloc(&h->sched_changed, 2 * sizeof(uint32_t)));
   CK(hipMemsetAsync(h->sched_changed, 0, 2 * sizeof(uint32_t), enq(h)));
   if (const char* v = getenv("VPTMCM_DARK")) h->dark = v[0] == '0' ? 0u : 1u;
   if (const char* v = getenv("VPTMCM_DONE_FLAG")) h->done_on = v[0] != '0';
   if (const char* v = getenv("VPTMCM_SCHED_CACHE")) h->sched_cache = v[0] != '0';
-  CK(hipMalloc(&h->done_ctr, sizeof(uint32_t)));
+  CK(dev_alloc(&h->done_ctr, sizeof(uint32_t)));
   CK(hipMemsetAsync(h->done_ctr, 0, sizeof(uint32_t), enq(h)));
   // the flag word in fine-grained host memory; without it, synchronize waits
   // for the stream (the signal is an optimisation, never a requirement)
@@ -1361,6 +1539,7 @@ void vptmcm_destroy(vptmcm* h) {
   // communicator, so their waits are plain stream waits).
   for (vptmcm* c : h->peers) {
     if (c->stream) (void)wait_stream(c, c->stream, "destroy");
+    if (c->grp_stream) (void)wait_stream(c, c->grp_stream, "destroy");
   }
   // Bounded waits while a communicator exists or after its abort; streams that
   // did not drain may still touch the handle's buffers (a composite kernel and
@@ -1370,6 +1549,7 @@ void vptmcm_destroy(vptmcm* h) {
   bool drained = true;
   if (h->comm_stream) drained = wait_stream(h, h->comm_stream, "destroy") == VPTMCM_OK && drained;
   if (h->stream) drained = wait_stream(h, h->stream, "destroy") == VPTMCM_OK && drained;
+  if (h->grp_stream) drained = wait_stream(h, h->grp_stream, "destroy") == VPTMCM_OK && drained;
   for (ncclComm_t c : h->grp_comms)
     if (c) (void)ncclCommDestroy(c);
   h->grp_comms.clear();
@@ -1377,10 +1557,16 @@ void vptmcm_destroy(vptmcm* h) {
     (void)ncclCommDestroy(h->comm);
   for (vptmcm* c : h->peers) {
     if (drained) {  // a peer's pack may be read by this handle's (undrained) composite
-      if (c->grp_pack) (void)hipFree(c->grp_pack);
+      (void)hipSetDevice(c->device);
+      for (auto& p : c->grp_pack) {
+        if (p) (void)dev_free(p);
+        p = nullptr;
+      }
       if (c->grp_packed) (void)hipEventDestroy(c->grp_packed);
-      c->grp_pack = nullptr;
-      c->grp_packed = nullptr;
+      if (c->grp_shard) (void)hipEventDestroy(c->grp_shard);
+      if (c->grp_stream) (void)hipStreamDestroy(c->grp_stream);
+      c->grp_packed = c->grp_shard = nullptr;
+      c->grp_stream = nullptr;
     }
     vptmcm_destroy(c);
   }
@@ -1391,43 +1577,48 @@ void vptmcm_destroy(vptmcm* h) {
     return;
   }
   (void)hipSetDevice(h->device);
-  if (h->grp_pack) (void)hipFree(h->grp_pack);
+  for (auto p : h->grp_pack)
+    if (p) (void)dev_free(p);
   if (h->grp_packed) (void)hipEventDestroy(h->grp_packed);
-  if (h->grp_gather) (void)hipFree(h->grp_gather);
-  if (h->grp_rgb32) (void)hipFree(h->grp_rgb32);
-  if (h->grp_rgba) (void)hipFree(h->grp_rgba);
-  if (h->grp_done) (void)hipEventDestroy(h->grp_done);
-  if (h->comp_rgb32) (void)hipFree(h->comp_rgb32);
-  if (h->comp_rgba) (void)hipFree(h->comp_rgba);
-  if (h->comp_counts) (void)hipFree(h->comp_counts);
-  if (h->band_cover) (void)hipFree(h->band_cover);
+  if (h->grp_shard) (void)hipEventDestroy(h->grp_shard);
+  if (h->grp_gather) (void)dev_free(h->grp_gather);
+  if (h->grp_rgb32) (void)dev_free(h->grp_rgb32);
+  if (h->grp_rgba) (void)dev_free(h->grp_rgba);
+  if (h->grp_counts) (void)dev_free(h->grp_counts);
+  for (auto e : h->grp_done)
+    if (e) (void)hipEventDestroy(e);
+  if (h->comp_rgb32) (void)dev_free(h->comp_rgb32);
+  if (h->comp_rgba) (void)dev_free(h->comp_rgba);
+  if (h->comp_counts) (void)dev_free(h->comp_counts);
+  if (h->band_cover) (void)dev_free(h->band_cover);
   for (int k = 0; k < 2; k++) {
-    if (h->comp[k]) (void)hipFree(h->comp[k]);
+    if (h->comp[k]) (void)dev_free(h->comp[k]);
     if (h->comp_ready[k]) (void)hipEventDestroy(h->comp_ready[k]);
     if (h->comp_done[k]) (void)hipEventDestroy(h->comp_done[k]);
   }
-  if (h->host_scratch) (void)hipFree(h->host_scratch);
+  if (h->host_scratch) (void)dev_free(h->host_scratch);
   if (h->region.beg) (void)hipEventDestroy(h->region.beg);
   if (h->region.end) (void)hipEventDestroy(h->region.end);
   free_volume(h);
-  if (h->photons) (void)hipFree(h->photons);
-  if (h->rgba) (void)hipFree(h->rgba);
-  if (h->rgb32) (void)hipFree(h->rgb32);
-  if (h->ldr) (void)hipFree(h->ldr);
-  if (h->tf_rgb) (void)hipFree(h->tf_rgb);
-  if (h->tf_rg) (void)hipFree(h->tf_rg);
-  if (h->tf_b4) (void)hipFree(h->tf_b4);
-  if (h->tf_brow) (void)hipFree(h->tf_brow);
-  if (h->tf_rows) (void)hipFree(h->tf_rows);
-  if (h->tf_rowmap) (void)hipFree(h->tf_rowmap);
-  if (h->bin_lut) (void)hipFree(h->bin_lut);
-  if (h->light) (void)hipFree(h->light);
-  if (h->sched) (void)hipFree(h->sched);
-  if (h->sched_prev) (void)hipFree(h->sched_prev);
-  if (h->sched_changed) (void)hipFree(h->sched_changed);
-  if (h->done_ctr) (void)hipFree(h->done_ctr);
+  if (h->photons) (void)dev_free(h->photons);
+  if (h->rgba) (void)dev_free(h->rgba);
+  if (h->rgb32) (void)dev_free(h->rgb32);
+  if (h->ldr) (void)dev_free(h->ldr);
+  if (h->tf_rgb) (void)dev_free(h->tf_rgb);
+  if (h->tf_rg) (void)dev_free(h->tf_rg);
+  if (h->tf_b4) (void)dev_free(h->tf_b4);
+  if (h->tf_brow) (void)dev_free(h->tf_brow);
+  if (h->tf_rows) (void)dev_free(h->tf_rows);
+  if (h->tf_rowmap) (void)dev_free(h->tf_rowmap);
+  if (h->bin_lut) (void)dev_free(h->bin_lut);
+  if (h->light) (void)dev_free(h->light);
+  if (h->sched) (void)dev_free(h->sched);
+  if (h->sched_prev) (void)dev_free(h->sched_prev);
+  if (h->sched_changed) (void)dev_free(h->sched_changed);
+  if (h->done_ctr) (void)dev_free(h->done_ctr);
   if (h->done_host) (void)hipHostFree(h->done_host);
   if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
+  if (h->grp_stream) (void)hipStreamDestroy(h->grp_stream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -1451,7 +1642,7 @@ static int volume_begin_one(vptmcm* h, uint32_t width, uint32_t height, uint32_t
   HIPCHK(h, hipStreamSynchronize(h->stream));
   free_volume(h);
   size_t n = (size_t)width * height * depth;
-  if (hipMalloc(&h->vol_lin, n) != hipSuccess) {
+  if (dev_alloc(&h->vol_lin, n) != hipSuccess) {
     h->vol_lin = nullptr;
     FAIL(h, VPTMCM_ENOMEM, "volume allocation of %zu bytes failed", n);
   }
@@ -1471,7 +1662,7 @@ static int volume_begin_one(vptmcm* h, uint32_t width, uint32_t height, uint32_t
     // hipDeviceMallocContiguous), bought nothing and is gone: in round 5 the
     // knob test found that once such an allocation had been freed, later
     // handles in the process rendered wrong bits)
-    if (hipMalloc(&h->vol_c8, ncell * 8) != hipSuccess) {
+    if (dev_alloc(&h->vol_c8, ncell * 8) != hipSuccess) {
       h->vol_c8 = nullptr;
       free_volume(h);
       FAIL(h, VPTMCM_ENOMEM, "%s volume allocation of %zu bytes failed",
@@ -1537,7 +1728,7 @@ static int volume_end_one(vptmcm* h) {
   if (int rc = flush_relayout(h)) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->layout != kLayoutLinear) {  // every cell is current: the staging copy goes
-    HIPCHK(h, hipFree(h->vol_lin));
+    HIPCHK(h, dev_free(h->vol_lin));
     h->vol_lin = nullptr;
   } else {
     h->vol_done = true;  // LINEAR: the staging copy is the volume
@@ -1723,7 +1914,7 @@ static int reset_one(vptmcm* h, const float* mvp, uint32_t seed_bits) {
   else
     HIPCHK(h, launch_reset(P, h->photons, enq(h)));
   h->grp_dirty = true;
-  return VPTMCM_OK;
+  return guard_check(h, "reset");
 }
 
 static int render_one(vptmcm* h, const float* mvp, uint32_t seed_bits) {
@@ -1776,7 +1967,8 @@ static int synchronize_one(vptmcm* h) {
   }
   if (!done && (rc = wait_stream(h, h->stream, "synchronize"))) return rc;
   if (h->comm_stream && (rc = wait_stream(h, h->comm_stream, "synchronize"))) return rc;
-  return VPTMCM_OK;
+  if (h->grp_stream && (rc = wait_stream(h, h->grp_stream, "synchronize"))) return rc;
+  return guard_check(h, "synchronize");
 }
 
 // ------------------------------------------------------------------ outputs
@@ -1785,8 +1977,8 @@ int vptmcm_read_rgba16f(vptmcm* h, uint16_t* out) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!out) FAIL(h, VPTMCM_EINVAL, "read_rgba16f: null output");
-  if (composited(h) && h->grp_dirty)
-    if (int rc = group_composite(h)) return rc;
+  if (composited(h))
+    if (int rc = composite_ready(h)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipMemcpyAsync(out, composited(h) ? h->grp_rgba : h->rgba, (size_t)h->R * h->R * 8,
                            hipMemcpyDeviceToHost, enq(h)));
@@ -1798,8 +1990,8 @@ int vptmcm_read_rgb(vptmcm* h, float* out) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!out) FAIL(h, VPTMCM_EINVAL, "read_rgb: null output");
-  if (composited(h) && h->grp_dirty)
-    if (int rc = group_composite(h)) return rc;
+  if (composited(h))
+    if (int rc = composite_ready(h)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipMemcpyAsync(out, composited(h) ? h->grp_rgb32 : h->rgb32,
                            (size_t)h->R * h->R * 3 * sizeof(float), hipMemcpyDeviceToHost, enq(h)));
@@ -1814,12 +2006,12 @@ int vptmcm_pack_radiance(vptmcm* h, float* out) {
   HIPCHK(h, hipSetDevice(h->device));
   const size_t bytes = (size_t)h->R * h->R * sizeof(float4);
   float4* d = nullptr;
-  HIPCHK(h, hipMalloc(&d, bytes));
+  HIPCHK(h, dev_alloc(&d, bytes));
   MarchParams P = make_params(h, kNoMatrix, 0);
   hipError_t e = launch_pack(P, h->photons, h->rgb32, d, enq(h));
   if (e == hipSuccess) e = hipMemcpyAsync(out, d, bytes, hipMemcpyDeviceToHost, enq(h));
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-  (void)hipFree(d);
+  (void)dev_free(d);
   if (e != hipSuccess) FAIL(h, VPTMCM_EHIP, "pack_radiance: %s", hipGetErrorString(e));
   return VPTMCM_OK;
 }
@@ -1828,11 +2020,11 @@ int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!params) FAIL(h, VPTMCM_EINVAL, "tonemap_artistic: null params");
-  if (composited(h) && h->grp_dirty)
-    if (int rc = group_composite(h)) return rc;
+  if (composited(h))
+    if (int rc = composite_ready(h)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
   const size_t npx = (size_t)h->R * h->R;
-  if (!h->ldr) HIPCHK(h, hipMalloc(&h->ldr, npx * 4));
+  if (!h->ldr) HIPCHK(h, dev_alloc(&h->ldr, npx * 4));
   // uniform-only terms in f32, as the shader evaluates them once per fragment
   const float low = params[0], mid = params[1], high = params[2];
   const float range = high - low;
@@ -2079,12 +2271,12 @@ int vptmcm_comm_init(vptmcm* h, const uint8_t* uid, int nranks, int rank) {
   HIPCHK(h, hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking));
   size_t bytes = (size_t)h->R * h->R * sizeof(float4);
   for (int k = 0; k < 2; k++) {
-    HIPCHK(h, hipMalloc(&h->comp[k], bytes));
+    HIPCHK(h, dev_alloc(&h->comp[k], bytes));
     HIPCHK(h, hipEventCreateWithFlags(&h->comp_ready[k], hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&h->comp_done[k], hipEventDisableTiming));
     HIPCHK(h, hipEventRecord(h->comp_done[k], h->comm_stream));
   }
-  HIPCHK(h, hipMalloc(&h->host_scratch, 64 * sizeof(double)));
+  HIPCHK(h, dev_alloc(&h->host_scratch, 64 * sizeof(double)));
   return VPTMCM_OK;
 }
 
@@ -2126,29 +2318,22 @@ int vptmcm_read_composite(vptmcm* h, uint16_t* rgba16f, float* rgb, float* count
   if (int rc_ = flush_renders(h)) return rc_;
   const size_t npx = (size_t)h->R * h->R;
   if (h->grouped) {  // a device-list handle: over its replicas (N = 1 included)
-    if (h->grp_dirty || !h->grp_rgb32) {
-      if (!h->grp_rgb32) {  // one replica, PEER: the buffers of the composite on first use
-        const int32_t dev = h->device;
-        if (int rc = group_alloc(h, &dev, 1)) return rc;
-      }
-      if (int rc = group_composite(h)) return rc;
+    if (!h->grp_rgb32) {  // one replica, PEER: the buffers of the composite on first use
+      const int32_t dev = h->device;
+      if (int rc = group_alloc(h, &dev, 1)) return rc;
     }
-    HIPCHK(h, hipSetDevice(h->device));
-    if (counts) {  // sum(n): the composite kernel again, counts only (cheap, same order)
-      CompositeSrc S;
-      memset(&S, 0, sizeof S);
+    if (int rc = composite_ready(h)) return rc;
+    if (counts) {  // sum(n): PEER's shards wrote it; RCCL: the composite kernel on the sum, counts only
       if (h->group_transport == VPTMCM_GROUP_RCCL) {
+        CompositeSrc S;
+        memset(&S, 0, sizeof S);
         S.n = 1;
         S.p[0] = h->grp_gather;
-      } else {
-        S.n = 1u + (uint32_t)h->peers.size();
-        S.p[0] = h->grp_pack;
-        for (uint32_t k = 1; k < S.n; k++) S.p[k] = h->grp_gather + (size_t)(k - 1) * npx;
+        if (!h->comp_counts) HIPCHK(h, dev_alloc(&h->comp_counts, npx * sizeof(float)));
+        HIPCHK(h, launch_composite(S, (uint32_t)npx, nullptr, nullptr, h->comp_counts, enq(h)));
       }
-      if (!h->comp_counts) HIPCHK(h, hipMalloc(&h->comp_counts, npx * sizeof(float)));
-      HIPCHK(h, launch_composite(S, (uint32_t)npx, nullptr, nullptr, h->comp_counts, enq(h)));
-      HIPCHK(h, hipMemcpyAsync(counts, h->comp_counts, npx * sizeof(float), hipMemcpyDeviceToHost,
-                               enq(h)));
+      HIPCHK(h, hipMemcpyAsync(counts, h->group_transport == VPTMCM_GROUP_RCCL ? h->comp_counts : h->grp_counts,
+                               npx * sizeof(float), hipMemcpyDeviceToHost, enq(h)));
     }
     if (rgba16f)
       HIPCHK(h, hipMemcpyAsync(rgba16f, h->grp_rgba, npx * 8, hipMemcpyDeviceToHost, enq(h)));
@@ -2161,9 +2346,9 @@ int vptmcm_read_composite(vptmcm* h, uint16_t* rgba16f, float* rgb, float* count
     FAIL(h, VPTMCM_ESTATE, "read_composite: no all-reduce issued (and not a device-list handle)");
   HIPCHK(h, hipSetDevice(h->device));
   // on the composite stream, behind the last all-reduce (the march stream keeps running)
-  if (!h->comp_rgb32) HIPCHK(h, hipMalloc(&h->comp_rgb32, npx * 3 * sizeof(float)));
-  if (!h->comp_rgba) HIPCHK(h, hipMalloc(&h->comp_rgba, npx * 4 * sizeof(uint16_t)));
-  if (!h->comp_counts) HIPCHK(h, hipMalloc(&h->comp_counts, npx * sizeof(float)));
+  if (!h->comp_rgb32) HIPCHK(h, dev_alloc(&h->comp_rgb32, npx * 3 * sizeof(float)));
+  if (!h->comp_rgba) HIPCHK(h, dev_alloc(&h->comp_rgba, npx * 4 * sizeof(uint16_t)));
+  if (!h->comp_counts) HIPCHK(h, dev_alloc(&h->comp_counts, npx * sizeof(float)));
   CompositeSrc S;
   memset(&S, 0, sizeof S);
   S.n = 1;
@@ -2190,7 +2375,7 @@ int vptmcm_comm_gather_bands(vptmcm* h, float* rgb) {
   int rc = 0;
   // The bands must tile the frame: every 8-row tile covered by exactly one rank.
   const uint32_t ty = (h->R + 7) / 8;
-  if (!h->band_cover) HIPCHK(h, hipMalloc(&h->band_cover, ty * sizeof(uint32_t)));
+  if (!h->band_cover) HIPCHK(h, dev_alloc(&h->band_cover, ty * sizeof(uint32_t)));
   std::vector<uint32_t> cover(ty, 0u);
   for (uint32_t t = h->band_y0 / 8; t < (h->band_y1 + 7) / 8; t++) cover[t] = 1u;
   HIPCHK(h, hipMemcpyAsync(h->band_cover, cover.data(), ty * sizeof(uint32_t), hipMemcpyHostToDevice,
@@ -2283,17 +2468,17 @@ int vptmcm_debug_eval(vptmcm* h, int fn, const uint32_t* in, uint32_t* out, uint
   if (n == 0) return VPTMCM_OK;
   HIPCHK(h, hipSetDevice(h->device));
   uint32_t *din = nullptr, *dout = nullptr;
-  HIPCHK(h, hipMalloc(&din, (size_t)n * 4));
-  if (hipMalloc(&dout, (size_t)n * 4) != hipSuccess) {
-    (void)hipFree(din);
+  HIPCHK(h, dev_alloc(&din, (size_t)n * 4));
+  if (dev_alloc(&dout, (size_t)n * 4) != hipSuccess) {
+    (void)dev_free(din);
     FAIL(h, VPTMCM_ENOMEM, "debug_eval: allocation failed");
   }
   hipError_t e = hipMemcpy(din, in, (size_t)n * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = launch_debug_eval(fn, din, dout, n, enq(h));
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost);
-  (void)hipFree(din);
-  (void)hipFree(dout);
+  (void)dev_free(din);
+  (void)dev_free(dout);
   if (e != hipSuccess) FAIL(h, VPTMCM_EHIP, "debug_eval: %s", hipGetErrorString(e));
   return VPTMCM_OK;
 }
@@ -2306,8 +2491,8 @@ int vptmcm_debug_verify(vptmcm* h, int fn, uint32_t lo, uint64_t count, uint64_t
   HIPCHK(h, hipSetDevice(h->device));
   unsigned long long* dbad = nullptr;
   uint32_t* dfirst = nullptr;
-  HIPCHK(h, hipMalloc(&dbad, sizeof(unsigned long long)));
-  HIPCHK(h, hipMalloc(&dfirst, (nfirst ? nfirst : 1) * sizeof(uint32_t)));
+  HIPCHK(h, dev_alloc(&dbad, sizeof(unsigned long long)));
+  HIPCHK(h, dev_alloc(&dfirst, (nfirst ? nfirst : 1) * sizeof(uint32_t)));
   HIPCHK(h, hipMemsetAsync(dbad, 0, sizeof(unsigned long long), enq(h)));
   uint64_t done = 0;
   hipError_t e = hipSuccess;
@@ -2322,8 +2507,8 @@ int vptmcm_debug_verify(vptmcm* h, int fn, uint32_t lo, uint64_t count, uint64_t
   if (e == hipSuccess) e = hipMemcpy(&nb, dbad, sizeof nb, hipMemcpyDeviceToHost);
   if (e == hipSuccess && nfirst)
     e = hipMemcpy(first_bad, dfirst, (size_t)nfirst * sizeof(uint32_t), hipMemcpyDeviceToHost);
-  (void)hipFree(dbad);
-  (void)hipFree(dfirst);
+  (void)dev_free(dbad);
+  (void)dev_free(dfirst);
   if (e != hipSuccess) FAIL(h, VPTMCM_EHIP, "debug_verify: %s", hipGetErrorString(e));
   *mismatches = nb;
   return VPTMCM_OK;
