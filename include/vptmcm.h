@@ -64,8 +64,11 @@ extern "C" {
 /* Multi-device handles (one process driving several GPUs, SURVEY 8(b)
  * "device list/mode"): how the replicas' radiance is composited. */
 #define VPTMCM_MAX_DEVICES 8
-#define VPTMCM_GROUP_PEER 0 /* ordered xGMI peer gather to devices[0] + k_composite (deterministic;
-                               a device may repeat: replicas then share a GPU)     */
+#define VPTMCM_GROUP_PEER 0 /* sharded over xGMI peer access: replica k sums pixel shard k of
+                               every replica's (rgb*n, n) in replica order on its own device and
+                               writes that slice of the composite into devices[0] (deterministic;
+                               needs peer access between every pair of distinct devices; a device
+                               may repeat: replicas then share a GPU)              */
 #define VPTMCM_GROUP_RCCL 1 /* ncclCommInitAll over the (distinct) devices, grouped ncclReduce to
                                devices[0] + k_composite (RCCL's summation order)   */
 

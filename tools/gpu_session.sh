@@ -121,6 +121,12 @@ for s in $STEPS; do
       python3 -c "import json; d=json.load(open('$OUT/dark_$d.json')); e=json.load(open('$OUT/darkd_$d.json')); print(json.dumps({'dark': '$d', 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'unfused_us': d['unfused']['kernel_avg_us'], 'drv_value': e['value'], 'drv_kernel_us': e['roofline']['kernel_avg_us']}))" >> $OUT/darkab.jsonl
     done
     echo "darkab rc=0" | tee -a $OUT/status.txt; cat $OUT/darkab.jsonl ;;
+  groupcomp)  # device-list composite: host enqueue behind the march, then the device chain under a kernel trace
+    timeout -k 10 300 python tools/group_enqueue.py --ns 2 4 8 --reps 30 --composite > $OUT/group_enqueue.jsonl 2> $OUT/group_enqueue.err
+    rc=$?; echo "groupcomp enqueue rc=$rc" | tee -a $OUT/status.txt; cat $OUT/group_enqueue.jsonl; fault $rc && exit $rc
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$OUT/groupprof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/group_enqueue.py" --ns 8 --reps 20 --composite --threads on > "$GRAFT_REPO_ROOT/$OUT/groupprof.jsonl" 2> "$GRAFT_REPO_ROOT/$OUT/groupprof.err")
+    rc=$?; echo "groupcomp prof rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
+    python3 tools/composite_trace.py $(ls $OUT/groupprof/*/run_kernel_trace.csv $OUT/groupprof/run_kernel_trace.csv 2>/dev/null | head -1) > $OUT/composite_trace.json 2>&1; cat $OUT/composite_trace.json ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)

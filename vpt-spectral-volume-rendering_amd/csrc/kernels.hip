@@ -1381,36 +1381,21 @@ __global__ __launch_bounds__(256) void k_pack(const MarchParams P, const float* 
 
 // Coherent access for the sharded device-list composite (COH): a shard kernel
 // on device K reads the other replicas' packs in their devices' memory and
-// writes its slice of the image into devices[0]'s memory over xGMI. Relaxed
-// system-scope atomic loads / stores (global_load / global_store with sc0 sc1
-// on gfx950) bypass the non-coherent caching of remote lines in K's L2, so
-// the shard sees exactly what each pack kernel left in memory (its event, a
-// system-scope release, precedes the shard kernel's cross-device wait) and its
-// stores reach devices[0]'s memory before its own completion event, whatever
-// the acquire / release scope of the dispatch packets.
-template <bool COH>
-__device__ __forceinline__ float ld_f(const float* p) {
-  if constexpr (COH)
-    return __uint_as_float(__hip_atomic_load(reinterpret_cast<uint32_t*>(const_cast<float*>(p)),
-                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-  else
-    return *p;
-}
-template <bool COH>
-__device__ __forceinline__ float4 ld_f4(const float4* p) {
-  if constexpr (COH) {
-    const float* f = reinterpret_cast<const float*>(p);
-    return make_float4(ld_f<true>(f), ld_f<true>(f + 1), ld_f<true>(f + 2), ld_f<true>(f + 3));
-  } else {
-    return *p;
-  }
-}
-template <bool COH>
-__device__ __forceinline__ void st_u(uint32_t* p, uint32_t v) {
-  if constexpr (COH)
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  else
-    *p = v;
+// writes its slice of the image into devices[0]'s memory over xGMI. Raw buffer
+// loads / stores with sc0 sc1 (system scope) bypass the non-coherent caching
+// of remote lines in K's L2, so the shard sees exactly what each pack kernel
+// left in memory (its event, a system-scope release, precedes the shard
+// kernel's cross-device wait) and its stores reach devices[0]'s memory before
+// its completion event, whatever the acquire / release scope of the dispatch
+// packets. Whole-pixel accesses (16-B loads, 12 / 8 / 4-B stores per pixel),
+// so a wave's requests coalesce into full lines over the link.
+constexpr int kCpolSystem = 1 | 16;  // cache-policy bits sc0 | sc1 (gfx950)
+constexpr int kRsrcWord3 = 0x00020000;  // raw buffer resource, 32-bit data format
+typedef float vf4 __attribute__((ext_vector_type(4)));
+typedef float vf3 __attribute__((ext_vector_type(3)));
+typedef uint32_t vu2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t coherent_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, kRsrcWord3);
 }
 
 // The composite of R^2 (rgb*n, n) float4 buffers (k_pack's, one per replica,
@@ -1427,29 +1412,54 @@ __global__ __launch_bounds__(256) void k_composite(const CompositeSrc S, uint32_
                                                    float* __restrict__ counts) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= npx) return;
-  float4 s = ld_f4<COH>(S.p[0] + i);
-  for (uint32_t k = 1; k < S.n; k++) {
-    const float4 t = ld_f4<COH>(S.p[k] + i);
-    s.x += t.x;
-    s.y += t.y;
-    s.z += t.z;
-    s.w += t.w;
+  auto ld = [&](uint32_t k) {
+    if constexpr (COH) {
+      const vf4 v = __builtin_amdgcn_raw_buffer_load_b128(coherent_rsrc(S.p[k], npx * 16u), i * 16u, 0,
+                                                          kCpolSystem);
+      return make_float4(v.x, v.y, v.z, v.w);
+    } else {
+      return S.p[k][i];
+    }
+  };
+  // every source's load issued before the first add (remote latency overlaps),
+  // then the sums in source order
+  float4 t[kMaxReplicas];
+#pragma unroll
+  for (uint32_t k = 0; k < kMaxReplicas; k++)
+    if (k < S.n) t[k] = ld(k);
+  float4 s = t[0];
+#pragma unroll
+  for (uint32_t k = 1; k < kMaxReplicas; k++) {
+    if (k < S.n) {
+      s.x += t[k].x;
+      s.y += t[k].y;
+      s.z += t[k].z;
+      s.w += t[k].w;
+    }
   }
   const float n = s.w;
   const bool any = n > 0.0f;
   const float r = any ? s.x / n : 0.0f, g = any ? s.y / n : 0.0f, b = any ? s.z / n : 0.0f;
-  if (rgb32) {
-    uint32_t* o = reinterpret_cast<uint32_t*>(rgb32) + 3u * i;
-    st_u<COH>(o, __float_as_uint(r));
-    st_u<COH>(o + 1, __float_as_uint(g));
-    st_u<COH>(o + 2, __float_as_uint(b));
+  const uint32_t h0 = (uint32_t)f2h(r) | ((uint32_t)f2h(g) << 16), h1 = (uint32_t)f2h(b) | (0x3c00u << 16);
+  if constexpr (COH) {
+    if (rgb32) {
+      const vf3 v = {r, g, b};
+      __builtin_amdgcn_raw_buffer_store_b96(v, coherent_rsrc(rgb32, npx * 12u), i * 12u, 0, kCpolSystem);
+    }
+    if (rgba) {
+      const vu2 v = {h0, h1};
+      __builtin_amdgcn_raw_buffer_store_b64(v, coherent_rsrc(rgba, npx * 8u), i * 8u, 0, kCpolSystem);
+    }
+    if (counts) __builtin_amdgcn_raw_buffer_store_b32(n, coherent_rsrc(counts, npx * 4u), i * 4u, 0, kCpolSystem);
+  } else {
+    if (rgb32) {
+      rgb32[3u * i] = r;
+      rgb32[3u * i + 1u] = g;
+      rgb32[3u * i + 2u] = b;
+    }
+    if (rgba) reinterpret_cast<uint2*>(rgba)[i] = make_uint2(h0, h1);
+    if (counts) counts[i] = n;
   }
-  if (rgba) {
-    uint32_t* o = reinterpret_cast<uint32_t*>(rgba) + 2u * i;
-    st_u<COH>(o, (uint32_t)f2h(r) | ((uint32_t)f2h(g) << 16));
-    st_u<COH>(o + 1, (uint32_t)f2h(b) | (0x3c00u << 16));
-  }
-  if (counts) st_u<COH>(reinterpret_cast<uint32_t*>(counts) + i, __float_as_uint(n));
 }
 
 // ------------------------------------------------------------ tone mapping
