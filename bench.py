@@ -106,6 +106,10 @@ def parse():
                     help="passes of a timed region on the general (non-FAST) march: a UI-like "
                          "TF with wavelength-varying anisotropy and 8 uneven bins (reported as "
                          "'general'; 0 = skip; N = 1 only)")
+    ap.add_argument("--near-steps", type=int, default=256,
+                    help="passes of an analysis region with the golden 'near' camera (the volume fills "
+                         "the frame: every photon-step is an in-volume gather), reported as 'near' with a "
+                         "roofline of its own; 0 = skip; N = 1, default camera only")
     ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (profiles/), if present")
     return ap.parse_args()
@@ -209,6 +213,28 @@ def stdout_to_stderr(fn):
         ctypes.CDLL(None).fflush(None)  # C stdio buffers, before fd 1 is restored
         os.dup2(saved, 1)
         os.close(saved)
+
+
+def pmc_entry(a, R: int, S: int, shapes: list, camera: str):
+    """The PMC passes' entry (profiles/pmc_traffic.json, tools/pmc_report.py) of
+    exactly this launch shape — R, S, layout, volume, passes per launch,
+    camera — with the benchmark TF and bins, or None."""
+    tp = Path(a.traffic_json)
+    if not tp.exists() or len(shapes) != 1 or a.tf != "spectral" or a.bins != "12":
+        return None
+    try:
+        t = json.loads(tp.read_text())
+    except (ValueError, OSError):
+        return None
+    for e in t.get("entries", [t]):
+        if (e.get("resolution") == R and e.get("steps") == S and e.get("layout") == a.layout
+                and e.get("volume", 512) == a.volume and e.get("passes_per_launch", 1) == shapes[0]
+                and e.get("camera", "default") == camera):
+            e = dict(e)
+            e["_source"] = f"{tp.relative_to(REPO) if tp.is_relative_to(REPO) else tp}"
+            e["_gather_peak"] = t.get("gather_peak")
+            return e
+    return None
 
 
 def group_devices(n: int) -> list:
@@ -488,6 +514,60 @@ def main():
                       "note": "one render() call per pass through the C-ABI (ctypes); the "
                               "library fuses queued passes into multi-pass launches"}
 
+    # The volume-filling regime: the golden 'near' camera puts
+    # the volume in front of every pixel, so every photon-step is an in-volume
+    # gather; same volume, TF, bins and launch shape as the main line
+    near = None
+    if a.near_steps > 0 and single and a.camera == "default":
+        r.synchronize()
+        mn = cf.golden_mvp("near")
+        nseeds = cf.seed_stream(a.near_steps + 65, start=3, rank=rank)
+        r.reset(mn, nseeds[0])
+        r.render_passes(mn, nseeds[1:65])  # the photons' depth distribution and the deal settle
+        r.synchronize()
+        r.enable_kernel_timing(not a.no_timing)
+        t6 = time.perf_counter()
+        nl = passes_on(nseeds, 65, a.near_steps)
+        r.synchronize()
+        el6 = time.perf_counter() - t6
+        nk_ms, nn = r.kernel_time()
+        nbytes = sum(cf.algorithmic_bytes_per_launch(R, S, n) for n in nl)
+        nshapes = sorted(set(nl))
+        near = {"value": round(R * R * S * a.near_steps / el6 / 1e6, 3),
+                "ms_per_step": round(el6 * 1e3 / a.near_steps, 5), "steps": a.near_steps,
+                "passes_per_launch": nshapes[0] if len(nshapes) == 1 else nshapes,
+                "kernel_us_per_pass": None, "roofline": None, "gather_roofline": None,
+                "workload": "same volume, TF, bins and launch shape as the main line with the golden "
+                            "'near' camera: the volume fills the frame, every photon-step gathers"}
+        if not a.no_timing:
+            nach = nbytes / (nk_ms * 1e-3) / 1e9
+            near["kernel_us_per_pass"] = round(nk_ms * 1e3 / a.near_steps, 3)
+            near["roofline"] = {"bound": "hbm", "achieved": round(nach, 1), "peak": HBM_PEAK_GBPS,
+                                "unit": "GB/s", "frac": round(nach / HBM_PEAK_GBPS, 4),
+                                "algorithmic_bytes_per_launch": nbytes // len(nl), "traffic": None}
+            ne = pmc_entry(a, R, S, nshapes, "near")
+            if ne is not None:
+                launch_s = nk_ms * 1e-3 / nn
+                fills = ne["read_requests"]["128B"] + ne["read_requests"]["64B"] + ne["read_requests"]["32B"]
+                near["roofline"].update({
+                    "traffic": ne["hbm_bytes_per_launch"], "traffic_source": ne["_source"],
+                    "traffic_gbps": round(ne["hbm_bytes_per_launch"] / launch_s / 1e9, 1),
+                    "traffic_frac": round(ne["hbm_bytes_per_launch"] / launch_s / 1e9 / HBM_PEAK_GBPS, 4)})
+                gp = ne.get("_gather_peak") or {}
+                if gp.get("ggathers_per_s"):
+                    g = fills / launch_s / 1e9
+                    near["gather_roofline"] = {
+                        "bound": "scattered 8-B gathers (one 128-B L2 fill each)", "achieved": round(g, 2),
+                        "peak": gp["ggathers_per_s"], "unit": "G gathers/s",
+                        "frac": round(g / gp["ggathers_per_s"], 4), "peak_source": gp.get("source"),
+                        "fills_per_launch": fills, "fills_source": ne["_source"]}
+                if ne.get("issue"):
+                    iv = ne["issue"]
+                    ach = iv["valu_insts"] / launch_s / 1e9
+                    near["issue"] = {"bound": "valu-issue", "achieved": round(ach, 1), "peak": VALU_PEAK_G,
+                                     "unit": "G wave-instructions/s", "frac": round(ach / VALU_PEAK_G, 4),
+                                     "valu_per_photon_step": iv["valu_per_photon_step"]}
+
     # The launch shape that actually ran (the last launch of a region can be
     # shorter than --fuse, and --steps < --fuse gives one short launch).
     shapes = sorted(set(launches))
@@ -495,31 +575,21 @@ def main():
     # PMC-derived memory-side bytes per launch (profiles/): attached only when a
     # profile of this exact launch shape (R, S, layout, volume, passes) exists.
     traffic, traffic_src, issue = None, None, None
-    tp = Path(a.traffic_json)
-    if tp.exists() and len(shapes) == 1:
-        try:
-            t = json.loads(tp.read_text())
-            for e in t.get("entries", [t]):
-                if (e.get("resolution") == R and e.get("steps") == S and e.get("layout") == a.layout
-                        and e.get("volume", 512) == a.volume
-                        and e.get("passes_per_launch", 1) == shapes[0]
-                        and a.tf == "spectral" and a.camera == "default" and a.bins == "12"):
-                    traffic = e.get("hbm_bytes_per_launch")
-                    traffic_src = f"{tp.relative_to(REPO) if tp.is_relative_to(REPO) else tp}"
-                    # VALU issue roofline: the launch's VALU wave-instructions
-                    # (PMC, same launch shape) over its live duration, against
-                    # 1024 SIMD-32s issuing one wave64 VALU instruction per 2
-                    # cycles at the 2.4 GHz peak clock
-                    iv = e.get("issue")
-                    if iv and not a.no_timing:
-                        ach = iv["valu_insts"] / (kern_avg_ms * 1e-3) / 1e9
-                        issue = {"bound": "valu-issue", "achieved": round(ach, 1),
-                                 "peak": VALU_PEAK_G, "unit": "G wave-instructions/s",
-                                 "frac": round(ach / VALU_PEAK_G, 4),
-                                 "valu_per_photon_step": iv["valu_per_photon_step"],
-                                 "source": traffic_src}
-        except (ValueError, OSError, KeyError):
-            traffic, issue = None, None
+    e = pmc_entry(a, R, S, shapes, a.camera)
+    if e is not None:
+        traffic = e.get("hbm_bytes_per_launch")
+        traffic_src = e["_source"]
+        # VALU issue roofline: the launch's VALU wave-instructions (PMC, same
+        # launch shape) over its live duration, against 1024 SIMD-32s issuing
+        # one wave64 VALU instruction per 2 cycles at the 2.4 GHz peak clock
+        iv = e.get("issue")
+        if iv and not a.no_timing:
+            ach = iv["valu_insts"] / (kern_avg_ms * 1e-3) / 1e9
+            issue = {"bound": "valu-issue", "achieved": round(ach, 1),
+                     "peak": VALU_PEAK_G, "unit": "G wave-instructions/s",
+                     "frac": round(ach / VALU_PEAK_G, 4),
+                     "valu_per_photon_step": iv["valu_per_photon_step"],
+                     "source": traffic_src}
 
     # The march on a UI-like configuration of the same volume: 8 uneven bins and
     # a materials TF with wavelength-varying anisotropy (MODE 6: FAST geometry,
@@ -656,6 +726,7 @@ def main():
             "render_api": render_api,
             "js_api": js_api,
             "general": general,
+            "near": near,
             "rgb": rgb,
             "per_pass_allreduce": per_pass,
             "cpu_baseline": None,

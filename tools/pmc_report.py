@@ -14,7 +14,7 @@ fraction: a wave64 VALU instruction occupies its SIMD-32 for 2 cycles
 (MI355X_MICROARCH.md, wave scheduling), so 1024 SIMDs issue at most
 512 wave-instructions per cycle.
 
-Usage: python tools/pmc_report.py <pmcreq dir> <out.json> [R S layout volume]
+Usage: python tools/pmc_report.py <pmcreq dir> <out.json> [R S layout volume [camera]]
 (<pmcreq dir>: gpurun_out/pmcreq as rocprofv3 wrote it, or profiles/r02/pmcreq
 with one trimmed <pass>.csv per counter pass)
 """
@@ -50,26 +50,34 @@ def read_bytes(c):
 
 def main():
     src, dst = Path(sys.argv[1]), Path(sys.argv[2])
-    R, S, layout, volume = 512, 8, "corner8", 512
+    R, S, layout, volume, camera = 512, 8, "corner8", 512, "default"
     if len(sys.argv) > 6:
         R, S, layout, volume = int(sys.argv[3]), int(sys.argv[4]), sys.argv[5], int(sys.argv[6])
+    if len(sys.argv) > 7:
+        camera = sys.argv[7]
     out = {"source": "tools/pmc_req.sh + tools/pmc_report.py", "entries": []}
 
-    cq, cdur, _ = last_dispatch(src / "calib_req", "k_gather")
-    cf, _, _ = last_dispatch(src / "calib_fetch", "k_gather")
     gathers = 4096 * 256 * 256  # tools/gather_calib defaults: 4096 blocks x 256 lanes x 256
-    out["gather_calibration"] = {
-        "launch": "tools/gather_calib 1024: 268,435,456 scattered 8-B loads from a 1 GiB table",
-        "requests_per_gather": round(cq["TCC_EA0_RDREQ_sum"] / gathers, 4),
-        "req_128B_share": round(cq["TCC_EA0_RDREQ_128B_sum"] / cq["TCC_EA0_RDREQ_sum"], 5),
-        "read_bytes_per_gather": round(read_bytes(cq) / gathers, 2),
-        "fetch_size_bytes_per_gather": round(cf["FETCH_SIZE"] * 1024 / gathers, 2),
-        "fetch_size_factor": round(read_bytes(cq) / (cf["FETCH_SIZE"] * 1024), 4),
-    }
+    if (src / "calib_req").exists() or (src / "calib_req.csv").exists():
+        cq, cdur, _ = last_dispatch(src / "calib_req", "k_gather")
+        cf, _, _ = last_dispatch(src / "calib_fetch", "k_gather")
+        out["gather_calibration"] = {
+            "launch": "tools/gather_calib 1024: 268,435,456 scattered 8-B loads from a 1 GiB table",
+            "requests_per_gather": round(cq["TCC_EA0_RDREQ_sum"] / gathers, 4),
+            "req_128B_share": round(cq["TCC_EA0_RDREQ_128B_sum"] / cq["TCC_EA0_RDREQ_sum"], 5),
+            "read_bytes_per_gather": round(read_bytes(cq) / gathers, 2),
+            "fetch_size_bytes_per_gather": round(cf["FETCH_SIZE"] * 1024 / gathers, 2),
+            "fetch_size_factor": round(read_bytes(cq) / (cf["FETCH_SIZE"] * 1024), 4),
+            "gathers_per_s_under_pmc": round(gathers / cdur, 1),
+        }
+    elif dst.exists():  # passes of another camera / volume: the file's calibration stands
+        out["gather_calibration"] = json.loads(dst.read_text()).get("gather_calibration")
     for ppl_dir in sorted({p.with_suffix("") for p in src.glob("bench*_req*")}):
         ppl = int(ppl_dir.name[len("bench"):-len("_req")])
         q, qdur, kname = last_dispatch(ppl_dir, "k_march")
-        w, _, _ = last_dispatch(src / f"bench{ppl}_write", "k_march")
+        wd = src / f"bench{ppl}_write"
+        w = last_dispatch(wd, "k_march")[0] if wd.exists() or wd.with_name(wd.name + ".csv").exists() \
+            else {"WRITE_SIZE": 0.0}  # no write pass: reads only
         sq, sdur, _ = last_dispatch(src / f"bench{ppl}_sq", "k_march")
         rb = read_bytes(q)
         wb = w["WRITE_SIZE"] * 1024
@@ -78,7 +86,8 @@ def main():
         photon_steps = R * R * S * ppl
         out["entries"].append({
             "kernel": "k_march", "kernel_name": kname, "resolution": R, "steps": S, "layout": layout,
-            "volume": volume, "passes_per_launch": ppl,
+            "volume": volume, "passes_per_launch": ppl, "camera": camera,
+            "kernel_us_under_pmc": round(qdur * 1e6, 2),
             "read_requests": {"32B": q["TCC_EA0_RDREQ_32B_sum"], "64B": q["TCC_EA0_RDREQ_64B_sum"],
                               "128B": q["TCC_EA0_RDREQ_128B_sum"]},
             "read_bytes_per_launch": int(rb), "write_bytes_per_launch": int(wb),
@@ -94,7 +103,8 @@ def main():
             },
         })
     if dst.exists():  # keep the other layouts' / shapes' entries
-        key = lambda e: (e["resolution"], e["steps"], e["layout"], e["volume"], e["passes_per_launch"])
+        key = lambda e: (e["resolution"], e["steps"], e["layout"], e["volume"], e["passes_per_launch"],
+                         e.get("camera", "default"))
         mine = {key(e) for e in out["entries"]}
         old = json.loads(dst.read_text()).get("entries", [])
         out["entries"] = [e for e in old if key(e) not in mine] + out["entries"]
