@@ -1450,7 +1450,9 @@ __global__ __launch_bounds__(256) void k_composite(const CompositeSrc S, uint32_
       const vu2 v = {h0, h1};
       __builtin_amdgcn_raw_buffer_store_b64(v, coherent_rsrc(rgba, npx * 8u), i * 8u, 0, kCpolSystem);
     }
-    if (counts) __builtin_amdgcn_raw_buffer_store_b32(n, coherent_rsrc(counts, npx * 4u), i * 4u, 0, kCpolSystem);
+    if (counts)  // (the b32 store takes an integer: the count's bits, not a conversion)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(n), coherent_rsrc(counts, npx * 4u), i * 4u, 0,
+                                            kCpolSystem);
   } else {
     if (rgb32) {
       rgb32[3u * i] = r;
