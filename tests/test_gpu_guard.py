@@ -45,7 +45,8 @@ def test_guard_build_cases_bitexact(lib):
 
 
 def test_dirty_device_pool_leaves_the_bits():
-    hip = C.CDLL("/opt/rocm/lib/libamdhip64.so")
+    vptmcm.load()  # the HIP runtime the library runs on: the same object by its soname
+    hip = C.CDLL("libamdhip64.so.7")
     hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
     hip.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
     hip.hipFree.argtypes = [C.c_void_p]
