@@ -127,6 +127,14 @@ for s in $STEPS; do
     (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$OUT/groupprof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/group_enqueue.py" --ns 8 --reps 20 --composite --threads on > "$GRAFT_REPO_ROOT/$OUT/groupprof.jsonl" 2> "$GRAFT_REPO_ROOT/$OUT/groupprof.err")
     rc=$?; echo "groupcomp prof rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
     python3 tools/composite_trace.py $(ls $OUT/groupprof/*/run_kernel_trace.csv $OUT/groupprof/run_kernel_trace.csv 2>/dev/null | head -1) > $OUT/composite_trace.json 2>&1; cat $OUT/composite_trace.json ;;
+  kernargab)  # the driver's command, alternating HIP_FORCE_DEV_KERNARG unset / 1 / 0 (kernel arguments in device or host memory)
+    for k in ${KARG_CASES:-unset 1 0 unset 1 0 unset 1 0}; do
+      if [ $k = unset ]; then unset HIP_FORCE_DEV_KERNARG; else export HIP_FORCE_DEV_KERNARG=$k; fi
+      timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --near-steps 0 > $OUT/karg.json 2>> $OUT/kernargab.err
+      rc=$?; unset HIP_FORCE_DEV_KERNARG; [ $rc -ne 0 ] && { echo "kernargab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      python3 -c "import json; d=json.load(open('$OUT/karg.json')); r=d['roofline']; print(json.dumps({'dev_kernarg': '$k', 'value': d['value'], 'region_wall_us': r['region_wall_us'], 'kernel_us': r['kernel_avg_us'], 'wall_minus_kernel_us': r['wall_minus_kernel_us']}))" >> $OUT/kernargab.jsonl
+    done
+    echo "kernargab rc=0" | tee -a $OUT/status.txt; cat $OUT/kernargab.jsonl ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)
