@@ -355,11 +355,11 @@ def main():
     F = max(1, min(a.fuse, 32))
     every = max(1, a.allreduce_every)
 
-    def passes_on(sd, first: int, count: int, F: int = F) -> list:
+    def passes_on(sd, first: int, count: int, F: int = F, m=mvp) -> list:
         launches, done = [], 0
         while done < count:
             n = min(F, count - done)
-            r.render_passes(mvp, sd[first + done:first + done + n])
+            r.render_passes(m, sd[first + done:first + done + n])
             launches.append(n)
             done += n
         return launches
@@ -543,7 +543,7 @@ def main():
         r.synchronize()
         r.enable_kernel_timing(not a.no_timing)
         t6 = time.perf_counter()
-        nl = passes_on(nseeds, 65, a.near_steps)
+        nl = passes_on(nseeds, 65, a.near_steps, m=mn)
         r.synchronize()
         el6 = time.perf_counter() - t6
         nk_ms, nn = r.kernel_time()

@@ -102,6 +102,9 @@ def main():
                 "note": "chip-wide: VALU wave-instructions x 2 cycles / (1024 SIMDs x kernel cycles)",
             },
         })
+    if dst.exists():  # keep the file's other top-level fields (gather_peak, ...)
+        for k, v in json.loads(dst.read_text()).items():
+            out.setdefault(k, v)
     if dst.exists():  # keep the other layouts' / shapes' entries
         key = lambda e: (e["resolution"], e["steps"], e["layout"], e["volume"], e["passes_per_launch"],
                          e.get("camera", "default"))
