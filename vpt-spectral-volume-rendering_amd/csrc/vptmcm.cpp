@@ -306,9 +306,14 @@ struct vptmcm {
   // j packs into [j & 1]), so a pack never waits for the composite before it
   float4* grp_pack[2] = {nullptr, nullptr};
   float4* grp_gather = nullptr;    // replica 0, RCCL: the reduced sum
-  float* grp_rgb32 = nullptr;      // replica 0: the composite, fp32
-  uint16_t* grp_rgba = nullptr;    // replica 0: the composite, rgba16float
-  float* grp_counts = nullptr;     // replica 0, PEER: the composite's sum(n)
+  // The composite image: PEER, this replica's pixel shard [grp_p0, grp_p1) of
+  // it, on its own device (the composite is never gathered on one device: the
+  // readers copy every shard to the host at once); RCCL, replica 0: all of it
+  float* grp_rgb32 = nullptr;      // fp32
+  uint16_t* grp_rgba = nullptr;    // rgba16float
+  float* grp_counts = nullptr;     // PEER: sum(n)
+  uint32_t* grp_ldr = nullptr;     // PEER: the tone mapper's rgba8 of the shard (lazily)
+  size_t grp_p0 = 0, grp_p1 = 0;
   hipEvent_t grp_packed = nullptr; // this replica's pack of the current composite is complete
   // PEER (sharded): replica k composites pixel shard k of every replica's pack
   // on its own device, on a stream of its own (its next march does not wait
@@ -1142,6 +1147,17 @@ const char* vptmcm_last_error(const vptmcm* h) {
 
 // ---- device-list handles (vptmcm_config::n_devices)
 
+// Replica k of a device-list handle (0: the handle itself).
+static vptmcm* replica_of(vptmcm* h, uint32_t k) { return k ? h->peers[k - 1] : h; }
+
+// Pixel shard k of N of the PEER composite: [p0, p1), whole 256-pixel blocks
+// of the composite kernel except the last (a shard may be empty for tiny R).
+static void shard_range(size_t npx, uint32_t n, uint32_t k, size_t* p0, size_t* p1) {
+  const size_t step = ((npx + n - 1) / n + 255) / 256 * 256;
+  *p0 = std::min(npx, (size_t)k * step);
+  *p1 = std::min(npx, *p0 + step);
+}
+
 // The composite's buffers and events. PEER: two pack buffers, a composite
 // stream and a shard event per replica; on devices[0] the composite image and
 // counts; xGMI peer access between EVERY pair of distinct devices (a shard
@@ -1159,19 +1175,26 @@ static int group_alloc(vptmcm* h, const int32_t* devs, uint32_t n) {
     if (peer) {
       HIPCHK(c, hipStreamCreateWithFlags(&c->grp_stream, hipStreamNonBlocking));
       HIPCHK(c, hipEventCreateWithFlags(&c->grp_shard, hipEventDisableTiming));
+      shard_range(npx, n, c->replica, &c->grp_p0, &c->grp_p1);
+      const size_t m = std::max<size_t>(c->grp_p1 - c->grp_p0, 1);  // (an empty shard keeps a stub)
+      HIPCHK(c, dev_alloc(&c->grp_rgb32, m * 3 * sizeof(float)));
+      HIPCHK(c, hipMemsetAsync(c->grp_rgb32, 0, m * 3 * sizeof(float), c->grp_stream));
+      HIPCHK(c, dev_alloc(&c->grp_rgba, m * 4 * sizeof(uint16_t)));
+      HIPCHK(c, hipMemsetAsync(c->grp_rgba, 0, m * 4 * sizeof(uint16_t), c->grp_stream));
+      HIPCHK(c, dev_alloc(&c->grp_counts, m * sizeof(float)));
+      HIPCHK(c, hipMemsetAsync(c->grp_counts, 0, m * sizeof(float), c->grp_stream));
+      HIPCHK(c, hipStreamSynchronize(c->grp_stream));
     }
     return VPTMCM_OK;
   });
   if (rc) return rc;
   HIPCHK(h, hipSetDevice(h->device));
-  if (!peer) HIPCHK(h, dev_alloc(&h->grp_gather, npx * sizeof(float4)));
-  HIPCHK(h, dev_alloc(&h->grp_rgb32, npx * 3 * sizeof(float)));
-  HIPCHK(h, hipMemsetAsync(h->grp_rgb32, 0, npx * 3 * sizeof(float), enq(h)));
-  HIPCHK(h, dev_alloc(&h->grp_rgba, npx * 4 * sizeof(uint16_t)));
-  HIPCHK(h, hipMemsetAsync(h->grp_rgba, 0, npx * 4 * sizeof(uint16_t), enq(h)));
-  if (peer) {
-    HIPCHK(h, dev_alloc(&h->grp_counts, npx * sizeof(float)));
-    HIPCHK(h, hipMemsetAsync(h->grp_counts, 0, npx * sizeof(float), enq(h)));
+  if (!peer) {
+    HIPCHK(h, dev_alloc(&h->grp_gather, npx * sizeof(float4)));
+    HIPCHK(h, dev_alloc(&h->grp_rgb32, npx * 3 * sizeof(float)));
+    HIPCHK(h, hipMemsetAsync(h->grp_rgb32, 0, npx * 3 * sizeof(float), enq(h)));
+    HIPCHK(h, dev_alloc(&h->grp_rgba, npx * 4 * sizeof(uint16_t)));
+    HIPCHK(h, hipMemsetAsync(h->grp_rgba, 0, npx * 4 * sizeof(uint16_t), enq(h)));
   }
   for (int k = 0; k < 2; k++) {
     HIPCHK(h, hipEventCreateWithFlags(&h->grp_done[k], hipEventDisableTiming));
@@ -1303,31 +1326,21 @@ static int create_group(const vptmcm_config* cfg, vptmcm** out) {
   return VPTMCM_OK;
 }
 
-// Replica k of a device-list handle (0: the handle itself).
-static vptmcm* replica_of(vptmcm* h, uint32_t k) { return k ? h->peers[k - 1] : h; }
-
-// Pixel shard k of N of the PEER composite: [p0, p1), whole 256-pixel blocks
-// of the composite kernel except the last (a shard may be empty for tiny R).
-static void shard_range(size_t npx, uint32_t n, uint32_t k, size_t* p0, size_t* p1) {
-  const size_t step = ((npx + n - 1) / n + 255) / 256 * 256;
-  *p0 = std::min(npx, (size_t)k * step);
-  *p1 = std::min(npx, *p0 + step);
-}
-
 // The composite of the current frame over every replica. Asynchronous: the
-// readers (and synchronize) wait for grp_done[grp_last].
+// readers wait for it (composite_ready, read_shards).
 //
 // PEER (sharded): (1) every replica packs (rgb*n, n) into its buffer j & 1 on
 // its own stream, behind its march (that buffer was last read by composite
 // j - 2: its grp_done); (2) replica k, on its composite stream, waits for
 // every replica's pack and composites pixel shard k of all of them — the
 // sources summed in replica order, the same f32 sums and division as one
-// k_composite over whole buffers — writing that slice of devices[0]'s fp32
-// image, rgba16f image and counts: each device reads 1/N of every pack over
-// its own links at once and writes 1/N of the image to devices[0]; (3)
-// devices[0]'s composite stream waits for every shard and records grp_done.
-// Steps (1) and (2) run on the replicas' worker threads; a step's host
-// enqueue starts once every replica has recorded the previous step's event.
+// k_composite over whole buffers — into its own shard of the image: each
+// device reads 1/N of every other replica's pack over its own links at once
+// and nothing is gathered on one device (readers copy the N shards to the
+// host in parallel); (3) devices[0]'s composite stream waits for every shard
+// and records grp_done[j & 1], the fence of the packs' reuse. Steps (1) and
+// (2) run on the replicas' worker threads; a step's host enqueue starts once
+// every replica has recorded the previous step's event.
 //
 // RCCL: every replica packs, a grouped ncclReduce sums the packs on
 // devices[0], and k_composite divides there, on replica 0's stream.
@@ -1350,8 +1363,7 @@ static int group_composite(vptmcm* h) {
   if (peer) {
     rc = for_replicas(h, [&](vptmcm* c) {
       HIPCHK(c, hipSetDevice(c->device));
-      // every pack, replica 0's included: its packed event also follows every
-      // read of the previous composite's image enqueued on devices[0]
+      // every pack (this shard's previous readers ran on this stream already)
       for (uint32_t k = 0; k < n; k++) HIPCHK(c, hipStreamWaitEvent(c->grp_stream, replica_of(h, k)->grp_packed, 0));
       size_t p0, p1;
       shard_range(npx, n, c->replica, &p0, &p1);
@@ -1360,8 +1372,8 @@ static int group_composite(vptmcm* h) {
         memset(&S, 0, sizeof S);
         S.n = n;
         for (uint32_t k = 0; k < n; k++) S.p[k] = replica_of(h, k)->grp_pack[b] + p0;
-        HIPCHK(c, launch_composite(S, (uint32_t)(p1 - p0), h->grp_rgb32 + 3 * p0, h->grp_rgba + 4 * p0,
-                                   h->grp_counts + p0, c->grp_stream, true));
+        HIPCHK(c, launch_composite(S, (uint32_t)(p1 - p0), c->grp_rgb32, c->grp_rgba, c->grp_counts,
+                                   c->grp_stream, true));
       }
       HIPCHK(c, hipEventRecord(c->grp_shard, c->grp_stream));
       return VPTMCM_OK;
@@ -1404,6 +1416,33 @@ static int composite_ready(vptmcm* h) {
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamWaitEvent(enq(h), h->grp_done[h->grp_last], 0));
   return VPTMCM_OK;
+}
+
+// A device-list handle whose composite is sharded over its replicas (PEER).
+static bool sharded(const vptmcm* h) {
+  return !h->peers.empty() && h->group_transport == VPTMCM_GROUP_PEER;
+}
+
+enum ShardPlane { kShardRgba, kShardRgb, kShardCounts };
+
+// PEER readers: every replica's shard of the composite (made first if a march
+// or reset ran since the last one) copied to its place in the host buffer, all
+// replicas at once, each on its composite stream, behind its shard kernel.
+static int read_shards(vptmcm* h, ShardPlane which, void* out) {
+  if (h->grp_dirty || h->grp_last < 0)
+    if (int rc = group_composite(h)) return rc;
+  const size_t bpp = which == kShardRgba ? 8 : which == kShardRgb ? 12 : 4;
+  return for_replicas(h, [&](vptmcm* c) {
+    const size_t m = c->grp_p1 - c->grp_p0;
+    if (m == 0) return VPTMCM_OK;
+    const void* src = which == kShardRgba ? (const void*)c->grp_rgba
+                      : which == kShardRgb ? (const void*)c->grp_rgb32 : (const void*)c->grp_counts;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(static_cast<char*>(out) + c->grp_p0 * bpp, src, m * bpp, hipMemcpyDeviceToHost,
+                             c->grp_stream));
+    HIPCHK(c, hipStreamSynchronize(c->grp_stream));
+    return VPTMCM_OK;
+  });
 }
 
 int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
@@ -1585,6 +1624,7 @@ void vptmcm_destroy(vptmcm* h) {
   if (h->grp_rgb32) (void)dev_free(h->grp_rgb32);
   if (h->grp_rgba) (void)dev_free(h->grp_rgba);
   if (h->grp_counts) (void)dev_free(h->grp_counts);
+  if (h->grp_ldr) (void)dev_free(h->grp_ldr);
   for (auto e : h->grp_done)
     if (e) (void)hipEventDestroy(e);
   if (h->comp_rgb32) (void)dev_free(h->comp_rgb32);
@@ -1977,6 +2017,7 @@ int vptmcm_read_rgba16f(vptmcm* h, uint16_t* out) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!out) FAIL(h, VPTMCM_EINVAL, "read_rgba16f: null output");
+  if (sharded(h)) return read_shards(h, kShardRgba, out);
   if (composited(h))
     if (int rc = composite_ready(h)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
@@ -1990,6 +2031,7 @@ int vptmcm_read_rgb(vptmcm* h, float* out) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!out) FAIL(h, VPTMCM_EINVAL, "read_rgb: null output");
+  if (sharded(h)) return read_shards(h, kShardRgb, out);
   if (composited(h))
     if (int rc = composite_ready(h)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
@@ -2034,6 +2076,23 @@ int vptmcm_tonemap_artistic(vptmcm* h, const float params[5], uint8_t* rgba8_out
   T.saturation = params[3];
   const float midpoint = (mid - low) / range;
   T.exponent = (float)(-std::log((double)midpoint) / std::log(2.0)) / params[4];
+  if (sharded(h)) {  // every shard tone-mapped on its own device, copied to its place
+    if (h->grp_dirty || h->grp_last < 0)
+      if (int rc = group_composite(h)) return rc;
+    return for_replicas(h, [&](vptmcm* c) {
+      const size_t m = c->grp_p1 - c->grp_p0;
+      if (m == 0) return VPTMCM_OK;
+      HIPCHK(c, hipSetDevice(c->device));
+      if (!c->grp_ldr) HIPCHK(c, dev_alloc(&c->grp_ldr, m * 4));
+      HIPCHK(c, launch_tonemap_artistic(c->grp_rgba, (uint32_t)m, T, c->grp_ldr, c->grp_stream));
+      if (rgba8_out) {
+        HIPCHK(c, hipMemcpyAsync(rgba8_out + c->grp_p0 * 4, c->grp_ldr, m * 4, hipMemcpyDeviceToHost,
+                                 c->grp_stream));
+        HIPCHK(c, hipStreamSynchronize(c->grp_stream));
+      }
+      return VPTMCM_OK;
+    });
+  }
   stream_op(h);
   HIPCHK(h, launch_tonemap_artistic(composited(h) ? h->grp_rgba : h->rgba, (uint32_t)npx, T, h->ldr,
                                     enq(h)));
@@ -2322,18 +2381,24 @@ int vptmcm_read_composite(vptmcm* h, uint16_t* rgba16f, float* rgb, float* count
       const int32_t dev = h->device;
       if (int rc = group_alloc(h, &dev, 1)) return rc;
     }
+    if (h->group_transport == VPTMCM_GROUP_PEER) {  // the shards, every one to its place
+      if (rgba16f)
+        if (int rc = read_shards(h, kShardRgba, rgba16f)) return rc;
+      if (rgb)
+        if (int rc = read_shards(h, kShardRgb, rgb)) return rc;
+      if (counts)
+        if (int rc = read_shards(h, kShardCounts, counts)) return rc;
+      return VPTMCM_OK;
+    }
     if (int rc = composite_ready(h)) return rc;
-    if (counts) {  // sum(n): PEER's shards wrote it; RCCL: the composite kernel on the sum, counts only
-      if (h->group_transport == VPTMCM_GROUP_RCCL) {
-        CompositeSrc S;
-        memset(&S, 0, sizeof S);
-        S.n = 1;
-        S.p[0] = h->grp_gather;
-        if (!h->comp_counts) HIPCHK(h, dev_alloc(&h->comp_counts, npx * sizeof(float)));
-        HIPCHK(h, launch_composite(S, (uint32_t)npx, nullptr, nullptr, h->comp_counts, enq(h)));
-      }
-      HIPCHK(h, hipMemcpyAsync(counts, h->group_transport == VPTMCM_GROUP_RCCL ? h->comp_counts : h->grp_counts,
-                               npx * sizeof(float), hipMemcpyDeviceToHost, enq(h)));
+    if (counts) {  // sum(n): the composite kernel on the reduced sum, counts only
+      CompositeSrc S;
+      memset(&S, 0, sizeof S);
+      S.n = 1;
+      S.p[0] = h->grp_gather;
+      if (!h->comp_counts) HIPCHK(h, dev_alloc(&h->comp_counts, npx * sizeof(float)));
+      HIPCHK(h, launch_composite(S, (uint32_t)npx, nullptr, nullptr, h->comp_counts, enq(h)));
+      HIPCHK(h, hipMemcpyAsync(counts, h->comp_counts, npx * sizeof(float), hipMemcpyDeviceToHost, enq(h)));
     }
     if (rgba16f)
       HIPCHK(h, hipMemcpyAsync(rgba16f, h->grp_rgba, npx * 8, hipMemcpyDeviceToHost, enq(h)));
