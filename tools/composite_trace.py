@@ -26,25 +26,34 @@ def main():
             "composite" if "k_composite" in name else None
         if k:
             kinds.append((k, int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
-    chains, packs, comps = [], [], []
-    last_march, comp_end, seen = None, None, False
-    for k, b, e in kinds:
-        if k == "march":
-            if seen:  # the previous region's composite is complete: a new region
-                chains.append((comp_end - last_march) / 1e3)
-                seen, last_march = False, None
-            last_march = e if last_march is None else max(last_march, e)
-        elif k == "pack":
-            packs.append((e - b) / 1e3)
-        else:
-            comps.append((e - b) / 1e3)
-            comp_end = e if not seen else max(comp_end, e)
-            seen = True
-    if seen:
-        chains.append((comp_end - last_march) / 1e3)
+    chains, packs, comps, gaps, pack_chain = [], [], [], [], []
+    group = []
+
+    def close(g):
+        marches = [x for x in g if x[0] == "march"]
+        pk = [x for x in g if x[0] == "pack"]
+        cm = [x for x in g if x[0] == "composite"]
+        if not (marches and cm):
+            return
+        last_march = max(x[2] for x in marches)
+        chains.append((max(x[2] for x in cm) - last_march) / 1e3)
+        packs.extend((x[2] - x[1]) / 1e3 for x in pk)
+        comps.extend((x[2] - x[1]) / 1e3 for x in cm)
+        if pk:  # the cross-stream wait: last pack done -> first shard kernel starts
+            gaps.append((min(x[1] for x in cm) - max(x[2] for x in pk)) / 1e3)
+            pack_chain.append((max(x[2] for x in pk) - last_march) / 1e3)
+
+    for x in kinds:  # a region: marches, then its packs and composites
+        if x[0] == "march" and any(g[0] == "composite" for g in group):
+            close(group)
+            group = []
+        group.append(x)
+    close(group)
     med = lambda v: round(statistics.median(v), 2) if v else None
     print(json.dumps({"composites": len(chains), "chain_us_median": med(chains),
                       "chain_us_p90": round(sorted(chains)[int(0.9 * len(chains))], 2) if chains else None,
+                      "last_march_to_last_pack_us_median": med(pack_chain),
+                      "last_pack_to_first_shard_us_median": med(gaps),
                       "k_pack_us_median": med(packs), "k_composite_us_median": med(comps)}))
 
 

@@ -124,9 +124,11 @@ for s in $STEPS; do
   groupcomp)  # device-list composite: host enqueue behind the march, then the device chain under a kernel trace
     timeout -k 10 300 python tools/group_enqueue.py --ns 2 4 8 --reps 30 --composite > $OUT/group_enqueue.jsonl 2> $OUT/group_enqueue.err
     rc=$?; echo "groupcomp enqueue rc=$rc" | tee -a $OUT/status.txt; cat $OUT/group_enqueue.jsonl; fault $rc && exit $rc
-    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$OUT/groupprof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/group_enqueue.py" --ns 8 --reps 20 --composite --threads on > "$GRAFT_REPO_ROOT/$OUT/groupprof.jsonl" 2> "$GRAFT_REPO_ROOT/$OUT/groupprof.err")
-    rc=$?; echo "groupcomp prof rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
-    python3 tools/composite_trace.py $(ls $OUT/groupprof/*/run_kernel_trace.csv $OUT/groupprof/run_kernel_trace.csv 2>/dev/null | head -1) > $OUT/composite_trace.json 2>&1; cat $OUT/composite_trace.json ;;
+    for gn in ${GROUP_PROF_NS:-2 8}; do
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$OUT/groupprof$gn" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/group_enqueue.py" --ns $gn --reps 20 --composite --threads on > "$GRAFT_REPO_ROOT/$OUT/groupprof$gn.jsonl" 2> "$GRAFT_REPO_ROOT/$OUT/groupprof$gn.err")
+      rc=$?; echo "groupcomp prof $gn rc=$rc" | tee -a $OUT/status.txt; fault $rc && exit $rc
+      python3 tools/composite_trace.py $OUT/groupprof$gn/run_kernel_trace.csv > $OUT/composite_trace$gn.json 2>&1; cat $OUT/composite_trace$gn.json
+    done ;;
   kernargab)  # the driver's command, alternating HIP_FORCE_DEV_KERNARG unset / 1 / 0 (kernel arguments in device or host memory)
     for k in ${KARG_CASES:-unset 1 0 unset 1 0 unset 1 0}; do
       if [ $k = unset ]; then unset HIP_FORCE_DEV_KERNARG; else export HIP_FORCE_DEV_KERNARG=$k; fi

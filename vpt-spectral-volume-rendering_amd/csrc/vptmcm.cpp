@@ -319,9 +319,11 @@ struct vptmcm {
   // on its own device, on a stream of its own (its next march does not wait
   // for the other replicas), writing that slice of the image into devices[0]
   hipStream_t grp_stream = nullptr;
-  hipEvent_t grp_shard = nullptr;  // this replica's shard of the current composite is written
-  // replica 0: composite j (buffer j & 1) has read every pack and written every
-  // shard; the readers and the pack two composites later wait for it
+  // this replica's shard of composite j is written (and, so, its reads of
+  // every replica's buffer j & 1 are done): [j & 1]
+  hipEvent_t grp_shard[2] = {nullptr, nullptr};
+  // replica 0, RCCL: the composite (reduce + k_composite) is complete; the
+  // readers and the next pack wait for it ([0]; PEER uses grp_shard instead)
   hipEvent_t grp_done[2] = {nullptr, nullptr};
   uint32_t grp_seq = 0;            // replica 0: composites issued
   int grp_last = -1;               // replica 0: the buffer of the last composite
@@ -1174,7 +1176,10 @@ static int group_alloc(vptmcm* h, const int32_t* devs, uint32_t n) {
     HIPCHK(c, hipEventCreateWithFlags(&c->grp_packed, hipEventDisableTiming));
     if (peer) {
       HIPCHK(c, hipStreamCreateWithFlags(&c->grp_stream, hipStreamNonBlocking));
-      HIPCHK(c, hipEventCreateWithFlags(&c->grp_shard, hipEventDisableTiming));
+      for (auto& e : c->grp_shard) {
+        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(e, c->grp_stream));
+      }
       shard_range(npx, n, c->replica, &c->grp_p0, &c->grp_p1);
       const size_t m = std::max<size_t>(c->grp_p1 - c->grp_p0, 1);  // (an empty shard keeps a stub)
       HIPCHK(c, dev_alloc(&c->grp_rgb32, m * 3 * sizeof(float)));
@@ -1330,16 +1335,17 @@ static int create_group(const vptmcm_config* cfg, vptmcm** out) {
 // readers wait for it (composite_ready, read_shards).
 //
 // PEER (sharded): (1) every replica packs (rgb*n, n) into its buffer j & 1 on
-// its own stream, behind its march (that buffer was last read by composite
-// j - 2: its grp_done); (2) replica k, on its composite stream, waits for
+// its own stream, behind its march (that buffer was last read by the shard
+// kernels of composite j - 2: every replica's grp_shard[j & 1], long complete
+// in steady state); (2) replica k, on its composite stream, waits for
 // every replica's pack and composites pixel shard k of all of them — the
 // sources summed in replica order, the same f32 sums and division as one
 // k_composite over whole buffers — into its own shard of the image: each
 // device reads 1/N of every other replica's pack over its own links at once
 // and nothing is gathered on one device (readers copy the N shards to the
-// host in parallel); (3) devices[0]'s composite stream waits for every shard
-// and records grp_done[j & 1], the fence of the packs' reuse. Steps (1) and
-// (2) run on the replicas' worker threads; a step's host enqueue starts once
+// host in parallel) and records grp_shard[j & 1]. No step waits on devices[0]
+// after the shards: one cross-stream hop (the packs' events) is the whole
+// chain. Steps (1) and (2) run on the replicas' worker threads; a step's host enqueue starts once
 // every replica has recorded the previous step's event.
 //
 // RCCL: every replica packs, a grouped ncclReduce sums the packs on
@@ -1349,11 +1355,14 @@ static int group_composite(vptmcm* h) {
   const size_t npx = (size_t)h->R * h->R;
   const bool peer = h->group_transport == VPTMCM_GROUP_PEER;
   const uint32_t b = peer ? (h->grp_seq & 1u) : 0u;
-  hipEvent_t prev = h->grp_done[b];
   int rc = for_replicas(h, [&](vptmcm* c) {
     if (int r = flush_renders(c)) return r;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamWaitEvent(enq(c), prev, 0));  // buffer b is free (and, RCCL, the reduce target)
+    if (peer) {  // buffer b is free: every shard kernel of composite j - 2 has read it
+      for (uint32_t k = 0; k < n; k++) HIPCHK(c, hipStreamWaitEvent(enq(c), replica_of(h, k)->grp_shard[b], 0));
+    } else {  // the last reduce has read it (and its target)
+      HIPCHK(c, hipStreamWaitEvent(enq(c), h->grp_done[b], 0));
+    }
     const MarchParams P = make_params(c, kNoMatrix, 0);
     HIPCHK(c, launch_pack(P, c->photons, c->rgb32, c->grp_pack[b], enq(c)));
     HIPCHK(c, hipEventRecord(c->grp_packed, enq(c)));
@@ -1375,13 +1384,10 @@ static int group_composite(vptmcm* h) {
         HIPCHK(c, launch_composite(S, (uint32_t)(p1 - p0), c->grp_rgb32, c->grp_rgba, c->grp_counts,
                                    c->grp_stream, true));
       }
-      HIPCHK(c, hipEventRecord(c->grp_shard, c->grp_stream));
+      HIPCHK(c, hipEventRecord(c->grp_shard[b], c->grp_stream));
       return VPTMCM_OK;
     });
     if (rc) return rc;
-    HIPCHK(h, hipSetDevice(h->device));
-    for (uint32_t k = 1; k < n; k++) HIPCHK(h, hipStreamWaitEvent(h->grp_stream, h->peers[k - 1]->grp_shard, 0));
-    HIPCHK(h, hipEventRecord(h->grp_done[b], h->grp_stream));
   } else {
     if (ncclGroupStart() != ncclSuccess) FAIL(h, VPTMCM_ECOMM, "composite: ncclGroupStart failed");
     ncclResult_t r = ncclSuccess;
@@ -1602,9 +1608,12 @@ void vptmcm_destroy(vptmcm* h) {
         p = nullptr;
       }
       if (c->grp_packed) (void)hipEventDestroy(c->grp_packed);
-      if (c->grp_shard) (void)hipEventDestroy(c->grp_shard);
+      for (auto& e : c->grp_shard) {
+        if (e) (void)hipEventDestroy(e);
+        e = nullptr;
+      }
       if (c->grp_stream) (void)hipStreamDestroy(c->grp_stream);
-      c->grp_packed = c->grp_shard = nullptr;
+      c->grp_packed = nullptr;
       c->grp_stream = nullptr;
     }
     vptmcm_destroy(c);
@@ -1619,7 +1628,8 @@ void vptmcm_destroy(vptmcm* h) {
   for (auto p : h->grp_pack)
     if (p) (void)dev_free(p);
   if (h->grp_packed) (void)hipEventDestroy(h->grp_packed);
-  if (h->grp_shard) (void)hipEventDestroy(h->grp_shard);
+  for (auto e : h->grp_shard)
+    if (e) (void)hipEventDestroy(e);
   if (h->grp_gather) (void)dev_free(h->grp_gather);
   if (h->grp_rgb32) (void)dev_free(h->grp_rgb32);
   if (h->grp_rgba) (void)dev_free(h->grp_rgba);
