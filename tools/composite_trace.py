@@ -26,7 +26,7 @@ def main():
             "composite" if "k_composite" in name else None
         if k:
             kinds.append((k, int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
-    chains, packs, comps, gaps, pack_chain = [], [], [], [], []
+    chains, packs, comps, gaps, pack_chain, march_gap = [], [], [], [], [], []
     group = []
 
     def close(g):
@@ -39,6 +39,7 @@ def main():
         chains.append((max(x[2] for x in cm) - last_march) / 1e3)
         packs.extend((x[2] - x[1]) / 1e3 for x in pk)
         comps.extend((x[2] - x[1]) / 1e3 for x in cm)
+        march_gap.append((min(x[1] for x in cm) - last_march) / 1e3)
         if pk:  # the cross-stream wait: last pack done -> first shard kernel starts
             gaps.append((min(x[1] for x in cm) - max(x[2] for x in pk)) / 1e3)
             pack_chain.append((max(x[2] for x in pk) - last_march) / 1e3)
@@ -52,6 +53,7 @@ def main():
     med = lambda v: round(statistics.median(v), 2) if v else None
     print(json.dumps({"composites": len(chains), "chain_us_median": med(chains),
                       "chain_us_p90": round(sorted(chains)[int(0.9 * len(chains))], 2) if chains else None,
+                      "last_march_to_first_shard_us_median": med(march_gap),
                       "last_march_to_last_pack_us_median": med(pack_chain),
                       "last_pack_to_first_shard_us_median": med(gaps),
                       "k_pack_us_median": med(packs), "k_composite_us_median": med(comps)}))

@@ -252,6 +252,13 @@ struct vptmcm {
   // it is the stream's last work, vptmcm_comm_allreduce_radiance reduces that
   // buffer without a k_pack launch.
   bool pack_fresh = false;
+  // Device-list (PEER) replicas: the march packs (rgb * n, n) into grp_pack[b]
+  // for the next composite (b = that composite's buffer), so a composite that
+  // follows a march launches no k_pack: pack_buf is the buffer the stream's
+  // last march packed (valid with pack_fresh), grp_owner the handle holding
+  // the composite's bookkeeping (replica 0; itself for replica 0).
+  int pack_buf = -1;
+  struct vptmcm* grp_owner = nullptr;
   MarchLaunchInfo last_launch{};
   // The camera's robust-miss region (robust_region: a double-precision matrix
   // inverse and the projected hull) for the last matrix seen: a progressive
@@ -326,6 +333,11 @@ struct vptmcm {
   // readers and the next pack wait for it ([0]; PEER uses grp_shard instead)
   hipEvent_t grp_done[2] = {nullptr, nullptr};
   uint32_t grp_seq = 0;            // replica 0: composites issued
+  // replica 0, PEER: the composite (1-based seq) that last used buffer b, and
+  // the highest composite known complete on the host (synchronize / reads):
+  // a buffer whose last composite is known complete needs no fence wait
+  uint32_t grp_use_seq[2] = {0u, 0u};
+  uint32_t grp_synced_seq = 0;
   int grp_last = -1;               // replica 0: the buffer of the last composite
   std::vector<ncclComm_t> grp_comms;  // RCCL transport: one communicator per replica (InitAll)
   // replica 0: one worker thread per peer (VPTMCM_GROUP_THREADS=0: none, the
@@ -767,6 +779,23 @@ int flush_relayout(vptmcm* h) {
   return guard_check(h, "relayout");
 }
 
+// A device-list handle whose composite is sharded over its replicas (PEER).
+bool sharded(const vptmcm* h) { return !h->peers.empty() && h->group_transport == VPTMCM_GROUP_PEER; }
+
+// Replica k of a device-list handle (0: the handle itself).
+vptmcm* replica_of(vptmcm* h, uint32_t k) { return k ? h->peers[k - 1] : h; }
+
+// Before replica c writes its PEER pack buffer b (owner o = replica 0): every
+// shard kernel that read buffer b in the last composite using it has finished
+// (its replicas' grp_shard[b]); nothing to wait for when the host already
+// knows that composite complete.
+int fence_pack_buffer(vptmcm* o, vptmcm* c, uint32_t b) {
+  if (o->grp_use_seq[b] <= o->grp_synced_seq) return VPTMCM_OK;
+  const uint32_t n = 1u + (uint32_t)o->peers.size();
+  for (uint32_t k = 0; k < n; k++) HIPCHK(c, hipStreamWaitEvent(enq(c), replica_of(o, k)->grp_shard[b], 0));
+  return VPTMCM_OK;
+}
+
 // One march launch of n <= kMaxFusedPasses passes (seeds) with matrix mvp.
 int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   if (!h->volume_ready) FAIL(h, VPTMCM_ESTATE, "render: no volume set (setVolume first)");
@@ -794,11 +823,18 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   const bool signal = h->done_on && h->kind == VPTMCM_RENDERER_SPECTRAL;
   // (measurement builds, VPT_STAMP != 0, store neither rgb32 nor the pack: the
   // all-reduce then runs k_pack, whose inputs are as invalid as those builds' results)
-  const bool pack = !VPT_STAMP && h->comm && h->kind == VPTMCM_RENDERER_SPECTRAL && h->band_y0 == 0 &&
-                    h->band_y1 == h->R;
-  if (pack) {  // the buffer is free once the all-reduce issued two composites ago is done
+  const bool packable = !VPT_STAMP && h->kind == VPTMCM_RENDERER_SPECTRAL && h->band_y0 == 0 &&
+                        h->band_y1 == h->R;
+  const bool pack = packable && (h->comm || (h->grp_owner && sharded(h->grp_owner)));
+  int pack_buf = -1;
+  if (pack && h->comm) {  // the buffer is free once the all-reduce issued two composites ago is done
     HIPCHK(h, hipStreamWaitEvent(enq(h), h->comp_done[h->comp_next], 0));
     T.pack = h->comp[h->comp_next];
+  } else if (pack) {  // the next composite's buffer, free once composite j - 2's shards have read it
+    vptmcm* o = h->grp_owner;
+    pack_buf = (int)(o->grp_seq & 1u);
+    if (int rc = fence_pack_buffer(o, h, (uint32_t)pack_buf)) return rc;
+    T.pack = h->grp_pack[pack_buf];
   }
   if (signal) {  // every block of the grid counts once (committed below, once launched)
     P.done_target = h->done_total + tile_blocks(P, kMarchBlock);
@@ -824,6 +860,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   }
   h->done_pending = signal;
   h->pack_fresh = pack;
+  h->pack_buf = pack_buf;
   return guard_check(h, "march");
 }
 
@@ -1149,9 +1186,6 @@ const char* vptmcm_last_error(const vptmcm* h) {
 
 // ---- device-list handles (vptmcm_config::n_devices)
 
-// Replica k of a device-list handle (0: the handle itself).
-static vptmcm* replica_of(vptmcm* h, uint32_t k) { return k ? h->peers[k - 1] : h; }
-
 // Pixel shard k of N of the PEER composite: [p0, p1), whole 256-pixel blocks
 // of the composite kernel except the last (a shard may be empty for tiny R).
 static void shard_range(size_t npx, uint32_t n, uint32_t k, size_t* p0, size_t* p1) {
@@ -1325,6 +1359,8 @@ static int create_group(const vptmcm_config* cfg, vptmcm** out) {
   if (n > 1 || h->group_transport == VPTMCM_GROUP_RCCL) {
     if ((rc = group_alloc(h, cfg->devices, n))) return fail(rc, "vptmcm_create: " + h->err);
   }
+  if (sharded(h))  // the replicas' marches pack for the next composite
+    for (uint32_t k = 0; k < n; k++) replica_of(h, k)->grp_owner = h;
   const char* threads = getenv("VPTMCM_GROUP_THREADS");
   if (n > 1 && !(threads && threads[0] == '0')) start_workers(h);
   *out = h;
@@ -1358,13 +1394,17 @@ static int group_composite(vptmcm* h) {
   int rc = for_replicas(h, [&](vptmcm* c) {
     if (int r = flush_renders(c)) return r;
     HIPCHK(c, hipSetDevice(c->device));
-    if (peer) {  // buffer b is free: every shard kernel of composite j - 2 has read it
-      for (uint32_t k = 0; k < n; k++) HIPCHK(c, hipStreamWaitEvent(enq(c), replica_of(h, k)->grp_shard[b], 0));
-    } else {  // the last reduce has read it (and its target)
-      HIPCHK(c, hipStreamWaitEvent(enq(c), h->grp_done[b], 0));
+    // PEER: the stream's last march packed buffer b already (TileSched::pack)
+    const bool fresh = peer && c->pack_fresh && c->pack_buf == (int)b;
+    if (!fresh) {
+      if (peer) {  // buffer b is free once composite j - 2's shard kernels have read it
+        if (int r = fence_pack_buffer(h, c, b)) return r;
+      } else {  // the last reduce has read it (and its target)
+        HIPCHK(c, hipStreamWaitEvent(enq(c), h->grp_done[b], 0));
+      }
+      const MarchParams P = make_params(c, kNoMatrix, 0);
+      HIPCHK(c, launch_pack(P, c->photons, c->rgb32, c->grp_pack[b], enq(c)));
     }
-    const MarchParams P = make_params(c, kNoMatrix, 0);
-    HIPCHK(c, launch_pack(P, c->photons, c->rgb32, c->grp_pack[b], enq(c)));
     HIPCHK(c, hipEventRecord(c->grp_packed, enq(c)));
     return VPTMCM_OK;
   });
@@ -1408,6 +1448,7 @@ static int group_composite(vptmcm* h) {
     HIPCHK(h, hipEventRecord(h->grp_done[b], enq(h)));
   }
   h->grp_seq++;
+  h->grp_use_seq[b] = h->grp_seq;
   h->grp_last = (int)b;
   h->grp_dirty = false;
   if (VPT_GUARD) return for_replicas(h, [&](vptmcm* c) { return guard_check(c, "composite"); });
@@ -1424,11 +1465,6 @@ static int composite_ready(vptmcm* h) {
   return VPTMCM_OK;
 }
 
-// A device-list handle whose composite is sharded over its replicas (PEER).
-static bool sharded(const vptmcm* h) {
-  return !h->peers.empty() && h->group_transport == VPTMCM_GROUP_PEER;
-}
-
 enum ShardPlane { kShardRgba, kShardRgb, kShardCounts };
 
 // PEER readers: every replica's shard of the composite (made first if a march
@@ -1438,7 +1474,7 @@ static int read_shards(vptmcm* h, ShardPlane which, void* out) {
   if (h->grp_dirty || h->grp_last < 0)
     if (int rc = group_composite(h)) return rc;
   const size_t bpp = which == kShardRgba ? 8 : which == kShardRgb ? 12 : 4;
-  return for_replicas(h, [&](vptmcm* c) {
+  const int rc = for_replicas(h, [&](vptmcm* c) {
     const size_t m = c->grp_p1 - c->grp_p0;
     if (m == 0) return VPTMCM_OK;
     const void* src = which == kShardRgba ? (const void*)c->grp_rgba
@@ -1449,6 +1485,8 @@ static int read_shards(vptmcm* h, ShardPlane which, void* out) {
     HIPCHK(c, hipStreamSynchronize(c->grp_stream));
     return VPTMCM_OK;
   });
+  if (rc == VPTMCM_OK) h->grp_synced_seq = h->grp_seq;  // the shards of the last composite are done
+  return rc;
 }
 
 int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
@@ -2673,7 +2711,9 @@ int vptmcm_render_passes(vptmcm* h, const float* mvp, const uint32_t* seeds, uin
 
 int vptmcm_synchronize(vptmcm* h) {
   if (check_handle(h)) return VPTMCM_EINVAL;
-  return for_replicas(h, [&](vptmcm* c) { return synchronize_one(c); });
+  if (int rc = for_replicas(h, [&](vptmcm* c) { return synchronize_one(c); })) return rc;
+  h->grp_synced_seq = h->grp_seq;  // every composite issued so far is complete
+  return VPTMCM_OK;
 }
 
 int vptmcm_enable_kernel_timing(vptmcm* h, int enable) {
