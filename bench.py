@@ -78,6 +78,11 @@ def parse():
                     help="N > 1 without a launcher: the device-list composite's transport "
                          "(peer: every GPU pushes its (rgb*n, n) buffer to device 0 over its own "
                          "xGMI link; rccl: ncclCommInitAll + grouped ncclReduce)")
+    ap.add_argument("--final-composite", choices=["inline", "side"], default="inline",
+                    help="N > 1 under a launcher: the all-reduce that ends a region runs on the march "
+                         "stream (inline: VPTMCM_ALLREDUCE_INLINE, no event hop to the side stream; "
+                         "the composite is about to be read) or on the side stream like the ones "
+                         "between launches, which overlap the next march")
     ap.add_argument("--per-pass-steps", type=int, default=64,
                     help="N > 1: passes of a second timed region compositing after EVERY pass "
                          "(north_star's 'all-reduce each progressive pass'; one launch per pass; "
@@ -347,6 +352,10 @@ def main():
     # the composite that ends a region (and runs every `every` passes): the
     # RCCL all-reduce across ranks, or the device-list handle's composite
     composite = r.allreduce_radiance if multi else (r.composite if grouped else None)
+    # the composite that ends a region (what the display reads next)
+    composite_last = composite
+    if multi and a.final_composite == "inline":
+        composite_last = lambda: r.allreduce_radiance(inline=True)  # noqa: E731
     single = not multi and not grouped
     n_unfused = a.unfused_steps if single else 0
     n_api = a.api_steps if single else 0
@@ -382,7 +391,7 @@ def main():
             launches.append(n)
             done += n
             if composite and ((first - 1 + done) % every == 0 or done == count):
-                composite()
+                (composite_last if done == count else composite)()
         return launches
 
     r.reset(mvp, seeds[0])

@@ -305,6 +305,13 @@ int vptmcm_comm_init(vptmcm* h, const uint8_t* unique_id, int nranks, int rank);
  * buffered, overlapping the next march). */
 int vptmcm_comm_allreduce_radiance(vptmcm* h);
 
+/* The same with flags. VPTMCM_ALLREDUCE_INLINE: the all-reduce runs on the
+ * march stream itself, behind the last pass (no hop to the side stream: the
+ * lowest latency for a composite about to be read / shown; the next march
+ * waits for it). Same results either way. */
+#define VPTMCM_ALLREDUCE_INLINE 1u
+int vptmcm_comm_allreduce_radiance_ex(vptmcm* h, uint32_t flags);
+
 /* Wait for the last all-reduce and return the composite rgb = sum(rgb*n)/sum(n)
  * (R*R*3 floats) and, if counts != NULL, the summed n per pixel. The division
  * and the rgba16float conversion run on the device (k_composite). */

@@ -64,8 +64,8 @@ DRIVER = textwrap.dedent('''
             LOG.append(["timing"])
         def kernel_time(self):
             return (time.perf_counter() - self.t0) * 1e3 + 1e-3, self.launches
-        def allreduce_radiance(self):
-            LOG.append(["allreduce"])
+        def allreduce_radiance(self, inline=False):
+            LOG.append(["allreduce_inline" if inline else "allreduce"])
             if os.environ.get("FAKE_DIE_RANK") == os.environ["RANK"]:
                 os._exit(3)  # this rank dies before its first composite
         def read_composite(self):
@@ -135,11 +135,12 @@ def test_bench_two_ranks_driver_command_line(tmp_path, world):
         kinds = [e[0] for e in timed]
         assert sum(len(e[1]) for e in timed if e[0] == "passes") == 20
         last_pass = max(i for i, k in enumerate(kinds) if k == "passes")
-        assert "allreduce" in kinds[last_pass:], "timed region must end with a composite"
+        # the region ends with a composite, the last one inline (about to be read)
+        assert kinds[last_pass + 1] == "allreduce_inline", "timed region must end with a composite"
         assert kinds.index("composite") > last_pass
         # per-pass compositing region: 64 one-pass launches, each followed by an all-reduce
-        rk = [e[0] for e in rest if e[0] in ("passes", "allreduce")]
-        assert rk[:128] == ["passes", "allreduce"] * 64
+        rk = [e[0] for e in rest if e[0] in ("passes", "allreduce", "allreduce_inline")]
+        assert rk[:128] == ["passes", "allreduce"] * 63 + ["passes", "allreduce_inline"]
         assert all(len(e[1]) == 1 for e in rest if e[0] == "passes")
     seeds = [[s for e in lg if e[0] == "passes" for s in e[1]] for lg in logs]
     for a in range(world):
@@ -255,7 +256,7 @@ def test_bench_gpus4_without_launcher_is_one_device_list_handle(tmp_path, transp
     log = json.loads((tmp_path / "log.json").read_text())
     creates = [e for e in log if e[0].startswith("create")]
     assert creates == [["create_group", 16, [0, 1, 2, 3], 0 if transport == "peer" else 1, 3]]
-    assert not [e for e in log if e[0] in ("comm_init", "allreduce")]
+    assert not [e for e in log if e[0] in ("comm_init", "allreduce", "allreduce_inline")]
     t = [e[0] for e in log].index("timing")
     after = [e[0] for e in log[t + 1:]]
     last_pass = max(i for i, k in enumerate(after[:after.index("read_group_composite")]) if k == "passes")

@@ -137,6 +137,13 @@ for s in $STEPS; do
       python3 -c "import json; d=json.load(open('$OUT/karg.json')); r=d['roofline']; print(json.dumps({'dev_kernarg': '$k', 'value': d['value'], 'region_wall_us': r['region_wall_us'], 'kernel_us': r['kernel_avg_us'], 'wall_minus_kernel_us': r['wall_minus_kernel_us']}))" >> $OUT/kernargab.jsonl
     done
     echo "kernargab rc=0" | tee -a $OUT/status.txt; cat $OUT/kernargab.jsonl ;;
+  finalab)  # one-rank RCCL path (VPTMCM_BENCH_FORCE_COMM=1), the driver's shape: the region's last all-reduce inline vs on the side stream
+    for f in ${FINAL_CASES:-side inline side inline side inline side inline}; do
+      VPTMCM_BENCH_FORCE_COMM=1 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --final-composite $f --per-pass-steps 64 > $OUT/final.json 2>> $OUT/finalab.err
+      rc=$?; [ $rc -ne 0 ] && { echo "finalab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      python3 -c "import json; d=json.load(open('$OUT/final.json')); r=d['roofline']; p=d['per_pass_allreduce']; print(json.dumps({'final': '$f', 'value': d['value'], 'region_wall_us': r['region_wall_us'], 'kernel_us': r['kernel_avg_us'], 'wall_minus_kernel_us': r['wall_minus_kernel_us'], 'per_pass_us': round(p['ms_per_step'] * 1e3, 2)}))" >> $OUT/finalab.jsonl
+    done
+    echo "finalab rc=0" | tee -a $OUT/status.txt; cat $OUT/finalab.jsonl ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)

@@ -2387,10 +2387,13 @@ int vptmcm_comm_init(vptmcm* h, const uint8_t* uid, int nranks, int rank) {
   return VPTMCM_OK;
 }
 
-int vptmcm_comm_allreduce_radiance(vptmcm* h) {
+int vptmcm_comm_allreduce_radiance(vptmcm* h) { return vptmcm_comm_allreduce_radiance_ex(h, 0u); }
+
+int vptmcm_comm_allreduce_radiance_ex(vptmcm* h, uint32_t flags) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!h->comm) FAIL(h, VPTMCM_ECOMM, "comm_allreduce_radiance: no communicator");
+  if (flags & ~(uint32_t)VPTMCM_ALLREDUCE_INLINE) FAIL(h, VPTMCM_EINVAL, "comm_allreduce_radiance: unknown flags");
   HIPCHK(h, hipSetDevice(h->device));
   int k = h->comp_next;
   if (!h->pack_fresh) {  // the stream does not end with a march that packed comp[k]
@@ -2400,14 +2403,27 @@ int vptmcm_comm_allreduce_radiance(vptmcm* h) {
     MarchParams P = make_params(h, kNoMatrix, 0);
     HIPCHK(h, launch_pack(P, h->photons, h->rgb32, h->comp[k], enq(h)));
   }
-  stream_op(h);
-  HIPCHK(h, hipEventRecord(h->comp_ready[k], enq(h)));
-  HIPCHK(h, hipStreamWaitEvent(h->comm_stream, h->comp_ready[k], 0));
-  if (int rc = comm_call(h, ncclAllReduce(h->comp[k], h->comp[k], (size_t)h->R * h->R * 4,
-                                          ncclFloat32, ncclSum, h->comm, h->comm_stream),
-                         "comm_allreduce_radiance"))
-    return rc;
-  HIPCHK(h, hipEventRecord(h->comp_done[k], h->comm_stream));
+  if (flags & VPTMCM_ALLREDUCE_INLINE) {
+    // On the march stream itself, right behind the pack: no event hop to the
+    // side stream (the composite about to be shown is ready soonest); the
+    // next march waits for it. Ordered after the side stream's last
+    // all-reduce, so the communicator's collectives stay in issue order.
+    HIPCHK(h, hipStreamWaitEvent(enq(h), h->comp_done[k ^ 1], 0));
+    if (int rc = comm_call(h, ncclAllReduce(h->comp[k], h->comp[k], (size_t)h->R * h->R * 4,
+                                            ncclFloat32, ncclSum, h->comm, enq(h)),
+                           "comm_allreduce_radiance"))
+      return rc;
+    HIPCHK(h, hipEventRecord(h->comp_done[k], enq(h)));
+  } else {
+    stream_op(h);
+    HIPCHK(h, hipEventRecord(h->comp_ready[k], enq(h)));
+    HIPCHK(h, hipStreamWaitEvent(h->comm_stream, h->comp_ready[k], 0));
+    if (int rc = comm_call(h, ncclAllReduce(h->comp[k], h->comp[k], (size_t)h->R * h->R * 4,
+                                            ncclFloat32, ncclSum, h->comm, h->comm_stream),
+                           "comm_allreduce_radiance"))
+      return rc;
+    HIPCHK(h, hipEventRecord(h->comp_done[k], h->comm_stream));
+  }
   h->comp_last = k;
   h->comp_next = k ^ 1;
   return VPTMCM_OK;
@@ -2466,6 +2482,8 @@ int vptmcm_read_composite(vptmcm* h, uint16_t* rgba16f, float* rgb, float* count
   memset(&S, 0, sizeof S);
   S.n = 1;
   S.p[0] = h->comp[h->comp_last];
+  // (an all-reduce issued inline ran on the march stream)
+  HIPCHK(h, hipStreamWaitEvent(h->comm_stream, h->comp_done[h->comp_last], 0));
   HIPCHK(h, launch_composite(S, (uint32_t)npx, h->comp_rgb32, h->comp_rgba, h->comp_counts,
                              h->comm_stream));
   if (rgba16f)

@@ -11,6 +11,7 @@
  */
 #define NAPI_VERSION 8
 #include <node_api.h>
+#include <stdbool.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -469,12 +470,24 @@ static napi_value js_comm_init(napi_env env, napi_callback_info info) {
                                           (int)get_u32(env, argv[3])));
 }
 
+/* commAllreduceRadiance(h[, inline]): inline = true runs the all-reduce on
+ * the march stream (VPTMCM_ALLREDUCE_INLINE, for a composite about to be shown) */
 static napi_value js_comm_allreduce_radiance(napi_env env, napi_callback_info info) {
-    napi_value argv[1];
-    if (get_args(env, info, 1, argv)) return NULL;
+    napi_value argv[2];
+    size_t argc = 2;
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return NULL;
+    if (argc < 1) {
+        napi_throw_type_error(env, NULL, "too few arguments");
+        return NULL;
+    }
     vptmcm* h = get_handle(env, argv[0]);
     if (!h) return NULL;
-    return check(env, h, vptmcm_comm_allreduce_radiance(h));
+    bool inl = false;
+    if (argc > 1 && napi_get_value_bool(env, argv[1], &inl) != napi_ok) {
+        napi_throw_type_error(env, NULL, "inline must be a boolean");
+        return NULL;
+    }
+    return check(env, h, vptmcm_comm_allreduce_radiance_ex(h, inl ? VPTMCM_ALLREDUCE_INLINE : 0u));
 }
 
 /* commReadComposite(h, Float32Array(R*R*3), R) */

@@ -18,6 +18,7 @@ LIB_DIR = PKG / "lib"
 VARIANT_DIR = PKG.parent / "build" / "variants"
 
 OK, EINVAL, EHIP, ESTATE, ENOMEM, ECOMM = 0, -1, -2, -3, -4, -5
+ALLREDUCE_INLINE = 1  # VPTMCM_ALLREDUCE_INLINE
 LAYOUT_LINEAR, LAYOUT_CORNER8, LAYOUT_BRICK8, LAYOUT_COLUMN4 = 0, 1, 2, 3
 RENDERER_SPECTRAL, RENDERER_RGB = 0, 1
 PHOTON_RGB_BYTES = 64
@@ -34,7 +35,8 @@ EXPORTS = [
     "vptmcm_read_rgba16f", "vptmcm_read_rgb", "vptmcm_pack_radiance", "vptmcm_read_photons", "vptmcm_write_photons",
     "vptmcm_tonemap_artistic", "vptmcm_set_transfer_function", "vptmcm_set_environment",
     "vptmcm_enable_kernel_timing", "vptmcm_kernel_time", "vptmcm_comm_unique_id",
-    "vptmcm_comm_init", "vptmcm_comm_allreduce_radiance", "vptmcm_comm_read_composite",
+    "vptmcm_comm_init", "vptmcm_comm_allreduce_radiance", "vptmcm_comm_allreduce_radiance_ex",
+    "vptmcm_comm_read_composite",
     "vptmcm_comm_barrier", "vptmcm_comm_allreduce_host", "vptmcm_debug_eval",
     "vptmcm_debug_verify", "vptmcm_debug_last_launch", "vptmcm_debug_schedule", "vptmcm_version",
     "vptmcm_read_composite", "vptmcm_composite", "vptmcm_group_devices",
@@ -119,6 +121,7 @@ def load() -> C.CDLL:
         "vptmcm_comm_unique_id": (C.c_int, [u8p]),
         "vptmcm_comm_init": (C.c_int, [vp, u8p, C.c_int, C.c_int]),
         "vptmcm_comm_allreduce_radiance": (C.c_int, [vp]),
+        "vptmcm_comm_allreduce_radiance_ex": (C.c_int, [vp, C.c_uint32]),
         "vptmcm_comm_read_composite": (C.c_int, [vp, f32p, f32p]),
         "vptmcm_comm_barrier": (C.c_int, [vp]),
         "vptmcm_comm_allreduce_host": (C.c_int, [vp, C.POINTER(C.c_double), C.c_int, C.c_int]),
@@ -398,8 +401,13 @@ class Renderer:
         u = (C.c_uint8 * 128).from_buffer_copy(uid)
         self._ck(self.L.vptmcm_comm_init(self.h, u, nranks, rank))
 
-    def allreduce_radiance(self) -> None:
-        self._ck(self.L.vptmcm_comm_allreduce_radiance(self.h))
+    def allreduce_radiance(self, inline: bool = False) -> None:
+        """The cross-rank composite; inline=True runs it on the march stream
+        (VPTMCM_ALLREDUCE_INLINE: soonest ready, the next march waits)."""
+        if inline:
+            self._ck(self.L.vptmcm_comm_allreduce_radiance_ex(self.h, ALLREDUCE_INLINE))
+        else:
+            self._ck(self.L.vptmcm_comm_allreduce_radiance(self.h))
 
     def read_composite(self):
         rgb = np.empty((self.R, self.R, 3), np.float32)
