@@ -144,14 +144,6 @@ for s in $STEPS; do
       python3 -c "import json; d=json.load(open('$OUT/final.json')); r=d['roofline']; p=d['per_pass_allreduce']; print(json.dumps({'final': '$f', 'value': d['value'], 'region_wall_us': r['region_wall_us'], 'kernel_us': r['kernel_avg_us'], 'wall_minus_kernel_us': r['wall_minus_kernel_us'], 'per_pass_us': round(p['ms_per_step'] * 1e3, 2)}))" >> $OUT/finalab.jsonl
     done
     echo "finalab rc=0" | tee -a $OUT/status.txt; cat $OUT/finalab.jsonl ;;
-  fenceab)  # device-list composite chain (N = 2, one GPU) with the pack events' system fence on / off
-    for f in ${FENCE_CASES:-system agent system agent}; do
-      (cd /tmp && export TMPDIR=/tmp VPTMCM_GROUP_FENCE=$f && timeout -k 10 300 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$OUT/fence_$f" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/group_enqueue.py" --ns 2 --reps 20 --composite --threads on > /dev/null 2>> "$GRAFT_REPO_ROOT/$OUT/fenceab.err")
-      rc=$?; [ $rc -ne 0 ] && { echo "fenceab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
-      python3 -c "import json,subprocess; r=json.loads(subprocess.check_output(['python3','tools/composite_trace.py','$OUT/fence_$f/run_kernel_trace.csv'])); r['fence']='$f'; print(json.dumps(r))" >> $OUT/fenceab.jsonl
-      rm -rf $OUT/fence_$f
-    done
-    echo "fenceab rc=0" | tee -a $OUT/status.txt; cat $OUT/fenceab.jsonl ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)
