@@ -76,8 +76,9 @@ def parse():
                     help="passes between radiance composites (N > 1)")
     ap.add_argument("--transport", choices=["peer", "rccl"], default="peer",
                     help="N > 1 without a launcher: the device-list composite's transport "
-                         "(peer: every GPU pushes its (rgb*n, n) buffer to device 0 over its own "
-                         "xGMI link; rccl: ncclCommInitAll + grouped ncclReduce)")
+                         "(peer: sharded, every GPU composites 1/N of the frame from every GPU's "
+                         "(rgb*n, n) buffer over xGMI peer reads; rccl: ncclCommInitAll + grouped "
+                         "ncclReduce to device 0)")
     ap.add_argument("--final-composite", choices=["inline", "side"], default="inline",
                     help="N > 1 under a launcher: the all-reduce that ends a region runs on the march "
                          "stream (inline: VPTMCM_ALLREDUCE_INLINE, no event hop to the side stream; "
@@ -695,7 +696,7 @@ def main():
         parallelism = (f"photon-parallel replicas x{group} in one process (device-list handle over "
                        f"devices {devs}), composite of (rgb*n, n) on device {devs[0]} every {every} "
                        f"pass(es)")
-        comp_kind = {"peer": "peer-push", "rccl": "rccl-reduce"}[a.transport]
+        comp_kind = {"peer": "peer-sharded", "rccl": "rccl-reduce"}[a.transport]
     else:
         parallelism, comp_kind = "single GPU", None
     if rank == 0:

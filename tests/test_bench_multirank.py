@@ -250,7 +250,7 @@ def test_bench_gpus4_without_launcher_is_one_device_list_handle(tmp_path, transp
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 4 and rec["config"]["workload"].startswith("custom: 16^3")
     assert rec["config"]["devices"] == [0, 1, 2, 3]
-    assert rec["config"]["composite_transport"] == {"peer": "peer-push", "rccl": "rccl-reduce"}[transport]
+    assert rec["config"]["composite_transport"] == {"peer": "peer-sharded", "rccl": "rccl-reduce"}[transport]
     assert "one process" in rec["config"]["parallelism"] and "x4" in rec["config"]["parallelism"]
     assert rec["cpu_baseline"] is None and rec["unfused"] is None
     log = json.loads((tmp_path / "log.json").read_text())

@@ -292,6 +292,6 @@ def test_bench_launcherless_two_gpus_repeated_device():
     assert p.returncode == 0, p.stdout + p.stderr[-3000:]
     rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["n_gpus"] == 2 and rec["config"]["devices"] == [0, 0]
-    assert rec["config"]["composite_transport"] == "peer-push" and "one process" in rec["config"]["parallelism"]
+    assert rec["config"]["composite_transport"] == "peer-sharded" and "one process" in rec["config"]["parallelism"]
     assert rec["value"] > 0 and rec["per_pass_allreduce"]["value"] > 0
     assert rec["roofline"]["passes_per_launch"] == 20
