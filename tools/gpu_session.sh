@@ -144,6 +144,14 @@ for s in $STEPS; do
       python3 -c "import json; d=json.load(open('$OUT/final.json')); r=d['roofline']; p=d['per_pass_allreduce']; print(json.dumps({'final': '$f', 'value': d['value'], 'region_wall_us': r['region_wall_us'], 'kernel_us': r['kernel_avg_us'], 'wall_minus_kernel_us': r['wall_minus_kernel_us'], 'per_pass_us': round(p['ms_per_step'] * 1e3, 2)}))" >> $OUT/finalab.jsonl
     done
     echo "finalab rc=0" | tee -a $OUT/status.txt; cat $OUT/finalab.jsonl ;;
+  majab)  # the macro-cell alpha bound off (VPTMCM_MARCH_VARIANT=256) / on, default and near camera, alternating
+    for c in ${MAJ_CASES:-256:default 0:default 256:near 0:near 256:default 0:default 256:near 0:near}; do
+      IFS=: read v cam <<< "$c"
+      VPTMCM_MARCH_VARIANT=$v timeout -k 10 300 python bench.py --camera $cam --steps 256 --warmup 1024 --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 0 --unfused-steps 64 --near-steps 0 > $OUT/maj.json 2>> $OUT/majab.err
+      rc=$?; [ $rc -ne 0 ] && { echo "majab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      python3 -c "import json; d=json.load(open('$OUT/maj.json')); print(json.dumps({'variant': $v, 'camera': '$cam', 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'unfused_us': d['unfused']['kernel_avg_us']}))" >> $OUT/majab.jsonl
+    done
+    echo "majab rc=0" | tee -a $OUT/status.txt; cat $OUT/majab.jsonl ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)

@@ -95,7 +95,17 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba, float* rgb32,
                         hipStream_t s, hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr,
                         const uint32_t* tf_rows = nullptr, const uint8_t* tf_rowmap = nullptr,
-                        const uint32_t* bin_lut = nullptr, MarchLaunchInfo* info = nullptr);
+                        const uint32_t* bin_lut = nullptr, MarchLaunchInfo* info = nullptr,
+                        const uint8_t* maj = nullptr);
+// Macro-cell alpha bound (MarchParams::maj_*): the density range of the macro
+// cells of the box [m0, m0 + mn) from the linear staging volume, and the
+// 4-bit alpha codes of all n cells from those ranges and the TF's per-row
+// maximum alpha byte
+hipError_t launch_macro_minmax(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, uint32_t shift,
+                               uint32_t nx, uint32_t ny, const uint32_t m0[3], const uint32_t mn[3],
+                               uint16_t* mm, hipStream_t s);
+hipError_t launch_macro_alpha(const uint16_t* mm, uint32_t n, const uint8_t* rowmax, uint8_t* q,
+                              uint32_t bytes, hipStream_t s);
 // Artistic tone mapper uniforms, derived on the host from (low, mid, high,
 // saturation, gamma) (WebGPUArtisticToneMapper.js:81-88, ArtisticToneMapper.wgsl:40-46).
 struct ToneParams {

@@ -152,14 +152,29 @@ __device__ __forceinline__ uint2 load8_a4(const uint8_t* __restrict__ p) {
   return make_uint2(v.x, v.y);
 }
 
-template <uint32_t L>
-__device__ __forceinline__ VolTap vol_fetch(const MarchParams& P, const uint8_t* __restrict__ vol,
-                                            f3 q) {
-  VolTap t;
+// The texel cell of a sample position: floor and fraction per axis (the
+// cell's corner voxels are ix .. ix + 1, clamped by the layout).
+struct VolCell {
+  int ix, iy, iz;
+  float fx, fy, fz;
+};
+__device__ __forceinline__ VolCell vol_cell(const MarchParams& P, f3 q) {
+  VolCell c;
   // q is an arithmetic result (the advanced position), never a signalling NaN
-  int ix = axis_floor_q(q.x, (float)P.W, &t.fx);
-  int iy = axis_floor_q(q.y, (float)P.H, &t.fy);
-  int iz = axis_floor_q(q.z, (float)P.D, &t.fz);
+  c.ix = axis_floor_q(q.x, (float)P.W, &c.fx);
+  c.iy = axis_floor_q(q.y, (float)P.H, &c.fy);
+  c.iz = axis_floor_q(q.z, (float)P.D, &c.fz);
+  return c;
+}
+
+template <uint32_t L>
+__device__ __forceinline__ VolTap vol_fetch_cell(const MarchParams& P, const uint8_t* __restrict__ vol,
+                                                 const VolCell& vc) {
+  VolTap t;
+  t.fx = vc.fx;
+  t.fy = vc.fy;
+  t.fz = vc.fz;
+  const int ix = vc.ix, iy = vc.iy, iz = vc.iz;
   if constexpr (L == kTplBrick8 || L == kTplBrick8Wide) {
     const uint32_t cx = (uint32_t)(clampi(ix + 1, (int)P.W));
     const uint32_t cy = (uint32_t)(clampi(iy + 1, (int)P.H));
@@ -221,6 +236,29 @@ __device__ __forceinline__ VolTap vol_fetch(const MarchParams& P, const uint8_t*
            ((uint32_t)vol[r11 + x0] << 16) | ((uint32_t)vol[r11 + x1] << 24);
   }
   return t;
+}
+
+template <uint32_t L>
+__device__ __forceinline__ VolTap vol_fetch(const MarchParams& P, const uint8_t* __restrict__ vol,
+                                            f3 q) {
+  return vol_fetch_cell<L>(P, vol, vol_cell(P, q));
+}
+
+// Macro-cell alpha bound (MarchParams::maj_on): the 4-bit code of the macro
+// cell holding texel cell (clamp(ix + 1, W), ...) — the cell index every layout
+// gathers — and the wheel value from which a step there is a certain null
+// collision. The code q bounds every alpha byte the cell's samples can reach
+// (q * 17 >= it, host/k_macro_alpha); with alpha <= RN(q*17 * RN(1/255)) the
+// reference's pabs and pabs + pscat (1 - RN(1 - alpha) - pscat, then + pscat,
+// in f32) stay below alpha + 2^-21, under fma(q*17, RN(1/255), 2^-16).
+__device__ __forceinline__ float maj_threshold(const MarchParams& P, const VolCell& vc,
+                                               const uint8_t* s_maj) {
+  const uint32_t mx = (uint32_t)clampi(vc.ix + 1, (int)P.W) >> P.maj_shift;
+  const uint32_t my = (uint32_t)clampi(vc.iy + 1, (int)P.H) >> P.maj_shift;
+  const uint32_t mz = (uint32_t)clampi(vc.iz + 1, (int)P.D) >> P.maj_shift;
+  const uint32_t m = mad_u24(mad_u24(mz, P.maj_ny, my), P.maj_nx, mx);
+  const uint32_t q = ((uint32_t)s_maj[m >> 1] >> ((m & 1u) << 2)) & 15u;
+  return fmaf((float)(q * 17u), kInv255, 0x1p-16f);
 }
 
 __device__ __forceinline__ float vol_filter(const VolTap& t) {
@@ -493,7 +531,8 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
                                                        uint16_t* __restrict__ rgba,
                                                        float* __restrict__ rgb32,
                                                        const uint8_t* __restrict__ tf_rowmap,
-                                                       const uint32_t* __restrict__ bin_lut) {
+                                                       const uint32_t* __restrict__ bin_lut,
+                                                       const uint8_t* __restrict__ maj) {
   constexpr bool NBF = MODE >= 1u && MODE <= 3u;
   constexpr bool GEO = MODE >= 2u;    // FAST geometry and light (MODE 2 to 5)
   constexpr bool UNIB = MODE == 2u || MODE == 3u;  // ... and 12 equal-width bins
@@ -510,6 +549,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __shared__ float s_brow[256];
   __shared__ uint32_t s_rowmap[256];  // P.tf_dedup: density row -> first texel of its distinct row
   __shared__ uint32_t s_binlut[LUTB ? kBinLutCells + kBinLutCells / 4 : 1];  // MODE 6 / 7
+  __shared__ uint4 s_maj4[SPEC ? kMajBytes / 16 : 1];  // macro-cell alpha codes (P.maj_on)
 
   __shared__ uint32_t s_red[64];
   __shared__ uint32_t s_tile[16];
@@ -520,6 +560,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     poison_lds(s_brow, sizeof s_brow);
     poison_lds(s_rowmap, sizeof s_rowmap);
     poison_lds(s_binlut, sizeof s_binlut);
+    poison_lds(s_maj4, sizeof s_maj4);
     poison_lds(s_red, sizeof s_red);
     poison_lds(s_tile, sizeof s_tile);
     poison_lds(&s_done, sizeof s_done);
@@ -627,6 +668,11 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 #pragma unroll
     for (uint32_t k = 0; k < 2u; k++)
       if (threadIdx.x + k * kMarchBlock < kLutWords) s_binlut[threadIdx.x + k * kMarchBlock] = binlut_v[k];
+  }
+  if constexpr (SPEC) {  // the macro-cell table (<= 20 KB: at most two 16-B words per thread)
+    if (P.maj_on != 0u)
+      for (uint32_t k = threadIdx.x; k < P.maj_bytes / 16u; k += kMarchBlock)
+        s_maj4[k] = reinterpret_cast<const uint4*>(maj)[k];
   }
   __syncthreads();
   if (live && !hot0) load_photon(ph, S, i, p);
@@ -880,7 +926,17 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
 
       entered = kFlagVolume;
       STAMP_AT(0);
-      const VolTap vt = vol_fetch<L>(P, vol, p.pos);  // gather in flight from here
+      // A lane whose wheel clears its macro cell's alpha bound takes the null
+      // collision whatever the sample: it skips the gather (no line fill); the
+      // decision below is masked for it, the other lanes' values are unchanged
+      const VolCell vcell = vol_cell(P, p.pos);
+      bool skip = false;
+      if (P.maj_on != 0u)
+        skip = !oob && wheel >= maj_threshold(P, vcell, reinterpret_cast<const uint8_t*>(s_maj4));
+      VolTap vt;
+      vt.fx = vt.fy = vt.fz = 0.0f;
+      vt.lo = vt.hi = 0u;
+      if (!skip) vt = vol_fetch_cell<L>(P, vol, vcell);  // gather in flight from here
 
       // Speculative candidates, all derived from the state after the wheel
       // draw and independent of the gather: the reset (draws h1..h5) and the
@@ -937,12 +993,12 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       float pabs = (1.0f - pnull) - pscat;
 
       STAMP_AT(3);
-      if (oob || wheel < pabs) {
+      if (oob || (!skip && wheel < pabs)) {
         // exit (wgsl:142-150) or absorption (wgsl:151-155): adopt the candidate
         terminate(oob ? exit_radiance<GEO>(P, p.dir, wc) : 0.0f, rc);
         wc = wcr;
         st = h5;
-      } else if (wheel < pabs + pscat) {
+      } else if (!skip && wheel < pabs + pscat) {
         // HG scatter (wgsl:82-97, :156-160) with g from the TF blue channel
         float bch = (FAST || (!DEDUP && P.b_rows)) ? lerp(s_brow[ri0], s_brow[ri1], fr) * kInv255
                              : lerp(lerp(byte_f(b4, 0), byte_f(b4, 8), wc.fc),
@@ -1362,6 +1418,71 @@ __global__ __launch_bounds__(256) void k_column4(const uint8_t* __restrict__ lin
   }
 }
 
+// ------------------------------------------------- macro-cell alpha bound
+// Density range of each macro cell (MarchParams::maj_*): macro m covers texel
+// cells [m << shift, (m + 1) << shift) per axis, i.e. (a cell's corners being
+// voxels c - 1 and c, clamped) voxels [(m << shift) - 1, ((m + 1) << shift) - 1]
+// clamped to the volume; min | max << 8 of those voxel bytes of the linear
+// staging copy. One block per macro cell of the box [m0, m0 + mn).
+__global__ __launch_bounds__(256) void k_macro_minmax(const uint8_t* __restrict__ lin, uint32_t W,
+                                                      uint32_t H, uint32_t D, uint32_t shift, uint32_t nx,
+                                                      uint32_t ny, uint3 m0, uint3 mn,
+                                                      uint16_t* __restrict__ mm) {
+  __shared__ uint32_t s_r[8];
+  const uint32_t b = blockIdx.x;
+  const uint32_t mx = m0.x + b % mn.x, my = m0.y + (b / mn.x) % mn.y, mz = m0.z + b / (mn.x * mn.y);
+  auto lo = [&](uint32_t m) { return (m << shift) == 0u ? 0u : (m << shift) - 1u; };
+  auto hi = [&](uint32_t m, uint32_t n) { return min(((m + 1u) << shift) - 1u, n - 1u); };  // inclusive
+  const uint32_t x0 = lo(mx), x1 = hi(mx, W), y0 = lo(my), y1 = hi(my, H), z0 = lo(mz), z1 = hi(mz, D);
+  const uint32_t wx = x1 - x0 + 1u, wy = y1 - y0 + 1u, rows = wy * (z1 - z0 + 1u);
+  uint32_t vmin = 255u, vmax = 0u;
+  for (uint32_t r = threadIdx.x; r < rows; r += 256u) {
+    const uint8_t* row = lin + ((size_t)(z0 + r / wy) * H + (y0 + r % wy)) * W + x0;
+    for (uint32_t k = 0; k < wx; k++) {
+      const uint32_t v = row[k];
+      vmin = min(vmin, v);
+      vmax = max(vmax, v);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    vmin = min(vmin, (uint32_t)__shfl_xor((int)vmin, o, 64));
+    vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+  }
+  if ((threadIdx.x & 63u) == 0u) {
+    s_r[threadIdx.x >> 6] = vmin;
+    s_r[4u + (threadIdx.x >> 6)] = vmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0u) {
+    const uint32_t a = min(min(s_r[0], s_r[1]), min(s_r[2], s_r[3]));
+    const uint32_t c = max(max(s_r[4], s_r[5]), max(s_r[6], s_r[7]));
+    mm[((size_t)mz * ny + my) * nx + mx] = (uint16_t)(a | (c << 8));
+  }
+}
+
+// The 4-bit alpha codes of n macro cells: q = ceil(k / 17), k the largest
+// alpha byte of the TF rows [min - 2, max + 2] (every row a filtered density
+// in [min, max] / 255 can reach: its row index is within one of the byte
+// value) over all columns (rowmax, host). Two cells per byte, low nibble first.
+__global__ __launch_bounds__(256) void k_macro_alpha(const uint16_t* __restrict__ mm, uint32_t n,
+                                                     const uint8_t* __restrict__ rowmax,
+                                                     uint8_t* __restrict__ q, uint32_t bytes) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= bytes) return;
+  uint32_t out = 0u;
+  for (uint32_t h = 0; h < 2u; h++) {
+    const uint32_t m = 2u * i + h;
+    if (m >= n) break;
+    const uint32_t v = mm[m], vmin = v & 0xffu, vmax = v >> 8;
+    const uint32_t r0 = vmin >= 2u ? vmin - 2u : 0u, r1 = min(vmax + 2u, 255u);
+    uint32_t k = 0u;
+    for (uint32_t r = r0; r <= r1; r++) k = max(k, (uint32_t)rowmax[r]);
+    out |= ((k + 16u) / 17u) << (4u * h);
+  }
+  q[i] = (uint8_t)out;
+}
+
 // ----------------------------------------------------- multi-GPU composite
 // (rgb * n, n) per pixel from the fp32 image of the last pass (before its f16
 // rounding) and the photon sample count n: the running mean rgb weighted by
@@ -1531,7 +1652,7 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
                         const uint8_t* tf_brow, const uint8_t* light, uint16_t* rgba, float* rgb32,
                         hipStream_t s, hipEvent_t ev_beg, hipEvent_t ev_end,
                         const uint32_t* tf_rows, const uint8_t* tf_rowmap, const uint32_t* bin_lut,
-                        MarchLaunchInfo* info) {
+                        MarchLaunchInfo* info, const uint8_t* maj) {
   dim3 grid(tile_blocks(P, kMarchBlock));
   // variant bits (analysis; results identical; bits 1-3 are the host's):
   // 0 plain (non-speculative) step, 4 none of the GEO specialisations (MODE 1
@@ -1546,6 +1667,8 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   // (P.tf_dedup on entry: the host found <= kTfRowsMax distinct rows)
   MarchParams Q = P;
   Q.tf_dedup = (P.tf_dedup && tf_rows && tf_rowmap && spec && !fast) ? 1u : 0u;
+  // the macro-cell bound serves the speculative step loop (variant bit 8: off)
+  Q.maj_on = (P.maj_on && maj && spec && (variant & 256u) == 0u) ? 1u : 0u;
   // MODE 4 / 5 -> 6 / 7 with the wavelength-bin table (variant bit 6: without)
   const bool lut = P.bins_lut && bin_lut && (variant & 64u) == 0u;
   const uint16_t* tf_lds = Q.tf_dedup ? reinterpret_cast<const uint16_t*>(tf_rows) : tf_rg;
@@ -1569,7 +1692,7 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   // (no extra barrier/marker packets between back-to-back launches)
 #define VPT_LAUNCH(LAY, SP, MO)                                                                \
   hipExtLaunchKernelGGL((k_march<LAY, SP, MO>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
-                        PS, Q, T, ph, vol, tf_lds, tf_b4, tf_brow, light, rgba, rgb32, rowmap, bin_lut)
+                        PS, Q, T, ph, vol, tf_lds, tf_b4, tf_brow, light, rgba, rgb32, rowmap, bin_lut, maj)
 #define VPT_LAUNCH_NB(LAY)                 \
   do {                                     \
     switch (spec ? mode : 8u + mode) {     \
@@ -1683,6 +1806,23 @@ hipError_t guard_take_oob(uint32_t* out) {
   *out = 0u;
   return hipSuccess;
 #endif
+}
+
+hipError_t launch_macro_minmax(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, uint32_t shift,
+                               uint32_t nx, uint32_t ny, const uint32_t m0[3], const uint32_t mn[3],
+                               uint16_t* mm, hipStream_t s) {
+  const uint32_t blocks = mn[0] * mn[1] * mn[2];
+  if (blocks == 0u) return hipSuccess;
+  hipLaunchKernelGGL(k_macro_minmax, dim3(blocks), dim3(256), 0, s, lin, W, H, D, shift, nx, ny,
+                     make_uint3(m0[0], m0[1], m0[2]), make_uint3(mn[0], mn[1], mn[2]), mm);
+  return hipGetLastError();
+}
+
+hipError_t launch_macro_alpha(const uint16_t* mm, uint32_t n, const uint8_t* rowmax, uint8_t* q,
+                              uint32_t bytes, hipStream_t s) {
+  if (bytes == 0u) return hipSuccess;
+  hipLaunchKernelGGL(k_macro_alpha, dim3((bytes + 255u) / 256u), dim3(256), 0, s, mm, n, rowmax, q, bytes);
+  return hipGetLastError();
 }
 
 hipError_t launch_pack(const MarchParams& P, const float* ph, const float* rgb32, float4* out,

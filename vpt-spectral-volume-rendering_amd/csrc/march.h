@@ -129,7 +129,18 @@ struct MarchParams {
   // 1 unless the host touched the schedule state since (first launch,
   // VPTMCM_SCHED_CACHE=0).
   uint32_t launch_seq, sched_reuse;
+  // Macro-cell alpha bound (k_march's certain null collisions, MODE-independent):
+  // texel cells (cx, cy, cz) >> maj_shift index a maj_nx x maj_ny x maj_nz table
+  // of 4-bit codes q (two per byte, maj_bytes staged in LDS, a multiple of 16),
+  // each with q * 17 >= every alpha byte of every TF texel a sample in those
+  // cells can reach; a lane whose wheel draw clears the code's bound takes the
+  // null collision without the volume gather (same decision, kernels.hip
+  // maj_threshold). maj_on 0: no table.
+  uint32_t maj_on, maj_shift, maj_nx, maj_ny, maj_bytes;
 };
+// Byte capacity of the LDS macro table (nibbles: 40,960 macro cells, e.g. 33^3
+// cells of 16^3 texel cells at 512^3)
+constexpr uint32_t kMajBytes = 20480;
 constexpr uint32_t kBinLutCells = 1024u;
 constexpr uint32_t kBinLutShift = 22u;
 

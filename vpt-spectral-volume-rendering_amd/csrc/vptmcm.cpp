@@ -193,6 +193,15 @@ struct vptmcm {
   uint32_t* tf_rows = nullptr;   // kTfRowsMax distinct TF rows, u32 texels (valid when tf_dedup)
   uint8_t* tf_rowmap = nullptr;  // density row -> distinct row
   uint32_t* bin_lut = nullptr;   // MarchParams::bins_lut table (device)
+  // Macro-cell alpha bound (MarchParams::maj_*): per macro cell the volume's
+  // byte range (maj_mm, kept current by every relayout) and the 4-bit alpha
+  // codes the march stages in LDS (maj_q, rebuilt before a march whenever the
+  // volume or the TF changed: maj_valid); tf_rowmax = max alpha byte per TF row
+  uint16_t* maj_mm = nullptr;
+  uint8_t* maj_q = nullptr;
+  uint8_t* tf_rowmax = nullptr;
+  uint32_t maj_shift = 0, maj_nx = 0, maj_ny = 0, maj_nz = 0, maj_n = 0, maj_bytes = 0;
+  bool maj_ok = false, maj_valid = false;
   bool bin_lut_ok = false;
   uint32_t bin_lut_host[kBinLutCells + kBinLutCells / 4] = {};
   uint32_t tf_dedup = 0;
@@ -771,11 +780,23 @@ int flush_relayout(vptmcm* h) {
     const uint32_t z1 = std::min(h->vol_c1[2] + 1u, h->D + 2u);
     const uint32_t nq[3] = {n[0], n[1], z1 - h->vol_c0[2]};
     HIPCHK(h, launch_column4(h->vol_lin, h->W, h->H, h->D, h->vol_c8, enq(h), h->vol_c0, nq));
-    return guard_check(h, "relayout");
+  } else {
+    HIPCHK(h, launch_corner8(h->vol_lin, h->W, h->H, h->D, brick ? (h->W + kBrickCells) / kBrickCells : 0u,
+                             brick ? (h->H + kBrickCells) / kBrickCells : 0u, h->vol_c8, enq(h),
+                             h->vol_c0, n));
   }
-  HIPCHK(h, launch_corner8(h->vol_lin, h->W, h->H, h->D, brick ? (h->W + kBrickCells) / kBrickCells : 0u,
-                           brick ? (h->H + kBrickCells) / kBrickCells : 0u, h->vol_c8, enq(h),
-                           h->vol_c0, n));
+  if (h->maj_ok) {  // the macro cells the re-laid-out cells fall in
+    uint32_t m0[3], mn[3];
+    const uint32_t lim[3] = {h->maj_nx, h->maj_ny, h->maj_nz};
+    for (int k = 0; k < 3; k++) {
+      m0[k] = h->vol_c0[k] >> h->maj_shift;
+      const uint32_t m1 = std::min((h->vol_c1[k] + (1u << h->maj_shift) - 1u) >> h->maj_shift, lim[k]);
+      mn[k] = m1 > m0[k] ? m1 - m0[k] : 0u;
+    }
+    HIPCHK(h, launch_macro_minmax(h->vol_lin, h->W, h->H, h->D, h->maj_shift, h->maj_nx, h->maj_ny, m0, mn,
+                                  h->maj_mm, enq(h)));
+    h->maj_valid = false;
+  }
   return guard_check(h, "relayout");
 }
 
@@ -802,7 +823,18 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   if (n == 0) return VPTMCM_OK;
   if (n > kMaxFusedPasses) FAIL(h, VPTMCM_EINVAL, "internal: %u passes in one launch", n);
   if (int rc = flush_relayout(h)) return rc;
+  if (h->maj_ok && !h->maj_valid) {  // the volume or the TF changed since the codes were built
+    HIPCHK(h, launch_macro_alpha(h->maj_mm, h->maj_n, h->tf_rowmax, h->maj_q, h->maj_bytes, enq(h)));
+    h->maj_valid = true;
+  }
   MarchParams P = make_params(h, mvp, seeds[0]);
+  if (h->maj_ok) {
+    P.maj_on = 1u;
+    P.maj_shift = h->maj_shift;
+    P.maj_nx = h->maj_nx;
+    P.maj_ny = h->maj_ny;
+    P.maj_bytes = h->maj_bytes;
+  }
   PassSeeds PS;
   memset(&PS, 0, sizeof PS);
   PS.n = n;
@@ -850,7 +882,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   else
     HIPCHK(h, launch_march(h->layout, h->variant, P, PS, T, h->photons, vol, h->tf_rg, h->tf_b4,
                            h->tf_brow, h->light, h->rgba, h->rgb32, h->stream, eb, ee, h->tf_rows,
-                           h->tf_rowmap, h->bin_lut, &h->last_launch));
+                           h->tf_rowmap, h->bin_lut, &h->last_launch, h->maj_q));
   h->march_launches++;
   h->sched_cur = c ^ 1u;
   h->grp_dirty = true;
@@ -1166,8 +1198,13 @@ bool composited(const vptmcm* h) { return !h->peers.empty(); }
 void free_volume(vptmcm* h) {
   if (h->vol_lin) (void)dev_free(h->vol_lin);
   if (h->vol_c8) (void)dev_free(h->vol_c8);
+  if (h->maj_mm) (void)dev_free(h->maj_mm);
+  if (h->maj_q) (void)dev_free(h->maj_q);
   h->vol_lin = nullptr;
   h->vol_c8 = nullptr;
+  h->maj_mm = nullptr;
+  h->maj_q = nullptr;
+  h->maj_ok = h->maj_valid = false;
   h->volume_ready = false;
   h->vol_done = false;
   h->vol_dirty = false;
@@ -1579,6 +1616,8 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   CK(hipMemsetAsync(h->tf_rows, 0, kTfRowsMax * 256 * sizeof(uint32_t), enq(h)));
   CK(dev_alloc(&h->bin_lut, sizeof h->bin_lut_host));
   CK(hipMemsetAsync(h->bin_lut, 0, sizeof h->bin_lut_host, enq(h)));
+  CK(dev_alloc(&h->tf_rowmax, 256));
+  CK(hipMemsetAsync(h->tf_rowmax, 0, 256, enq(h)));  // the zero texture: alpha 0 in every row
   CK(dev_alloc(&h->tf_rowmap, 256));
   CK(hipMemsetAsync(h->tf_rowmap, 0, 256, enq(h)));
   CK(dev_alloc(&h->light, 256));
@@ -1698,6 +1737,7 @@ void vptmcm_destroy(vptmcm* h) {
   if (h->tf_brow) (void)dev_free(h->tf_brow);
   if (h->tf_rows) (void)dev_free(h->tf_rows);
   if (h->tf_rowmap) (void)dev_free(h->tf_rowmap);
+  if (h->tf_rowmax) (void)dev_free(h->tf_rowmax);
   if (h->bin_lut) (void)dev_free(h->bin_lut);
   if (h->light) (void)dev_free(h->light);
   if (h->sched) (void)dev_free(h->sched);
@@ -1762,6 +1802,34 @@ static int volume_begin_one(vptmcm* h, uint32_t width, uint32_t height, uint32_t
   h->W = width;
   h->H = height;
   h->D = depth;
+  // the macro-cell table: the finest power-of-two macro (>= 8 texel cells)
+  // whose codes fit the march's LDS table (spectral march, re-laid-out layouts)
+  if (h->kind == VPTMCM_RENDERER_SPECTRAL && h->layout != kLayoutLinear) {
+    for (uint32_t sh = 3; sh < 14 && !h->maj_ok; sh++) {
+      const uint64_t nx = ((uint64_t)width + (1u << sh)) >> sh, ny = ((uint64_t)height + (1u << sh)) >> sh,
+                     nz = ((uint64_t)depth + (1u << sh)) >> sh;  // ceil((W + 1) / M)
+      const uint64_t n = nx * ny * nz, bytes = ((n + 1) / 2 + 15) / 16 * 16;
+      if (bytes > kMajBytes) continue;
+      h->maj_shift = sh;
+      h->maj_nx = (uint32_t)nx;
+      h->maj_ny = (uint32_t)ny;
+      h->maj_nz = (uint32_t)nz;
+      h->maj_n = (uint32_t)n;
+      h->maj_bytes = (uint32_t)bytes;
+      h->maj_ok = true;
+    }
+    if (h->maj_ok) {
+      // a fresh volume reads zero: every macro cell's range is [0, 0]
+      if (dev_alloc(&h->maj_mm, (size_t)h->maj_n * sizeof(uint16_t)) != hipSuccess ||
+          dev_alloc(&h->maj_q, h->maj_bytes) != hipSuccess) {
+        free_volume(h);
+        FAIL(h, VPTMCM_ENOMEM, "macro-cell table allocation failed");
+      }
+      HIPCHK(h, hipMemsetAsync(h->maj_mm, 0, (size_t)h->maj_n * sizeof(uint16_t), enq(h)));
+      HIPCHK(h, hipMemsetAsync(h->maj_q, 0, h->maj_bytes, enq(h)));
+      h->maj_valid = false;
+    }
+  }
   h->volume_ready = true;
   return VPTMCM_OK;
 }
@@ -1867,6 +1935,15 @@ static int set_material_tf_one(vptmcm* h, const uint8_t* rgba) {
   }
   HIPCHK(h, hipMemcpyAsync(h->tf_brow, brow, 256, hipMemcpyHostToDevice, enq(h)));
   h->b_rows = inv;
+  // the largest alpha byte of each density row (the macro-cell alpha codes)
+  uint8_t rowmax[256];
+  for (int r = 0; r < 256; r++) {
+    uint8_t m = 0;
+    for (int c = 0; c < 256; c++) m = std::max(m, rgba[(r * 256 + c) * 4 + 1]);
+    rowmax[r] = m;
+  }
+  HIPCHK(h, hipMemcpyAsync(h->tf_rowmax, rowmax, 256, hipMemcpyHostToDevice, enq(h)));
+  h->maj_valid = false;
   // Distinct density rows over (albedo, alpha, anisotropy): a UI TF paints one
   // material's wavelength arrays into every row of a density range
   // (MaterialTransferFunction.js:56-75), so it has few; with <= kTfRowsMax of
