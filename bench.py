@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--bins", default="12", help="spectrum bin layout (non-12: analysis only)")
     ap.add_argument("--camera", choices=["default", "near", "orbit", "orbit_tilted"],
                     default="default", help="golden camera pose (non-default: analysis only)")
+    ap.add_argument("--camera-mix", type=float, default=None,
+                    help="analysis: blend the default and near cameras' inverse matrices, "
+                         "(1 - t) * default + t * near, for intermediate screen coverage")
     ap.add_argument("--fuse", type=int, default=32,
                     help="passes per march launch (render_passes; photon state stays in "
                          "registers between them, every pass stores its image); 1 = one launch "
@@ -300,6 +303,10 @@ def main():
     spd, ldir = cf.light_default()
     spec = cf.spectrum_buffer(a.bins)
     mvp = cf.default_mvp_inverse() if a.camera == "default" else cf.golden_mvp(a.camera)
+    if a.camera_mix is not None:
+        t = np.float64(a.camera_mix)
+        mvp = ((1 - t) * cf.default_mvp_inverse().astype(np.float64)
+               + t * cf.golden_mvp("near").astype(np.float64)).astype(np.float32)
 
     # VPTMCM_BENCH_DEVICE pins every rank to one ordinal (rehearsing the N > 1
     # path on a one-GPU box); the default is one GPU per local rank
@@ -708,7 +715,9 @@ def main():
             "config": {
                 "workload": f"{config_name(a.volume, n_gpus)}: {a.volume}^3 fBm volume (seed "
                             f"{volume_seed(a.volume)}), {TF_DESC.get(a.tf, a.tf + ' TF')}, R={R}, S={S}, "
-                            f"{a.bins} bins, extinction {a.extinction}, {a.camera} camera",
+                            f"{a.bins} bins, extinction {a.extinction}, "
+                            + (f"{a.camera} camera" if a.camera_mix is None else
+                               f"camera mix {a.camera_mix} (default -> near)"),
                 "resolution": R, "photon_steps_per_pass": S, "volume": a.volume,
                 "volume_layout": a.layout, "passes_per_launch": ppl,
                 "clock_settle_ms": round(settle_ms, 1), "clock_settle_passes": settle_passes,

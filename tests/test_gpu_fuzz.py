@@ -133,8 +133,13 @@ def _volume(shape, seed):
 
 
 @pytest.mark.parametrize("k", range(N_CASES))
-def test_random_configuration_bitexact(k):
+def test_random_configuration_bitexact(k, monkeypatch):
     R, shape, layout, spec, tf, ld, spd, params, mvp, vol_seed, what = _draw(k)
+    # the macro-cell null-collision skip pinned on for even cases (odd: the
+    # tuner's pick, which probes both sides on a handle's first launches)
+    if k % 2 == 0:
+        monkeypatch.setenv("VPTMCM_MAJ", "on")
+        what += " maj=on"
     print(what)
     vol = _volume(shape, vol_seed)
     with vptmcm.Renderer(R, device=0, layout=layout) as gpu:

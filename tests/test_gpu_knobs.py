@@ -17,6 +17,8 @@ pytestmark = pytest.mark.gpu
 # (variable, value): every documented knob, each variant bit of VPTMCM_MARCH_VARIANT
 KNOBS = [("VPTMCM_MARCH_VARIANT", str(b)) for b in (1, 2, 4, 8, 16, 32, 64, 128, 256)] + [
     ("VPTMCM_MARCH_VARIANT", "511"),
+    ("VPTMCM_MAJ", "on"),
+    ("VPTMCM_MAJ", "off"),
     ("VPTMCM_DARK", "0"),
     ("VPTMCM_DONE_FLAG", "0"),
     ("VPTMCM_SCHED_CACHE", "0"),

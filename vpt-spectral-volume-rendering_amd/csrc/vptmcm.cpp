@@ -269,6 +269,27 @@ struct vptmcm {
   int pack_buf = -1;
   struct vptmcm* grp_owner = nullptr;
   MarchLaunchInfo last_launch{};
+  // Whether the march skips certain null collisions' gathers (MarchParams::
+  // maj_on; same results either way) is measured, not guessed: it pays where
+  // the march waits on volume line fills (a volume filling the frame, +31 %
+  // per pass at 512^3; 1024^3, +5 %) and costs where it does not (the
+  // default camera, -7 %; a cache-resident 256^3 volume). VPTMCM_MAJ=auto
+  // (default): launches outside timed regions are timed now and then with
+  // their own events, alternately with and without the skip, and a moving
+  // average per pass picks the faster; on / off pin it.
+  struct MajTuner {
+    int mode = 2;                 // 0 off, 1 on, 2 auto
+    int choice = 0;               // the current pick (auto)
+    float ema[2] = {-1.0f, -1.0f};  // us per pass, per choice (-1: none yet)
+    uint32_t ema_n = 0;           // the launch size (passes) the averages hold
+    uint32_t launches = 0;        // launches since the last probe
+    struct Probe {
+      hipEvent_t b = nullptr, e = nullptr;
+      int choice = 0;
+      uint32_t n = 0;
+      bool busy = false;
+    } probes[4];
+  } maj_tune;
   // The camera's robust-miss region (robust_region: a double-precision matrix
   // inverse and the projected hull) for the last matrix seen: a progressive
   // renderer re-sends one camera every pass, so launches reuse it instead of
@@ -767,6 +788,13 @@ int time_close(vptmcm* h) {
   return VPTMCM_OK;
 }
 
+// The macro-cell tuner (vptmcm::maj_tune): forget the averages (the volume,
+// the TF or the march parameters changed: the trade-off moved).
+void maj_tune_reset(vptmcm* h) {
+  h->maj_tune.ema[0] = h->maj_tune.ema[1] = -1.0f;
+  h->maj_tune.launches = 0;
+}
+
 // Re-lay out the cells of the blocks that arrived since the last relayout
 // (vptmcm::vol_dirty) from the staging copy, on the handle's stream.
 int flush_relayout(vptmcm* h) {
@@ -796,6 +824,7 @@ int flush_relayout(vptmcm* h) {
     HIPCHK(h, launch_macro_minmax(h->vol_lin, h->W, h->H, h->D, h->maj_shift, h->maj_nx, h->maj_ny, m0, mn,
                                   h->maj_mm, enq(h)));
     h->maj_valid = false;
+    maj_tune_reset(h);
   }
   return guard_check(h, "relayout");
 }
@@ -817,6 +846,58 @@ int fence_pack_buffer(vptmcm* o, vptmcm* c, uint32_t b) {
   return VPTMCM_OK;
 }
 
+// Fold every finished probe into its choice's average (non-blocking).
+void maj_tune_harvest(vptmcm* h) {
+  auto& t = h->maj_tune;
+  for (auto& p : t.probes) {
+    if (!p.busy || hipEventQuery(p.e) != hipSuccess) continue;
+    p.busy = false;
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, p.b, p.e) != hipSuccess || !(ms > 0.0f)) {
+      (void)hipGetLastError();
+      continue;
+    }
+    const float us = ms * 1e3f / (float)p.n;
+    if (p.n != t.ema_n) {  // another launch size: the averages start over
+      t.ema[0] = t.ema[1] = -1.0f;
+      t.ema_n = p.n;
+    }
+    t.ema[p.choice] = t.ema[p.choice] < 0.0f ? us : 0.75f * t.ema[p.choice] + 0.25f * us;
+  }
+  (void)hipGetLastError();  // a not-ready query is not an error
+}
+
+// The skip for the next launch of n passes, and the probe events to time it
+// with (none when it is not a probe, or while the caller times a region).
+int maj_tune_pick(vptmcm* h, uint32_t n, hipEvent_t* pb, hipEvent_t* pe) {
+  auto& t = h->maj_tune;
+  *pb = *pe = nullptr;
+  if (t.mode != 2) return t.mode;
+  maj_tune_harvest(h);
+  int probe = -1;
+  if (t.ema[0] < 0.0f || t.ema[1] < 0.0f || t.ema_n != n)
+    probe = (t.ema[0] < 0.0f || t.ema_n != n) ? 0 : 1;  // what is not measured yet
+  else
+    t.choice = t.ema[1] < t.ema[0] ? 1 : 0;
+  if (probe < 0 && ++t.launches >= 16) probe = t.choice ^ 1;  // keep the other side current
+  if (probe < 0 || h->timing) return t.choice;  // (a timed region keeps its launches untouched)
+  for (auto& p : t.probes) {
+    if (p.busy) continue;
+    if (!p.b && (hipEventCreate(&p.b) != hipSuccess || hipEventCreate(&p.e) != hipSuccess)) {
+      (void)hipGetLastError();
+      return t.choice;
+    }
+    p.busy = true;
+    p.choice = probe;
+    p.n = n;
+    *pb = p.b;
+    *pe = p.e;
+    t.launches = 0;
+    return probe;
+  }
+  return t.choice;  // every probe still in flight
+}
+
 // One march launch of n <= kMaxFusedPasses passes (seeds) with matrix mvp.
 int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   if (!h->volume_ready) FAIL(h, VPTMCM_ESTATE, "render: no volume set (setVolume first)");
@@ -828,7 +909,8 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
     h->maj_valid = true;
   }
   MarchParams P = make_params(h, mvp, seeds[0]);
-  if (h->maj_ok) {
+  hipEvent_t tb = nullptr, te = nullptr;  // a tuner probe's events
+  if (h->maj_ok && h->kind == VPTMCM_RENDERER_SPECTRAL && maj_tune_pick(h, n, &tb, &te) == 1) {
     P.maj_on = 1u;
     P.maj_shift = h->maj_shift;
     P.maj_nx = h->maj_nx;
@@ -844,6 +926,10 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   int rc = time_slot(h, &eb);
   if (rc) return rc;
   if (h->timing && h->time_stop) ee = h->region.end;
+  if (tb) {  // a tuner probe (never inside a timed region)
+    eb = tb;
+    ee = te;
+  }
   const uint8_t* vol = h->layout != kLayoutLinear ? (const uint8_t*)h->vol_c8 : h->vol_lin;
   const uint32_t c = h->sched_cur, nf = sched_flag_bytes(h->n_tiles);
   TileSched T{h->sched + c * nf, h->sched + (c ^ 1u) * nf, h->sched_prev, nullptr, nullptr, nullptr,
@@ -1632,6 +1718,8 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   if (const char* v = getenv("VPTMCM_DARK")) h->dark = v[0] == '0' ? 0u : 1u;
   if (const char* v = getenv("VPTMCM_DONE_FLAG")) h->done_on = v[0] != '0';
   if (const char* v = getenv("VPTMCM_SCHED_CACHE")) h->sched_cache = v[0] != '0';
+  if (const char* v = getenv("VPTMCM_MAJ"))
+    h->maj_tune.mode = strcmp(v, "off") == 0 ? 0 : strcmp(v, "on") == 0 ? 1 : 2;
   CK(dev_alloc(&h->done_ctr, sizeof(uint32_t)));
   CK(hipMemsetAsync(h->done_ctr, 0, sizeof(uint32_t), enq(h)));
   // the flag word in fine-grained host memory; without it, synchronize waits
@@ -1724,6 +1812,10 @@ void vptmcm_destroy(vptmcm* h) {
     if (h->comp_done[k]) (void)hipEventDestroy(h->comp_done[k]);
   }
   if (h->host_scratch) (void)dev_free(h->host_scratch);
+  for (auto& pr : h->maj_tune.probes) {
+    if (pr.b) (void)hipEventDestroy(pr.b);
+    if (pr.e) (void)hipEventDestroy(pr.e);
+  }
   if (h->region.beg) (void)hipEventDestroy(h->region.beg);
   if (h->region.end) (void)hipEventDestroy(h->region.end);
   free_volume(h);
@@ -1944,6 +2036,7 @@ static int set_material_tf_one(vptmcm* h, const uint8_t* rgba) {
   }
   HIPCHK(h, hipMemcpyAsync(h->tf_rowmax, rowmax, 256, hipMemcpyHostToDevice, enq(h)));
   h->maj_valid = false;
+  maj_tune_reset(h);
   // Distinct density rows over (albedo, alpha, anisotropy): a UI TF paints one
   // material's wavelength arrays into every row of a density range
   // (MaterialTransferFunction.js:56-75), so it has few; with <= kTfRowsMax of
@@ -2000,6 +2093,7 @@ static int set_spectrum_one(vptmcm* h, const float* buf) {
     FAIL(h, VPTMCM_EINVAL, "set_spectrum: n_bins = %g exceeds MAX_N_BINS (12)", (double)buf[0]);
   h->bin_lut_ok = false;  // every error path below leaves the bin table disabled
   memcpy(h->spectrum, buf, sizeof h->spectrum);
+  maj_tune_reset(h);
   return build_bin_lut(h);
 }
 
@@ -2062,6 +2156,7 @@ static int set_params_one(vptmcm* h, const vptmcm_params* p) {
   if (memcmp(&h->params, p, sizeof *p) == 0) return VPTMCM_OK;
   if (int rc_ = flush_renders(h)) return rc_;
   h->params = *p;
+  maj_tune_reset(h);
   return VPTMCM_OK;
 }
 
