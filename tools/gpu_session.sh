@@ -148,9 +148,10 @@ for s in $STEPS; do
     for c in ${MAJ_CASES:-256:default 0:default 256:near 0:near 256:default 0:default 256:near 0:near}; do
       IFS=: read v cam vol <<< "$c"
       case $cam in mix*) camarg="--camera-mix ${cam#mix}";; *) camarg="--camera $cam";; esac
+      case $v in auto|on|off) export VPTMCM_MAJ=$v; v=0;; *) unset VPTMCM_MAJ;; esac
       VPTMCM_MARCH_VARIANT=$v timeout -k 10 300 python bench.py $camarg --volume ${vol:-512} --steps 256 --warmup 1024 --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 0 --unfused-steps 64 --near-steps 0 > $OUT/maj.json 2>> $OUT/majab.err
       rc=$?; [ $rc -ne 0 ] && { echo "majab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
-      python3 -c "import json; d=json.load(open('$OUT/maj.json')); print(json.dumps({'variant': $v, 'camera': '$cam', 'volume': ${vol:-512}, 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'unfused_us': d['unfused']['kernel_avg_us']}))" >> $OUT/majab.jsonl
+      python3 -c "import json; d=json.load(open('$OUT/maj.json')); print(json.dumps({'variant': $v, 'maj': '${VPTMCM_MAJ:-auto}', 'camera': '$cam', 'volume': ${vol:-512}, 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'unfused_us': d['unfused']['kernel_avg_us']}))" >> $OUT/majab.jsonl
     done
     echo "majab rc=0" | tee -a $OUT/status.txt; cat $OUT/majab.jsonl ;;
   counters)

@@ -282,6 +282,7 @@ struct vptmcm {
     int choice = 0;               // the current pick (auto)
     float ema[2] = {-1.0f, -1.0f};  // us per pass, per choice (-1: none yet)
     uint32_t ema_n = 0;           // the launch size (passes) the averages hold
+    float mvp[16] = {};           // the camera the averages hold (another one: start over)
     uint32_t launches = 0;        // launches since the last probe
     struct Probe {
       hipEvent_t b = nullptr, e = nullptr;
@@ -869,11 +870,15 @@ void maj_tune_harvest(vptmcm* h) {
 
 // The skip for the next launch of n passes, and the probe events to time it
 // with (none when it is not a probe, or while the caller times a region).
-int maj_tune_pick(vptmcm* h, uint32_t n, hipEvent_t* pb, hipEvent_t* pe) {
+int maj_tune_pick(vptmcm* h, const float* mvp, uint32_t n, hipEvent_t* pb, hipEvent_t* pe) {
   auto& t = h->maj_tune;
   *pb = *pe = nullptr;
   if (t.mode != 2) return t.mode;
   maj_tune_harvest(h);
+  if (memcmp(t.mvp, mvp, sizeof t.mvp) != 0) {  // the volume's screen coverage moved
+    memcpy(t.mvp, mvp, sizeof t.mvp);
+    maj_tune_reset(h);
+  }
   int probe = -1;
   if (t.ema[0] < 0.0f || t.ema[1] < 0.0f || t.ema_n != n)
     probe = (t.ema[0] < 0.0f || t.ema_n != n) ? 0 : 1;  // what is not measured yet
@@ -910,7 +915,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   }
   MarchParams P = make_params(h, mvp, seeds[0]);
   hipEvent_t tb = nullptr, te = nullptr;  // a tuner probe's events
-  if (h->maj_ok && h->kind == VPTMCM_RENDERER_SPECTRAL && maj_tune_pick(h, n, &tb, &te) == 1) {
+  if (h->maj_ok && h->kind == VPTMCM_RENDERER_SPECTRAL && maj_tune_pick(h, mvp, n, &tb, &te) == 1) {
     P.maj_on = 1u;
     P.maj_shift = h->maj_shift;
     P.maj_nx = h->maj_nx;
