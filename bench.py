@@ -464,6 +464,9 @@ def main():
     elif grouped:
         r.read_composite_all()  # the composite on devices[0] to the host, after the region
     kern_ms, n_launch = r.kernel_time()
+    # timing only inside timed regions: launches between them are the library's
+    # own (its macro-skip tuner times some of them itself, outside regions)
+    r.enable_kernel_timing(False)
     if a.no_timing:
         kern_ms, n_launch = float("nan"), len(launches)
     assert n_launch == len(launches), (n_launch, len(launches))
@@ -520,6 +523,7 @@ def main():
         r.synchronize()
         el1 = time.perf_counter() - t1
         uk_ms, un = r.kernel_time()
+        r.enable_kernel_timing(False)
         if a.no_timing:
             uk_ms, un = float("nan"), len(ul)
         assert un == len(ul)
@@ -564,6 +568,7 @@ def main():
         r.synchronize()
         el6 = time.perf_counter() - t6
         nk_ms, nn = r.kernel_time()
+        r.enable_kernel_timing(False)
         nbytes = sum(cf.algorithmic_bytes_per_launch(R, S, n) for n in nl)
         nshapes = sorted(set(nl))
         near = {"value": round(R * R * S * a.near_steps / el6 / 1e6, 3),
@@ -642,6 +647,7 @@ def main():
         r.synchronize()
         el3 = time.perf_counter() - t3
         gk_ms, gn = r.kernel_time()
+        r.enable_kernel_timing(False)
         general = {"value": round(R * R * S * a.general_steps / el3 / 1e6, 3),
                    "ms_per_step": round(el3 * 1e3 / a.general_steps, 5),
                    "steps": a.general_steps, "passes_per_launch": sorted(set(gl)),

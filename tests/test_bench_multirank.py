@@ -61,7 +61,7 @@ DRIVER = textwrap.dedent('''
         def synchronize(self): pass
         def enable_kernel_timing(self, on):
             self.t0, self.launches = time.perf_counter(), 0
-            LOG.append(["timing"])
+            LOG.append(["timing"] if on else ["timing_off"])
         def kernel_time(self):
             return (time.perf_counter() - self.t0) * 1e3 + 1e-3, self.launches
         def allreduce_radiance(self, inline=False):

@@ -280,16 +280,19 @@ struct vptmcm {
   struct MajTuner {
     int mode = 2;                 // 0 off, 1 on, 2 auto
     int choice = 0;               // the current pick (auto)
-    float ema[2] = {-1.0f, -1.0f};  // us per pass, per choice (-1: none yet)
-    uint32_t ema_n = 0;           // the launch size (passes) the averages hold
-    float mvp[16] = {};           // the camera the averages hold (another one: start over)
-    uint32_t launches = 0;        // launches since the last probe
+    // per-pass time with the skip over without it, from pairs of adjacent
+    // launches of one size (one each way, the order alternating, so the
+    // clock's ramp and drift cancel), averaged (-1: no pair measured yet)
+    float ratio = -1.0f;
+    uint32_t launches = 0;        // launches since the last pair
+    int stage = 0;                // 0 no pair in flight, 1 its first launch enqueued, 2 both
+    int first = 0;                // the first choice of the next pair
+    float mvp[16] = {};           // the camera the ratio holds (another one: start over)
     struct Probe {
       hipEvent_t b = nullptr, e = nullptr;
       int choice = 0;
       uint32_t n = 0;
-      bool busy = false;
-    } probes[4];
+    } probes[2];
   } maj_tune;
   // The camera's robust-miss region (robust_region: a double-precision matrix
   // inverse and the projected hull) for the last matrix seen: a progressive
@@ -789,11 +792,13 @@ int time_close(vptmcm* h) {
   return VPTMCM_OK;
 }
 
-// The macro-cell tuner (vptmcm::maj_tune): forget the averages (the volume,
-// the TF or the march parameters changed: the trade-off moved).
+// The macro-cell tuner (vptmcm::maj_tune): forget the ratio (the volume, the
+// TF, the camera or the march parameters changed: the trade-off moved). A pair
+// in flight is abandoned (its events are simply recorded again later).
 void maj_tune_reset(vptmcm* h) {
-  h->maj_tune.ema[0] = h->maj_tune.ema[1] = -1.0f;
+  h->maj_tune.ratio = -1.0f;
   h->maj_tune.launches = 0;
+  h->maj_tune.stage = 0;
 }
 
 // Re-lay out the cells of the blocks that arrived since the last relayout
@@ -847,29 +852,34 @@ int fence_pack_buffer(vptmcm* o, vptmcm* c, uint32_t b) {
   return VPTMCM_OK;
 }
 
-// Fold every finished probe into its choice's average (non-blocking).
+// Fold a finished pair into the ratio (non-blocking).
 void maj_tune_harvest(vptmcm* h) {
   auto& t = h->maj_tune;
-  for (auto& p : t.probes) {
-    if (!p.busy || hipEventQuery(p.e) != hipSuccess) continue;
-    p.busy = false;
-    float ms = 0.0f;
-    if (hipEventElapsedTime(&ms, p.b, p.e) != hipSuccess || !(ms > 0.0f)) {
-      (void)hipGetLastError();
-      continue;
-    }
-    const float us = ms * 1e3f / (float)p.n;
-    if (p.n != t.ema_n) {  // another launch size: the averages start over
-      t.ema[0] = t.ema[1] = -1.0f;
-      t.ema_n = p.n;
-    }
-    t.ema[p.choice] = t.ema[p.choice] < 0.0f ? us : 0.75f * t.ema[p.choice] + 0.25f * us;
+  if (t.stage != 2 || hipEventQuery(t.probes[0].e) != hipSuccess || hipEventQuery(t.probes[1].e) != hipSuccess) {
+    (void)hipGetLastError();  // a not-ready query is not an error
+    return;
   }
-  (void)hipGetLastError();  // a not-ready query is not an error
+  t.stage = 0;
+  float ms[2] = {0.0f, 0.0f};
+  for (int k = 0; k < 2; k++)
+    if (hipEventElapsedTime(&ms[k], t.probes[k].b, t.probes[k].e) != hipSuccess || !(ms[k] > 0.0f)) {
+      (void)hipGetLastError();
+      return;
+    }
+  const float on = t.probes[0].choice ? ms[0] : ms[1], off = t.probes[0].choice ? ms[1] : ms[0];
+  const float r = on / off;
+  t.ratio = t.ratio < 0.0f ? r : 0.5f * t.ratio + 0.5f * r;
+  t.choice = t.ratio < 1.0f ? 1 : 0;
+  if (const char* v = getenv("VPTMCM_MAJ_TRACE"))
+    if (v[0] == '1')
+      fprintf(stderr, "maj_tune: pair n=%u on %.3f off %.3f us/pass, ratio %.4f -> %.4f, choice %d\n",
+              t.probes[0].n, (double)(on * 1e3f / t.probes[0].n), (double)(off * 1e3f / t.probes[0].n), (double)r,
+              (double)t.ratio, t.choice);
 }
 
 // The skip for the next launch of n passes, and the probe events to time it
-// with (none when it is not a probe, or while the caller times a region).
+// with (none unless it is one of a pair; never while the caller times a
+// region, whose launches stay untouched).
 int maj_tune_pick(vptmcm* h, const float* mvp, uint32_t n, hipEvent_t* pb, hipEvent_t* pe) {
   auto& t = h->maj_tune;
   *pb = *pe = nullptr;
@@ -879,28 +889,30 @@ int maj_tune_pick(vptmcm* h, const float* mvp, uint32_t n, hipEvent_t* pb, hipEv
     memcpy(t.mvp, mvp, sizeof t.mvp);
     maj_tune_reset(h);
   }
-  int probe = -1;
-  if (t.ema[0] < 0.0f || t.ema[1] < 0.0f || t.ema_n != n)
-    probe = (t.ema[0] < 0.0f || t.ema_n != n) ? 0 : 1;  // what is not measured yet
-  else
-    t.choice = t.ema[1] < t.ema[0] ? 1 : 0;
-  if (probe < 0 && ++t.launches >= 16) probe = t.choice ^ 1;  // keep the other side current
-  if (probe < 0 || h->timing) return t.choice;  // (a timed region keeps its launches untouched)
-  for (auto& p : t.probes) {
-    if (p.busy) continue;
-    if (!p.b && (hipEventCreate(&p.b) != hipSuccess || hipEventCreate(&p.e) != hipSuccess)) {
-      (void)hipGetLastError();
-      return t.choice;
-    }
-    p.busy = true;
-    p.choice = probe;
-    p.n = n;
-    *pb = p.b;
-    *pe = p.e;
-    t.launches = 0;
-    return probe;
+  if (h->timing) return t.choice;
+  int k = -1;
+  if (t.stage == 1) {  // the pair's second launch, if it is the same size
+    if (t.probes[0].n == n) k = 1;
+    else t.stage = 0;
   }
-  return t.choice;  // every probe still in flight
+  if (k < 0 && t.stage == 0 && (t.ratio < 0.0f || ++t.launches >= 16)) k = 0;
+  if (k < 0) return t.choice;
+  auto& p = t.probes[k];
+  if (!p.b && (hipEventCreate(&p.b) != hipSuccess || hipEventCreate(&p.e) != hipSuccess)) {
+    (void)hipGetLastError();
+    t.stage = 0;
+    return t.choice;
+  }
+  p.choice = k == 0 ? t.first : t.first ^ 1;
+  p.n = n;
+  t.stage = k + 1;
+  if (k == 1) {
+    t.first ^= 1;
+    t.launches = 0;
+  }
+  *pb = p.b;
+  *pe = p.e;
+  return p.choice;
 }
 
 // One march launch of n <= kMaxFusedPasses passes (seeds) with matrix mvp.
