@@ -25,8 +25,8 @@ def main():
     for m in re.finditer(r"\.name:\s+(_ZN3vpt7k_march\S+)\n((?:\s+\..*\n)+?)\s+\.wavefront_size", s):
         name, meta = m.group(1), m.group(2)
         f = dict(re.findall(r"\.(\w+):\s+(\d+)", meta))
-        tpl = re.search(r"k_marchILj(\d)ELb(\d)ELj(\d)EE", name).groups()
-        print(f"k_march<L={tpl[0]},SPEC={tpl[1]},MODE={tpl[2]}> vgpr={f.get('vgpr_count')} "
+        tpl = re.search(r"k_marchILj(\d)ELb(\d)ELj(\d)ELb(\d)EE", name).groups()
+        print(f"k_march<L={tpl[0]},SPEC={tpl[1]},MODE={tpl[2]},MAJ={tpl[3]}> vgpr={f.get('vgpr_count')} "
               f"sgpr={f.get('sgpr_count')} sgpr_spill={f.get('sgpr_spill_count')} "
               f"vgpr_spill={f.get('vgpr_spill_count')}")
 

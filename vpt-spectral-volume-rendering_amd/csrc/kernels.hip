@@ -520,7 +520,7 @@ __device__ __forceinline__ bool robust_pixel(const MarchParams& P, float sx, flo
 // 5: MODE 2's geometry and light with any bin layout and a TF of more than
 // kTfRowsMax distinct rows (u16 LDS TF; anisotropy from the row table or the
 // tf_b4 gather).
-template <uint32_t L, bool SPEC, uint32_t MODE>
+template <uint32_t L, bool SPEC, uint32_t MODE, bool MAJ>
 __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const MarchParams P,
                                                        const TileSched T, float* __restrict__ ph,
                                                        const uint8_t* __restrict__ vol,
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
   __shared__ float s_brow[256];
   __shared__ uint32_t s_rowmap[256];  // P.tf_dedup: density row -> first texel of its distinct row
   __shared__ uint32_t s_binlut[LUTB ? kBinLutCells + kBinLutCells / 4 : 1];  // MODE 6 / 7
-  __shared__ uint4 s_maj4[SPEC ? kMajBytes / 16 : 1];  // macro-cell alpha codes (P.maj_on)
+  __shared__ uint4 s_maj4[MAJ ? kMajBytes / 16 : 1];  // macro-cell alpha codes (P.maj_on)
 
   __shared__ uint32_t s_red[64];
   __shared__ uint32_t s_tile[16];
@@ -669,7 +669,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
     for (uint32_t k = 0; k < 2u; k++)
       if (threadIdx.x + k * kMarchBlock < kLutWords) s_binlut[threadIdx.x + k * kMarchBlock] = binlut_v[k];
   }
-  if constexpr (SPEC) {  // the macro-cell table (<= 20 KB: at most two 16-B words per thread)
+  if constexpr (MAJ) {  // the macro-cell table (<= 20 KB: at most two 16-B words per thread)
     if (P.maj_on != 0u)
       for (uint32_t k = threadIdx.x; k < P.maj_bytes / 16u; k += kMarchBlock)
         s_maj4[k] = reinterpret_cast<const uint4*>(maj)[k];
@@ -931,7 +931,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march(const PassSeeds PS, const
       // decision below is masked for it, the other lanes' values are unchanged
       const VolCell vcell = vol_cell(P, p.pos);
       bool skip = false;
-      if (P.maj_on != 0u)
+      if constexpr (MAJ)
         skip = !oob && wheel >= maj_threshold(P, vcell, reinterpret_cast<const uint8_t*>(s_maj4));
       VolTap vt;
       vt.fx = vt.fy = vt.fz = 0.0f;
@@ -1690,22 +1690,30 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   if (info) *info = MarchLaunchInfo{mode, tpl, spec ? 1u : 0u, PS.n};
   // hipExtLaunchKernelGGL stamps the events from the dispatch packet itself
   // (no extra barrier/marker packets between back-to-back launches)
-#define VPT_LAUNCH(LAY, SP, MO)                                                                \
-  hipExtLaunchKernelGGL((k_march<LAY, SP, MO>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
+#define VPT_LAUNCH(LAY, SP, MO, MJ)                                                                \
+  hipExtLaunchKernelGGL((k_march<LAY, SP, MO, MJ>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
                         PS, Q, T, ph, vol, tf_lds, tf_b4, tf_brow, light, rgba, rgb32, rowmap, bin_lut, maj)
+  // the macro-cell bound is a template argument: without it the step loop has
+  // no skip test and no 20 KB LDS table (measured: a runtime-off test cost the
+  // default camera 8 %)
+#define VPT_LAUNCH_S(LAY, MO)                                      \
+  do {                                                             \
+    if (Q.maj_on) VPT_LAUNCH(LAY, true, MO, true);                 \
+    else VPT_LAUNCH(LAY, true, MO, false);                         \
+  } while (0)
 #define VPT_LAUNCH_NB(LAY)                 \
   do {                                     \
     switch (spec ? mode : 8u + mode) {     \
-      case 2u: VPT_LAUNCH(LAY, true, 2u); break; \
-      case 3u: VPT_LAUNCH(LAY, true, 3u); break; \
-      case 4u: VPT_LAUNCH(LAY, true, 4u); break; \
-      case 5u: VPT_LAUNCH(LAY, true, 5u); break; \
-      case 6u: VPT_LAUNCH(LAY, true, 6u); break; \
-      case 7u: VPT_LAUNCH(LAY, true, 7u); break; \
-      case 1u: VPT_LAUNCH(LAY, true, 1u); break; \
-      case 0u: VPT_LAUNCH(LAY, true, 0u); break; \
-      case 9u: VPT_LAUNCH(LAY, false, 1u); break; \
-      default: VPT_LAUNCH(LAY, false, 0u); break; \
+      case 2u: VPT_LAUNCH_S(LAY, 2u); break; \
+      case 3u: VPT_LAUNCH_S(LAY, 3u); break; \
+      case 4u: VPT_LAUNCH_S(LAY, 4u); break; \
+      case 5u: VPT_LAUNCH_S(LAY, 5u); break; \
+      case 6u: VPT_LAUNCH_S(LAY, 6u); break; \
+      case 7u: VPT_LAUNCH_S(LAY, 7u); break; \
+      case 1u: VPT_LAUNCH_S(LAY, 1u); break; \
+      case 0u: VPT_LAUNCH_S(LAY, 0u); break; \
+      case 9u: VPT_LAUNCH(LAY, false, 1u, false); break; \
+      default: VPT_LAUNCH(LAY, false, 0u, false); break; \
     }                                      \
   } while (0)
   switch (tpl) {
@@ -1718,6 +1726,7 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
     default: VPT_LAUNCH_NB(kTplLinear); break;
   }
 #undef VPT_LAUNCH_NB
+#undef VPT_LAUNCH_S
 #undef VPT_LAUNCH
   return hipGetLastError();
 }
