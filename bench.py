@@ -224,10 +224,10 @@ def stdout_to_stderr(fn):
         os.close(saved)
 
 
-def pmc_entry(a, R: int, S: int, shapes: list, camera: str):
+def pmc_entry(a, R: int, S: int, shapes: list, camera: str, macro: bool = False):
     """The PMC passes' entry (profiles/pmc_traffic.json, tools/pmc_report.py) of
     exactly this launch shape — R, S, layout, volume, passes per launch,
-    camera — with the benchmark TF and bins, or None."""
+    camera, macro-cell bound on or off — with the benchmark TF and bins, or None."""
     tp = Path(a.traffic_json)
     if not tp.exists() or len(shapes) != 1 or a.tf != "spectral" or a.bins != "12":
         return None
@@ -238,7 +238,7 @@ def pmc_entry(a, R: int, S: int, shapes: list, camera: str):
     for e in t.get("entries", [t]):
         if (e.get("resolution") == R and e.get("steps") == S and e.get("layout") == a.layout
                 and e.get("volume", 512) == a.volume and e.get("passes_per_launch", 1) == shapes[0]
-                and e.get("camera", "default") == camera):
+                and e.get("camera", "default") == camera and e.get("macro_skip", False) == macro):
             e = dict(e)
             e["_source"] = f"{tp.relative_to(REPO) if tp.is_relative_to(REPO) else tp}"
             e["_gather_peak"] = t.get("gather_peak")
@@ -467,6 +467,7 @@ def main():
     # timing only inside timed regions: launches between them are the library's
     # own (its macro-skip tuner times some of them itself, outside regions)
     r.enable_kernel_timing(False)
+    macro = bool(r.last_launch().get("macro", False))  # the macro-cell bound in the timed launches
     if a.no_timing:
         kern_ms, n_launch = float("nan"), len(launches)
     assert n_launch == len(launches), (n_launch, len(launches))
@@ -569,12 +570,14 @@ def main():
         el6 = time.perf_counter() - t6
         nk_ms, nn = r.kernel_time()
         r.enable_kernel_timing(False)
+        nmacro = bool(r.last_launch().get("macro", False))
         nbytes = sum(cf.algorithmic_bytes_per_launch(R, S, n) for n in nl)
         nshapes = sorted(set(nl))
         near = {"value": round(R * R * S * a.near_steps / el6 / 1e6, 3),
                 "ms_per_step": round(el6 * 1e3 / a.near_steps, 5), "steps": a.near_steps,
                 "passes_per_launch": nshapes[0] if len(nshapes) == 1 else nshapes,
                 "kernel_us_per_pass": None, "roofline": None, "gather_roofline": None,
+                "macro_skip": nmacro,
                 "workload": "same volume, TF, bins and launch shape as the main line with the golden "
                             "'near' camera: the volume fills the frame, every photon-step gathers"}
         if not a.no_timing:
@@ -583,7 +586,7 @@ def main():
             near["roofline"] = {"bound": "hbm", "achieved": round(nach, 1), "peak": HBM_PEAK_GBPS,
                                 "unit": "GB/s", "frac": round(nach / HBM_PEAK_GBPS, 4),
                                 "algorithmic_bytes_per_launch": nbytes // len(nl), "traffic": None}
-            ne = pmc_entry(a, R, S, nshapes, "near")
+            ne = pmc_entry(a, R, S, nshapes, "near", nmacro)
             if ne is not None:
                 launch_s = nk_ms * 1e-3 / nn
                 fills = ne["read_requests"]["128B"] + ne["read_requests"]["64B"] + ne["read_requests"]["32B"]
@@ -613,7 +616,7 @@ def main():
     # PMC-derived memory-side bytes per launch (profiles/): attached only when a
     # profile of this exact launch shape (R, S, layout, volume, passes) exists.
     traffic, traffic_src, issue = None, None, None
-    e = pmc_entry(a, R, S, shapes, a.camera)
+    e = pmc_entry(a, R, S, shapes, a.camera, macro)
     if e is not None:
         traffic = e.get("hbm_bytes_per_launch")
         traffic_src = e["_source"]
@@ -730,6 +733,9 @@ def main():
                 "parallelism": parallelism,
                 "composite_transport": comp_kind,
                 "devices": devs if grouped else None,
+                # the macro-cell alpha bound (VPTMCM_MAJ, default auto: the library's
+                # tuner measures it on and off and keeps the faster) in the timed launches
+                "macro_skip": macro,
             },
             "hbm_gbps_algorithmic": round(achieved, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,

@@ -370,8 +370,9 @@ int vptmcm_debug_verify(vptmcm* h, int fn, uint32_t lo, uint64_t count, uint64_t
  * info[0] the march specialisation (MODE 0-7 of the spectral kernel, see
  * DESIGN.md; RGB renderer: 1 with the fast geometry, else 0), info[1] the
  * volume layout template (0 linear, 1 corner8, 2 corner8 with 64-bit offsets,
- * 3 brick8, 4 brick8 with 64-bit offsets), info[2] 1 for the speculative step
- * loop, info[3] the passes fused into it; *launches (may be NULL) counts every
+ * 3 brick8, 4 brick8 with 64-bit offsets), info[2] bit 0 set for the
+ * speculative step loop, bit 1 for the macro-cell alpha bound (VPTMCM_MAJ),
+ * info[3] the passes fused into it; *launches (may be NULL) counts every
  * march launch since create. */
 int vptmcm_debug_last_launch(vptmcm* h, uint32_t info[4], uint64_t* launches);
 

@@ -55,7 +55,7 @@ def _run(layout, tf, spec, with_oracle=False, devices=None):
     gpu.synchronize()
     ms, n = gpu.kernel_time()
     assert n >= 2 and ms > 0
-    got = (gpu.read_photons(), gpu.read_rgb(), gpu.read_rgba16f())
+    got = (gpu.read_photons(), gpu.read_rgb(), gpu.read_rgba16f(), gpu.last_launch()["macro"])
     gpu.close()
     if with_oracle:
         cpu.reset(m1, seeds[0], nthreads=16)
@@ -80,6 +80,8 @@ def test_every_knob_leaves_the_bits(layout, tfname, spec, monkeypatch):
         got = _run(layout, tf, spec)
         monkeypatch.delenv(var)
         what = f"{var}={val}"
+        if var == "VPTMCM_MAJ":  # the last launch ran k_march<..., MAJ> as asked
+            assert got[3] == (val == "on"), what
         assert_photons_equal(got[0], base[0], what)
         assert_rgb32_equal(got[1], base[1], what)
         assert_rgba_equal(got[2], base[2], what)

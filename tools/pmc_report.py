@@ -20,6 +20,7 @@ with one trimmed <pass>.csv per counter pass)
 """
 import csv
 import json
+import re
 import sys
 from pathlib import Path
 
@@ -84,9 +85,12 @@ def main():
         cycles = sq["GRBM_GUI_ACTIVE"] / 8
         valu, salu = sq["SQ_INSTS_VALU"], sq["SQ_INSTS_SALU"]
         photon_steps = R * R * S * ppl
+        # k_march<L, SPEC, MODE, MAJ>: the macro-cell bound is the 4th template argument
+        mj = re.search(r"k_marchILj\d+ELb\dELj\d+ELb(\d)EE", kname)
         out["entries"].append({
             "kernel": "k_march", "kernel_name": kname, "resolution": R, "steps": S, "layout": layout,
             "volume": volume, "passes_per_launch": ppl, "camera": camera,
+            "macro_skip": bool(mj and mj.group(1) == "1"),
             "kernel_us_under_pmc": round(qdur * 1e6, 2),
             "read_requests": {"32B": q["TCC_EA0_RDREQ_32B_sum"], "64B": q["TCC_EA0_RDREQ_64B_sum"],
                               "128B": q["TCC_EA0_RDREQ_128B_sum"]},
@@ -107,7 +111,7 @@ def main():
             out.setdefault(k, v)
     if dst.exists():  # keep the other layouts' / shapes' entries
         key = lambda e: (e["resolution"], e["steps"], e["layout"], e["volume"], e["passes_per_launch"],
-                         e.get("camera", "default"))
+                         e.get("camera", "default"), e.get("macro_skip", False))
         mine = {key(e) for e in out["entries"]}
         old = json.loads(dst.read_text()).get("entries", [])
         out["entries"] = [e for e in old if key(e) not in mine] + out["entries"]

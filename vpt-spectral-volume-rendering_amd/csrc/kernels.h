@@ -83,8 +83,8 @@ inline uint32_t sched_slot_words(uint32_t n_tiles) {  // TileSched::prev: 16 wav
 
 hipError_t launch_reset(const MarchParams& P, float* ph, hipStream_t s);
 // What one march launch ran (vptmcm_debug_last_launch): the MODE
-// specialisation, the layout template (kTpl*), the step loop (1 speculative,
-// 0 plain) and the number of fused passes.
+// specialisation, the layout template (kTpl*), the step loop (bit 0: 1
+// speculative, 0 plain; bit 1: the macro-cell bound) and the number of fused passes.
 struct MarchLaunchInfo {
   uint32_t mode, tpl, spec, passes;
 };

@@ -1687,7 +1687,7 @@ hipError_t launch_march(uint32_t layout, uint32_t variant, const MarchParams& P,
   else if (layout == kLayoutColumn4) tpl = P.vol32 ? kTplColumn4 : kTplColumn4Wide;
   else if (layout == kLayoutCorner8) tpl = P.vol32 ? kTplCorner8 : kTplCorner8Wide;
   else tpl = kTplLinear;
-  if (info) *info = MarchLaunchInfo{mode, tpl, spec ? 1u : 0u, PS.n};
+  if (info) *info = MarchLaunchInfo{mode, tpl, (spec ? 1u : 0u) | (Q.maj_on ? 2u : 0u), PS.n};
   // hipExtLaunchKernelGGL stamps the events from the dispatch packet itself
   // (no extra barrier/marker packets between back-to-back launches)
 #define VPT_LAUNCH(LAY, SP, MO, MJ)                                                                \

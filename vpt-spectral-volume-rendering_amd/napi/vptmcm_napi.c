@@ -529,7 +529,7 @@ static napi_value js_comm_barrier(napi_env env, napi_callback_info info) {
     return check(env, h, vptmcm_comm_barrier(h));
 }
 
-/* lastLaunch(h) -> { mode, tpl, spec, passes, launches } (vptmcm_debug_last_launch) */
+/* lastLaunch(h) -> { mode, tpl, spec, passes, macro, launches } (vptmcm_debug_last_launch) */
 static napi_value js_last_launch(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     if (get_args(env, info, 1, argv)) return NULL;
@@ -539,11 +539,12 @@ static napi_value js_last_launch(napi_env env, napi_callback_info info) {
     uint64_t n = 0;
     int rc = vptmcm_debug_last_launch(h, v, &n);
     if (rc) return throw_code(env, rc, vptmcm_last_error(h));
-    static const char* names[4] = {"mode", "tpl", "spec", "passes"};
+    static const char* names[5] = {"mode", "tpl", "spec", "passes", "macro"};
+    const uint32_t w[5] = {v[0], v[1], v[2] & 1u, v[3], (v[2] >> 1) & 1u};
     napi_value o, x;
     napi_create_object(env, &o);
-    for (int k = 0; k < 4; k++) {
-        napi_create_uint32(env, v[k], &x);
+    for (int k = 0; k < 5; k++) {
+        napi_create_uint32(env, w[k], &x);
         napi_set_named_property(env, o, names[k], x);
     }
     napi_create_double(env, (double)n, &x);

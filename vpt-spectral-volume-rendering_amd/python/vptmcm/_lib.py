@@ -460,7 +460,8 @@ class Renderer:
         info = np.zeros(4, np.uint32)
         n = C.c_uint64()
         self._ck(self.L.vptmcm_debug_last_launch(self.h, _u32p(info), C.byref(n)))
-        return {"mode": int(info[0]), "tpl": int(info[1]), "spec": bool(info[2]),
+        return {"mode": int(info[0]), "tpl": int(info[1]), "spec": bool(info[2] & 1),
+                "macro": bool(info[2] & 2),
                 "passes": int(info[3]), "launches": n.value}
 
     def debug_schedule(self) -> np.ndarray:
