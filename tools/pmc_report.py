@@ -85,12 +85,13 @@ def main():
         cycles = sq["GRBM_GUI_ACTIVE"] / 8
         valu, salu = sq["SQ_INSTS_VALU"], sq["SQ_INSTS_SALU"]
         photon_steps = R * R * S * ppl
-        # k_march<L, SPEC, MODE, MAJ>: the macro-cell bound is the 4th template argument
-        mj = re.search(r"k_marchILj\d+ELb\dELj\d+ELb(\d)EE", kname)
+        # k_march<L, SPEC, MODE, MAJ>: the macro-cell bound is the 4th template
+        # argument (rocprofv3 writes the demangled name)
+        mj = re.search(r"k_march<\d+u, (?:true|false), \d+u, (true|false)>", kname)
         out["entries"].append({
             "kernel": "k_march", "kernel_name": kname, "resolution": R, "steps": S, "layout": layout,
             "volume": volume, "passes_per_launch": ppl, "camera": camera,
-            "macro_skip": bool(mj and mj.group(1) == "1"),
+            "macro_skip": bool(mj and mj.group(1) == "true"),
             "kernel_us_under_pmc": round(qdur * 1e6, 2),
             "read_requests": {"32B": q["TCC_EA0_RDREQ_32B_sum"], "64B": q["TCC_EA0_RDREQ_64B_sum"],
                               "128B": q["TCC_EA0_RDREQ_128B_sum"]},

@@ -275,8 +275,9 @@ struct vptmcm {
   // per pass at 512^3; 1024^3, +5 %) and costs where it does not (the
   // default camera, -7 %; a cache-resident 256^3 volume). VPTMCM_MAJ=auto
   // (default): launches outside timed regions are timed now and then with
-  // their own events, alternately with and without the skip, and a moving
-  // average per pass picks the faster; on / off pin it.
+  // their own events, in pairs of adjacent launches (one with the skip, one
+  // without), and the averaged ratio picks the faster; on / off pin it. Off
+  // runs k_march<..., MAJ = false>, the step loop without the test.
   struct MajTuner {
     int mode = 2;                 // 0 off, 1 on, 2 auto
     int choice = 0;               // the current pick (auto)
