@@ -368,7 +368,8 @@ def main():
     n_unfused = a.unfused_steps if single else 0
     n_api = a.api_steps if single else 0
     n_pp = a.per_pass_steps if not single else 0
-    seeds = cf.seed_stream(a.warmup + a.steps + n_unfused + n_api + n_pp + 1, start=0, rank=rank)
+    n_uwarm = 32 if n_unfused > 0 else 0  # untimed one-pass launches ahead of the unfused region
+    seeds = cf.seed_stream(a.warmup + a.steps + n_unfused + n_api + n_pp + n_uwarm + 1, start=0, rank=rank)
     F = max(1, min(a.fuse, 32))
     every = max(1, a.allreduce_every)
 
@@ -517,6 +518,9 @@ def main():
 
     unfused = None
     if n_unfused > 0:
+        # one-pass launches before the region, as a display loop runs them (the
+        # library's macro-skip tuner measures this launch size here, untimed)
+        passes(1 + a.warmup + a.steps + n_unfused + n_api + n_pp, n_uwarm, F=1)
         r.synchronize()
         r.enable_kernel_timing(not a.no_timing)  # restart the launch timings
         t1 = time.perf_counter()

@@ -280,14 +280,21 @@ struct vptmcm {
   // runs k_march<..., MAJ = false>, the step loop without the test.
   struct MajTuner {
     int mode = 2;                 // 0 off, 1 on, 2 auto
-    int choice = 0;               // the current pick (auto)
-    // per-pass time with the skip over without it, from pairs of adjacent
-    // launches of one size (one each way, the order alternating, so the
-    // clock's ramp and drift cancel), averaged (-1: no pair measured yet)
-    float ratio = -1.0f;
-    uint32_t launches = 0;        // launches since the last pair
+    int choice = 0;               // the last pick measured, for sizes with none yet
+    // per launch size n (passes): the time with the skip over without it,
+    // from pairs of adjacent launches of that size, one each way. A pair's
+    // two launches do not run alike (one-pass launches: the first of a pair
+    // runs ~7 % slower whichever it is), so a pair counts only with the next
+    // pair of the other order: the geometric mean of their ratios, averaged
+    // over such pairs of pairs (-1: none measured yet). Sizes differ: at the
+    // default camera a 32-pass launch is issue-bound (the skip costs 6 %)
+    // while a one-pass launch ends with its slowest in-volume waves (the skip
+    // saves 1.6 %).
+    float ratio[kMaxFusedPasses + 1];
+    float half[kMaxFusedPasses + 1];         // a pair's ratio awaiting the other order (-1: none)
+    uint32_t launches[kMaxFusedPasses + 1];  // launches of size n since its last pair
+    uint8_t first[kMaxFusedPasses + 1];      // the first choice of size n's next pair
     int stage = 0;                // 0 no pair in flight, 1 its first launch enqueued, 2 both
-    int first = 0;                // the first choice of the next pair
     float mvp[16] = {};           // the camera the ratio holds (another one: start over)
     struct Probe {
       hipEvent_t b = nullptr, e = nullptr;
@@ -797,8 +804,11 @@ int time_close(vptmcm* h) {
 // TF, the camera or the march parameters changed: the trade-off moved). A pair
 // in flight is abandoned (its events are simply recorded again later).
 void maj_tune_reset(vptmcm* h) {
-  h->maj_tune.ratio = -1.0f;
-  h->maj_tune.launches = 0;
+  for (uint32_t n = 0; n <= kMaxFusedPasses; n++) {
+    h->maj_tune.ratio[n] = h->maj_tune.half[n] = -1.0f;
+    h->maj_tune.launches[n] = 0;
+    h->maj_tune.first[n] = 0;
+  }
   h->maj_tune.stage = 0;
 }
 
@@ -869,13 +879,21 @@ void maj_tune_harvest(vptmcm* h) {
     }
   const float on = t.probes[0].choice ? ms[0] : ms[1], off = t.probes[0].choice ? ms[1] : ms[0];
   const float r = on / off;
-  t.ratio = t.ratio < 0.0f ? r : 0.5f * t.ratio + 0.5f * r;
-  t.choice = t.ratio < 1.0f ? 1 : 0;
+  const uint32_t n = t.probes[0].n;
+  float& q = t.ratio[n];
+  if (t.half[n] < 0.0f) {  // the first of a pair of pairs (the next one runs the other order)
+    t.half[n] = r;
+    return;
+  }
+  const float rr = sqrtf(t.half[n] * r);
+  t.half[n] = -1.0f;
+  q = q < 0.0f ? rr : 0.5f * q + 0.5f * rr;
+  t.choice = q < 1.0f ? 1 : 0;
   if (const char* v = getenv("VPTMCM_MAJ_TRACE"))
     if (v[0] == '1')
-      fprintf(stderr, "maj_tune: pair n=%u on %.3f off %.3f us/pass, ratio %.4f -> %.4f, choice %d\n",
-              t.probes[0].n, (double)(on * 1e3f / t.probes[0].n), (double)(off * 1e3f / t.probes[0].n), (double)r,
-              (double)t.ratio, t.choice);
+      fprintf(stderr, "maj_tune: pairs n=%u on %.3f off %.3f us/pass, ratio %.4f (both orders %.4f) -> %.4f, "
+              "choice %d\n", n, (double)(on * 1e3f / n), (double)(off * 1e3f / n), (double)r, (double)rr,
+              (double)q, t.choice);
 }
 
 // The skip for the next launch of n passes, and the probe events to time it
@@ -890,26 +908,27 @@ int maj_tune_pick(vptmcm* h, const float* mvp, uint32_t n, hipEvent_t* pb, hipEv
     memcpy(t.mvp, mvp, sizeof t.mvp);
     maj_tune_reset(h);
   }
-  if (h->timing) return t.choice;
+  const int pick = t.ratio[n] < 0.0f ? t.choice : t.ratio[n] < 1.0f ? 1 : 0;
+  if (h->timing) return pick;
   int k = -1;
   if (t.stage == 1) {  // the pair's second launch, if it is the same size
     if (t.probes[0].n == n) k = 1;
     else t.stage = 0;
   }
-  if (k < 0 && t.stage == 0 && (t.ratio < 0.0f || ++t.launches >= 16)) k = 0;
-  if (k < 0) return t.choice;
+  if (k < 0 && t.stage == 0 && (t.ratio[n] < 0.0f || ++t.launches[n] >= 16)) k = 0;
+  if (k < 0) return pick;
   auto& p = t.probes[k];
   if (!p.b && (hipEventCreate(&p.b) != hipSuccess || hipEventCreate(&p.e) != hipSuccess)) {
     (void)hipGetLastError();
     t.stage = 0;
-    return t.choice;
+    return pick;
   }
-  p.choice = k == 0 ? t.first : t.first ^ 1;
+  p.choice = k == 0 ? t.first[n] : t.first[n] ^ 1;
   p.n = n;
   t.stage = k + 1;
   if (k == 1) {
-    t.first ^= 1;
-    t.launches = 0;
+    t.first[n] ^= 1;
+    t.launches[n] = 0;
   }
   *pb = p.b;
   *pe = p.e;
@@ -1738,6 +1757,7 @@ int vptmcm_create(const vptmcm_config* cfg, vptmcm** out) {
   if (const char* v = getenv("VPTMCM_SCHED_CACHE")) h->sched_cache = v[0] != '0';
   if (const char* v = getenv("VPTMCM_MAJ"))
     h->maj_tune.mode = strcmp(v, "off") == 0 ? 0 : strcmp(v, "on") == 0 ? 1 : 2;
+  maj_tune_reset(h);  // no size measured yet
   CK(dev_alloc(&h->done_ctr, sizeof(uint32_t)));
   CK(hipMemsetAsync(h->done_ctr, 0, sizeof(uint32_t), enq(h)));
   // the flag word in fine-grained host memory; without it, synchronize waits
