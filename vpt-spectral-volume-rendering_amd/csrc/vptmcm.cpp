@@ -273,11 +273,15 @@ struct vptmcm {
   // maj_on; same results either way) is measured, not guessed: it pays where
   // the march waits on volume line fills (a volume filling the frame, +31 %
   // per pass at 512^3; 1024^3, +5 %) and costs where it does not (the
-  // default camera, -7 %; a cache-resident 256^3 volume). VPTMCM_MAJ=auto
+  // default camera, -6 %; a cache-resident 256^3 volume). VPTMCM_MAJ=auto
   // (default): launches outside timed regions are timed now and then with
   // their own events, in pairs of adjacent launches (one with the skip, one
   // without), and the averaged ratio picks the faster; on / off pin it. Off
-  // runs k_march<..., MAJ = false>, the step loop without the test.
+  // runs k_march<..., MAJ = false>, the step loop without the test. Pairs
+  // are read back without blocking, up to kPairs of them in flight, so a
+  // caller that enqueues many launches ahead of the GPU still gets its
+  // measurements.
+  static constexpr int kPairs = 8;
   struct MajTuner {
     int mode = 2;                 // 0 off, 1 on, 2 auto
     int choice = 0;               // the last pick measured, for sizes with none yet
@@ -294,13 +298,16 @@ struct vptmcm {
     float half[kMaxFusedPasses + 1];         // a pair's ratio awaiting the other order (-1: none)
     uint32_t launches[kMaxFusedPasses + 1];  // launches of size n since its last pair
     uint8_t first[kMaxFusedPasses + 1];      // the first choice of size n's next pair
-    int stage = 0;                // 0 no pair in flight, 1 its first launch enqueued, 2 both
+    uint8_t half_first[kMaxFusedPasses + 1]; // the first choice of the pair held in half
     float mvp[16] = {};           // the camera the ratio holds (another one: start over)
-    struct Probe {
-      hipEvent_t b = nullptr, e = nullptr;
-      int choice = 0;
-      uint32_t n = 0;
-    } probes[2];
+    uint32_t epoch = 0;           // bumped by a reset: pairs of an older epoch are dropped
+    struct Pair {
+      hipEvent_t b[2] = {nullptr, nullptr}, e[2] = {nullptr, nullptr};
+      int first = 0;              // the choice of the pair's first launch (the second: the other)
+      uint32_t n = 0, epoch = 0;
+      int stage = 0;              // launches enqueued (2: complete, waiting to be read)
+    } pairs[kPairs];              // a ring: head the oldest, count in flight
+    int head = 0, count = 0;
   } maj_tune;
   // The camera's robust-miss region (robust_region: a double-precision matrix
   // inverse and the projected hull) for the last matrix seen: a progressive
@@ -809,7 +816,7 @@ void maj_tune_reset(vptmcm* h) {
     h->maj_tune.launches[n] = 0;
     h->maj_tune.first[n] = 0;
   }
-  h->maj_tune.stage = 0;
+  h->maj_tune.epoch++;
 }
 
 // Re-lay out the cells of the blocks that arrived since the last relayout
@@ -863,37 +870,47 @@ int fence_pack_buffer(vptmcm* o, vptmcm* c, uint32_t b) {
   return VPTMCM_OK;
 }
 
-// Fold a finished pair into the ratio (non-blocking).
+// Fold the finished pairs into the ratios, oldest first (non-blocking: stops
+// at the first pair the GPU has not finished).
 void maj_tune_harvest(vptmcm* h) {
   auto& t = h->maj_tune;
-  if (t.stage != 2 || hipEventQuery(t.probes[0].e) != hipSuccess || hipEventQuery(t.probes[1].e) != hipSuccess) {
-    (void)hipGetLastError();  // a not-ready query is not an error
-    return;
-  }
-  t.stage = 0;
-  float ms[2] = {0.0f, 0.0f};
-  for (int k = 0; k < 2; k++)
-    if (hipEventElapsedTime(&ms[k], t.probes[k].b, t.probes[k].e) != hipSuccess || !(ms[k] > 0.0f)) {
-      (void)hipGetLastError();
+  while (t.count > 0) {
+    auto& pr = t.pairs[t.head];
+    if (pr.stage == 1) return;  // the open pair: its second launch is not enqueued yet
+    if (pr.stage == 2 && (hipEventQuery(pr.e[0]) != hipSuccess || hipEventQuery(pr.e[1]) != hipSuccess)) {
+      (void)hipGetLastError();  // a not-ready query is not an error
       return;
     }
-  const float on = t.probes[0].choice ? ms[0] : ms[1], off = t.probes[0].choice ? ms[1] : ms[0];
-  const float r = on / off;
-  const uint32_t n = t.probes[0].n;
-  float& q = t.ratio[n];
-  if (t.half[n] < 0.0f) {  // the first of a pair of pairs (the next one runs the other order)
-    t.half[n] = r;
-    return;
+    t.head = (t.head + 1) % vptmcm::kPairs;
+    t.count--;
+    if (pr.stage != 2 || pr.epoch != t.epoch) continue;  // abandoned, or from before a reset
+    float ms[2] = {0.0f, 0.0f};
+    bool ok = true;
+    for (int k = 0; k < 2; k++)
+      ok = ok && hipEventElapsedTime(&ms[k], pr.b[k], pr.e[k]) == hipSuccess && ms[k] > 0.0f;
+    if (!ok) {
+      (void)hipGetLastError();
+      continue;
+    }
+    const float on = pr.first ? ms[0] : ms[1], off = pr.first ? ms[1] : ms[0];
+    const float r = on / off;
+    const uint32_t n = pr.n;
+    if (t.half[n] < 0.0f || t.half_first[n] == pr.first) {  // wait for a pair of the other order
+      t.half[n] = r;
+      t.half_first[n] = (uint8_t)pr.first;
+      continue;
+    }
+    const float rr = sqrtf(t.half[n] * r);
+    t.half[n] = -1.0f;
+    float& q = t.ratio[n];
+    q = q < 0.0f ? rr : 0.5f * q + 0.5f * rr;
+    t.choice = q < 1.0f ? 1 : 0;
+    if (const char* v = getenv("VPTMCM_MAJ_TRACE"))
+      if (v[0] == '1')
+        fprintf(stderr, "maj_tune: pairs n=%u on %.3f off %.3f us/pass, ratio %.4f (both orders %.4f) -> %.4f, "
+                "choice %d\n", n, (double)(on * 1e3f / n), (double)(off * 1e3f / n), (double)r, (double)rr,
+                (double)q, t.choice);
   }
-  const float rr = sqrtf(t.half[n] * r);
-  t.half[n] = -1.0f;
-  q = q < 0.0f ? rr : 0.5f * q + 0.5f * rr;
-  t.choice = q < 1.0f ? 1 : 0;
-  if (const char* v = getenv("VPTMCM_MAJ_TRACE"))
-    if (v[0] == '1')
-      fprintf(stderr, "maj_tune: pairs n=%u on %.3f off %.3f us/pass, ratio %.4f (both orders %.4f) -> %.4f, "
-              "choice %d\n", n, (double)(on * 1e3f / n), (double)(off * 1e3f / n), (double)r, (double)rr,
-              (double)q, t.choice);
 }
 
 // The skip for the next launch of n passes, and the probe events to time it
@@ -909,30 +926,36 @@ int maj_tune_pick(vptmcm* h, const float* mvp, uint32_t n, hipEvent_t* pb, hipEv
     maj_tune_reset(h);
   }
   const int pick = t.ratio[n] < 0.0f ? t.choice : t.ratio[n] < 1.0f ? 1 : 0;
+  auto* open = t.count > 0 ? &t.pairs[(t.head + t.count - 1) % vptmcm::kPairs] : nullptr;
+  if (open && open->stage != 1) open = nullptr;
+  if (open && (h->timing || open->n != n || open->epoch != t.epoch)) {
+    open->stage = 0;  // its second launch would not be adjacent or alike: abandoned
+    open = nullptr;
+  }
   if (h->timing) return pick;
-  int k = -1;
-  if (t.stage == 1) {  // the pair's second launch, if it is the same size
-    if (t.probes[0].n == n) k = 1;
-    else t.stage = 0;
+  if (open) {  // the pair's second launch, the other way
+    open->stage = 2;
+    *pb = open->b[1];
+    *pe = open->e[1];
+    return open->first ^ 1;
   }
-  if (k < 0 && t.stage == 0 && (t.ratio[n] < 0.0f || ++t.launches[n] >= 16)) k = 0;
-  if (k < 0) return pick;
-  auto& p = t.probes[k];
-  if (!p.b && (hipEventCreate(&p.b) != hipSuccess || hipEventCreate(&p.e) != hipSuccess)) {
-    (void)hipGetLastError();
-    t.stage = 0;
-    return pick;
-  }
-  p.choice = k == 0 ? t.first[n] : t.first[n] ^ 1;
-  p.n = n;
-  t.stage = k + 1;
-  if (k == 1) {
-    t.first[n] ^= 1;
-    t.launches[n] = 0;
-  }
-  *pb = p.b;
-  *pe = p.e;
-  return p.choice;
+  if (t.count == vptmcm::kPairs || !(t.ratio[n] < 0.0f || ++t.launches[n] >= 16)) return pick;
+  auto& pr = t.pairs[(t.head + t.count) % vptmcm::kPairs];
+  for (int k = 0; k < 2; k++)
+    if ((!pr.b[k] && hipEventCreate(&pr.b[k]) != hipSuccess) || (!pr.e[k] && hipEventCreate(&pr.e[k]) != hipSuccess)) {
+      (void)hipGetLastError();
+      return pick;
+    }
+  t.count++;
+  pr.first = t.first[n];
+  pr.n = n;
+  pr.epoch = t.epoch;
+  pr.stage = 1;
+  t.first[n] ^= 1;
+  t.launches[n] = 0;
+  *pb = pr.b[0];
+  *pe = pr.e[0];
+  return pr.first;
 }
 
 // One march launch of n <= kMaxFusedPasses passes (seeds) with matrix mvp.
@@ -1850,10 +1873,11 @@ void vptmcm_destroy(vptmcm* h) {
     if (h->comp_done[k]) (void)hipEventDestroy(h->comp_done[k]);
   }
   if (h->host_scratch) (void)dev_free(h->host_scratch);
-  for (auto& pr : h->maj_tune.probes) {
-    if (pr.b) (void)hipEventDestroy(pr.b);
-    if (pr.e) (void)hipEventDestroy(pr.e);
-  }
+  for (auto& pr : h->maj_tune.pairs)
+    for (int k = 0; k < 2; k++) {
+      if (pr.b[k]) (void)hipEventDestroy(pr.b[k]);
+      if (pr.e[k]) (void)hipEventDestroy(pr.e[k]);
+    }
   if (h->region.beg) (void)hipEventDestroy(h->region.beg);
   if (h->region.end) (void)hipEventDestroy(h->region.end);
   free_volume(h);
