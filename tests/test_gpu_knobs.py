@@ -110,3 +110,29 @@ def test_every_knob_leaves_the_bits_device_list(monkeypatch):
         assert_photons_equal(got[0], base[0], what)
         assert_rgb32_equal(got[1], base[1], what)
         assert_rgba_equal(got[2], base[2], what)
+
+
+def test_auto_bound_follows_the_measurement(monkeypatch):
+    """VPTMCM_MAJ=auto (the default) times pairs of launches with and without
+    the macro-cell alpha bound outside timed regions and keeps the faster: at
+    the near camera on C3's 512^3 volume the bound saves ~26 % of a pass
+    (profiles/r06/s18), far beyond the pairs' spread, so after a dozen
+    32-pass launches read back by synchronize the march runs with it."""
+    for var in ("VPTMCM_MAJ", "VPTMCM_MARCH_VARIANT"):
+        monkeypatch.delenv(var, raising=False)
+    vol = cf.fbm_volume(512, 512, nthreads=8)
+    gpu = vptmcm.Renderer(512, device=0, layout=vptmcm.LAYOUT_COLUMN4)
+    gpu.set_spectrum(cf.spectrum_buffer("12"))
+    gpu.set_volume(vol)
+    gpu.set_material_tf(cf.tf_spectral())
+    gpu.set_light(np.full(256, 100, np.uint8), np.asarray((1, 0, 0), np.float32))
+    gpu.set_params(extinction=32.0, bounces=8, steps=8)
+    mn = cf.golden_mvp("near")
+    seeds = cf.seed_stream(1 + 12 * 32, start=5)
+    gpu.reset(mn, seeds[0])
+    for j in range(12):
+        gpu.render_passes(mn, seeds[1 + 32 * j: 1 + 32 * (j + 1)])
+        gpu.synchronize()
+    info = gpu.last_launch()
+    gpu.close()
+    assert info["macro"] and info["passes"] == 32, info
