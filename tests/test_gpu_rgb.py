@@ -41,7 +41,11 @@ def same_words(a, b):
                                                ("ramp", 0.6, 24.0, (255, 255, 255, 255)),
                                                ("odd", -0.4, 8.0, (200, 150, 90, 255)),
                                                ("ramp", 0.0, 32.0, (255, 255, 255, 255))])
-def test_rgb_renderer_bitexact(layout, tfk, aniso, ext, env):
+@pytest.mark.parametrize("maj", ["auto", "on"])
+def test_rgb_renderer_bitexact(layout, tfk, aniso, ext, env, maj, monkeypatch):
+    """maj: VPTMCM_MAJ (on: every launch with the macro-cell alpha bound,
+    except on LINEAR, which keeps no macro table)."""
+    monkeypatch.setenv("VPTMCM_MAJ", maj)
     R = 64
     vol = cf.fbm_volume(48, 13)
     gpu = vptmcm.Renderer(R, device=0, layout=layout, renderer=vptmcm.RENDERER_RGB)
@@ -70,6 +74,8 @@ def test_rgb_renderer_bitexact(layout, tfk, aniso, ext, env):
         _, want = cpu.render(mvp, s)
     assert same_words(gpu.read_photons(), cpu.photons).all(), "fused"
     assert np.array_equal(gpu.read_rgba16f(), want)
+    if maj == "on":
+        assert gpu.last_launch()["macro"] == (layout != vptmcm.LAYOUT_LINEAR)
     gpu.close()
 
 
@@ -87,12 +93,15 @@ def test_rgb_environment_and_tf_validation():
     s.close()
 
 
-@pytest.mark.parametrize("camera", ["default", "near", "orbit_tilted"])
-def test_rgb_fused_schedule_robust(camera):
+@pytest.mark.parametrize("camera,maj", [("default", "auto"), ("near", "auto"), ("orbit_tilted", "auto"),
+                                        ("near", "on"), ("default", "on")])
+def test_rgb_fused_schedule_robust(camera, maj, monkeypatch):
     """Fused multi-pass launches of the RGB march at R = 128: the tile schedule
     (volume flags carried between launches), the volume-wave priority, the
     robust-miss path (start points materialised at the end of the launch) and
-    the FAST geometry, bit-exact against the oracle after every launch."""
+    the FAST geometry, bit-exact against the oracle after every launch; with
+    the macro-cell alpha bound pinned on as well."""
+    monkeypatch.setenv("VPTMCM_MAJ", maj)
     R = 128
     vol = cf.fbm_volume(64, 21)
     gpu = vptmcm.Renderer(R, device=0, renderer=vptmcm.RENDERER_RGB)

@@ -15,8 +15,10 @@ scatters). Three links, each checked here in f32 as the kernel rounds:
   3. with alpha from a bilinear lerp of bytes <= k and q = ceil(k / 17),
      fma(17 q, RN(1/255), 2^-16) exceeds pabs and pabs + pscat for every
      albedo.
-The GPU side (tests/test_gpu_fuzz.py even cases, test_gpu_knobs.py
-VPTMCM_MAJ=on) checks the whole march bit-exact against the oracle with it.
+The RGB sibling (k_march_rgb, MCMComputeRenderer.wgsl) gets the same bound
+from row 0 of its TF: the last two tests. The GPU side (tests/test_gpu_fuzz.py
+even cases, test_gpu_knobs.py and test_gpu_rgb.py with VPTMCM_MAJ=on) checks
+the whole march bit-exact against the oracle with it.
 """
 import numpy as np
 
@@ -128,3 +130,62 @@ def test_threshold_dominates_pabs_and_pscat():
             assert np.all(tot < thr) and np.all(pabs < thr), (k, q)
             worst = min(worst, float(np.min(thr.astype(np.float64) - tot.astype(np.float64))))
     assert worst > 2.0 ** -18  # the margin the 2^-16 term buys
+
+
+def rgb_rowmax(alpha_bytes: np.ndarray) -> np.ndarray:
+    """vptmcm.cpp set_transfer_function_one: per density byte v the largest
+    alpha byte of TF row 0's texels [floor((v-1)/255 w - 0.5) - 1,
+    floor((v+1)/255 w - 0.5) + 2], clamped."""
+    w = len(alpha_bytes)
+    out = np.zeros(256, np.uint8)
+    for v in range(256):
+        lo = max(0, int(np.floor((v - 1) / 255.0 * w - 0.5)) - 1)
+        hi = min(w - 1, int(np.floor((v + 1) / 255.0 * w - 0.5)) + 2)
+        out[v] = alpha_bytes[lo:hi + 1].max()
+    return out
+
+
+def test_rgb_texels_a_sample_reaches_are_in_its_rows():
+    """The RGB sibling samples TF row 0 at (density, 0) (MCMComputeRenderer.wgsl
+    sampleVolumeColor; kernels.hip k_march_rgb): texels floor(d w - 0.5) and
+    the next, clamped. Every alpha byte it can read is within the macro cell's
+    code (the row maxima of bytes vmin - 2 .. vmax + 2, k_macro_alpha)."""
+    rng = np.random.default_rng(3)
+    for w in (2, 3, 100, 255, 256, 257, 1000, 4096):
+        alpha = rng.integers(0, 256, w).astype(np.uint8)
+        rm = rgb_rowmax(alpha)
+        n = 100_000
+        vmin = rng.integers(0, 256, n)
+        vmax = np.minimum(vmin + rng.integers(0, 64, n), 255)
+        span = (vmax - vmin + 1).astype(np.float64)
+        b = (vmin[:, None] + np.floor(rng.random((n, 8)) * span[:, None])).astype(F32)
+        fr = rng.random((n, 3)).astype(F32)
+        c00, c10 = lerp(b[:, 0], b[:, 1], fr[:, 0]), lerp(b[:, 2], b[:, 3], fr[:, 0])
+        c01, c11 = lerp(b[:, 4], b[:, 5], fr[:, 0]), lerp(b[:, 6], b[:, 7], fr[:, 0])
+        d = lerp(lerp(c00, c10, fr[:, 1]), lerp(c01, c11, fr[:, 1]), fr[:, 2]) * INV255
+        x = fma(np.clip(d, F32(-1), F32(2)), F32(w), F32(-0.5))
+        i = np.floor(x).astype(np.int64)
+        got = np.maximum(alpha[np.clip(i, 0, w - 1)], alpha[np.clip(i + 1, 0, w - 1)])
+        code_k = np.array([rm[max(a - 2, 0):min(c + 2, 255) + 1].max() for a, c in zip(vmin, vmax)])
+        assert np.all(got <= code_k), w
+
+
+def test_rgb_threshold_dominates_pabs_and_pscat():
+    """alpha = lerp of two RN(byte / 255) texels (the host decodes alpha
+    linearly), pscat = alpha * max(r, g, b) with the sRGB-decoded channels
+    (<= 1, one ulp over allowed)."""
+    rng = np.random.default_rng(4)
+    cmax = np.concatenate([rng.random(512).astype(F32),
+                           np.array([0.0, 1.0, np.nextafter(F32(1), F32(2))], F32)])
+    for k in range(256):
+        thr = threshold((k + 16) // 17)
+        a = (rng.integers(0, k + 1, 4096).astype(F32) * INV255).astype(F32)
+        bb = (rng.integers(0, k + 1, 4096).astype(F32) * INV255).astype(F32)
+        a[:64] = bb[64:128] = F32(k) * INV255
+        ft = rng.random(4096).astype(F32)
+        ft[::5] = F32(1.0)
+        ca = lerp(a, bb, ft)[:, None]
+        pnull = F32(1) - ca
+        for pscat in (np.zeros_like(ca), ca * cmax[None, :]):
+            pabs = (F32(1) - pnull) - pscat
+            assert np.all(pabs + pscat < thr) and np.all(pabs < thr), k

@@ -154,6 +154,14 @@ for s in $STEPS; do
       python3 -c "import json; d=json.load(open('$OUT/maj.json')); print(json.dumps({'variant': $v, 'maj': '${VPTMCM_MAJ:-auto}', 'camera': '$cam', 'volume': ${vol:-512}, 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'unfused_us': d['unfused']['kernel_avg_us']}))" >> $OUT/majab.jsonl
     done
     echo "majab rc=0" | tee -a $OUT/status.txt; cat $OUT/majab.jsonl ;;
+  rgbab)  # the RGB sibling's line with the macro-cell bound on / off / auto, "maj:camera" cases
+    for c in ${RGB_CASES:-on:near off:near on:default off:default auto:near auto:default}; do
+      IFS=: read m cam <<< "$c"
+      VPTMCM_MAJ=$m timeout -k 10 300 python bench.py --camera $cam --steps 64 --warmup 64 --cpu-seconds 0 --js-steps 0 --rgb-steps 256 --general-steps 0 --api-steps 0 --unfused-steps 0 --near-steps 0 > $OUT/rgb.json 2>> $OUT/rgbab.err
+      rc=$?; [ $rc -ne 0 ] && { echo "rgbab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
+      python3 -c "import json; d=json.load(open('$OUT/rgb.json'))['rgb']; print(json.dumps({'maj': '$m', 'camera': '$cam', 'value': d['value'], 'us_per_pass': d['kernel_us_per_pass'], 'macro_skip': d['macro_skip']}))" >> $OUT/rgbab.jsonl
+    done
+    echo "rgbab rc=0" | tee -a $OUT/status.txt; cat $OUT/rgbab.jsonl ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?" | tee -a $OUT/status.txt ;;
   pmc)

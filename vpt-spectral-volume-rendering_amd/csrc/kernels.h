@@ -119,7 +119,7 @@ hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSee
                             const TileSched& T, float* ph, const uint8_t* vol, const float4* tf,
                             uint16_t* rgba, float* rgb32, hipStream_t s,
                             hipEvent_t ev_beg = nullptr, hipEvent_t ev_end = nullptr,
-                            MarchLaunchInfo* info = nullptr);
+                            MarchLaunchInfo* info = nullptr, const uint8_t* maj = nullptr);
 // LINEAR -> CORNER8 / BRICK8 relayout of the cell box [c0, c0 + n) (default:
 // every cell of the (W+1)(H+1)(D+1) grid)
 hipError_t launch_corner8(const uint8_t* lin, uint32_t W, uint32_t H, uint32_t D, uint32_t BW,

@@ -1156,19 +1156,24 @@ __device__ __forceinline__ void rgb_reset_fast(const MarchParams& P, float sx, f
   }
 }
 
-template <uint32_t L, bool GEO>
+// MAJ: the macro-cell alpha bound of k_march (maj_threshold; the host's row
+// maxima for this TF cover every texel a density byte's samples reach)
+template <uint32_t L, bool GEO, bool MAJ>
 __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, const MarchParams P,
                                                            const TileSched T,
                                                            float* __restrict__ ph,
                                                            const uint8_t* __restrict__ vol,
                                                            const float4* __restrict__ tf,
                                                            uint16_t* __restrict__ rgba,
-                                                           float* __restrict__ rgb32) {
+                                                           float* __restrict__ rgb32,
+                                                           const uint8_t* __restrict__ maj) {
   __shared__ float4 s_tf[kRgbTfMax];
+  __shared__ uint4 s_maj4[MAJ ? kMajBytes / 16 : 1];
   __shared__ uint32_t s_red[64];
   __shared__ uint32_t s_tile[16];
   if (VPT_GUARD) {
     poison_lds(s_tf, sizeof s_tf);
+    poison_lds(s_maj4, sizeof s_maj4);
     poison_lds(s_red, sizeof s_red);
     poison_lds(s_tile, sizeof s_tile);
     __syncthreads();
@@ -1212,6 +1217,9 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
     rad = f3{ph[(kRgbRad0 + 0) * S + i], ph[(kRgbRad0 + 1) * S + i], ph[(kRgbRad0 + 2) * S + i]};
   }
   for (uint32_t k = threadIdx.x; k < P.tf_w; k += kMarchBlock) s_tf[k] = tf[k];
+  if constexpr (MAJ)
+    for (uint32_t k = threadIdx.x; k < P.maj_bytes / 16u; k += kMarchBlock)
+      s_maj4[k] = reinterpret_cast<const uint4*>(maj)[k];
   __syncthreads();
   if (!live) {
     if (tile < P.n_tiles && lane == 0u) {  // an idle out-of-band tile
@@ -1283,7 +1291,15 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
         continue;
       }
       entered = true;
-      VolTap vt = vol_fetch<L>(P, vol, pos);  // gather in flight from here
+      // a certain null collision skips the gather (k_march)
+      const VolCell vcell = vol_cell(P, pos);
+      bool skip = false;
+      if constexpr (MAJ)
+        skip = !oob && wheel >= maj_threshold(P, vcell, reinterpret_cast<const uint8_t*>(s_maj4));
+      VolTap vt;
+      vt.fx = vt.fy = vt.fz = 0.0f;
+      vt.lo = vt.hi = 0u;
+      if (!skip) vt = vol_fetch_cell<L>(P, vol, vcell);  // gather in flight from here
       // speculative reset candidate (draws h1..h4) and the g-independent HG half
       f3 rpos, rdir;
       rgb_reset_fast<GEO>(P, sx, sy, fixed, from, slab_hw, omf, h1, h2, h3, h4, rpos, rdir);
@@ -1304,7 +1320,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
       float pnull = 1.0f - ca;
       float pscat = (bounces >= P.max_bounces) ? 0.0f : ca * smax(smax(cr, cg), cb);
       float pabs = (1.0f - pnull) - pscat;
-      if (oob || wheel < pabs) {  // exit (environment) or absorption (wgsl:126-139)
+      if (oob || (!skip && wheel < pabs)) {  // exit (environment) or absorption (wgsl:126-139)
         samples++;
         float inv = rcp_in_range((float)samples);
         f3 Lr = oob ? f3{tr.x * P.env[0], tr.y * P.env[1], tr.z * P.env[2]} : f3{0.0f, 0.0f, 0.0f};
@@ -1316,7 +1332,7 @@ __global__ __launch_bounds__(kMarchBlock) void k_march_rgb(const PassSeeds PS, c
         tr = f3{1.0f, 1.0f, 1.0f};
         st = h4;
         rb = rbpix;
-      } else if (wheel < pabs + pscat) {  // scattering (wgsl:140-144)
+      } else if (!skip && wheel < pabs + pscat) {  // scattering (wgsl:140-144)
         tr = f3{tr.x * cr, tr.y * cg, tr.z * cb};
         if (iso) {
           dir = u;
@@ -1739,24 +1755,26 @@ hipError_t launch_reset_rgb(const MarchParams& P, float* ph, hipStream_t s) {
 hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSeeds& PS,
                             const TileSched& T, float* ph, const uint8_t* vol, const float4* tf,
                             uint16_t* rgba, float* rgb32, hipStream_t s, hipEvent_t ev_beg,
-                            hipEvent_t ev_end, MarchLaunchInfo* info) {
+                            hipEvent_t ev_end, MarchLaunchInfo* info, const uint8_t* maj) {
   dim3 grid(tile_blocks(P, kMarchBlock));
   const bool geo = P.w_bounded && P.blur == 0.0f && (P.R & 1u) == 0u;
+  const bool mj = P.maj_on && maj;
   if (info) {  // mode: 1 with the FAST geometry (k_march_rgb<L, true>), else 0
     const uint32_t tpl = layout == kLayoutBrick8 ? (P.vol32 ? kTplBrick8 : kTplBrick8Wide)
                        : layout == kLayoutColumn4 ? (P.vol32 ? kTplColumn4 : kTplColumn4Wide)
                        : layout == kLayoutCorner8 ? (P.vol32 ? kTplCorner8 : kTplCorner8Wide)
                        : kTplLinear;
-    *info = MarchLaunchInfo{geo ? 1u : 0u, tpl, 1u, PS.n};
+    *info = MarchLaunchInfo{geo ? 1u : 0u, tpl, 1u | (mj ? 2u : 0u), PS.n};
   }
-#define VPT_LAUNCH_RGB(LAY)                                                                       \
-  do {                                                                                            \
-    if (geo)                                                                                      \
-      hipExtLaunchKernelGGL((k_march_rgb<LAY, true>), grid, dim3(kMarchBlock), 0, s, ev_beg,      \
-                            ev_end, 0, PS, P, T, ph, vol, tf, rgba, rgb32);                       \
-    else                                                                                          \
-      hipExtLaunchKernelGGL((k_march_rgb<LAY, false>), grid, dim3(kMarchBlock), 0, s, ev_beg,     \
-                            ev_end, 0, PS, P, T, ph, vol, tf, rgba, rgb32);                       \
+#define VPT_LAUNCH_RGB1(LAY, G, MJ)                                                                \
+  hipExtLaunchKernelGGL((k_march_rgb<LAY, G, MJ>), grid, dim3(kMarchBlock), 0, s, ev_beg, ev_end, 0, \
+                        PS, P, T, ph, vol, tf, rgba, rgb32, maj)
+#define VPT_LAUNCH_RGB(LAY)                                             \
+  do {                                                                  \
+    if (geo && mj) VPT_LAUNCH_RGB1(LAY, true, true);                    \
+    else if (geo) VPT_LAUNCH_RGB1(LAY, true, false);                    \
+    else if (mj) VPT_LAUNCH_RGB1(LAY, false, true);                     \
+    else VPT_LAUNCH_RGB1(LAY, false, false);                            \
   } while (0)
   if (layout == kLayoutBrick8 && P.vol32)
     VPT_LAUNCH_RGB(kTplBrick8);
@@ -1773,6 +1791,7 @@ hipError_t launch_march_rgb(uint32_t layout, const MarchParams& P, const PassSee
   else
     VPT_LAUNCH_RGB(kTplLinear);
 #undef VPT_LAUNCH_RGB
+#undef VPT_LAUNCH_RGB1
   return hipGetLastError();
 }
 

@@ -970,7 +970,7 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   }
   MarchParams P = make_params(h, mvp, seeds[0]);
   hipEvent_t tb = nullptr, te = nullptr;  // a tuner probe's events
-  if (h->maj_ok && h->kind == VPTMCM_RENDERER_SPECTRAL && maj_tune_pick(h, mvp, n, &tb, &te) == 1) {
+  if (h->maj_ok && maj_tune_pick(h, mvp, n, &tb, &te) == 1) {
     P.maj_on = 1u;
     P.maj_shift = h->maj_shift;
     P.maj_nx = h->maj_nx;
@@ -1024,7 +1024,8 @@ int do_march(vptmcm* h, const float* mvp, const uint32_t* seeds, uint32_t n) {
   P.sched = (h->n_tiles > kSchedMaxTiles || (h->variant & 2u)) ? 1u : (h->variant & 128u) ? 2u : 0u;
   if (h->kind == VPTMCM_RENDERER_RGB)
     HIPCHK(h, launch_march_rgb(h->layout, P, PS, T, h->photons, vol, h->tf_rgb, h->rgba, h->rgb32,
-                               h->stream, eb, ee, &h->last_launch));
+                               h->stream, eb, ee, &h->last_launch,
+                               (h->variant & 256u) ? nullptr : h->maj_q));  // variant bit 8: no bound
   else
     HIPCHK(h, launch_march(h->layout, h->variant, P, PS, T, h->photons, vol, h->tf_rg, h->tf_b4,
                            h->tf_brow, h->light, h->rgba, h->rgb32, h->stream, eb, ee, h->tf_rows,
@@ -1957,8 +1958,8 @@ static int volume_begin_one(vptmcm* h, uint32_t width, uint32_t height, uint32_t
   h->H = height;
   h->D = depth;
   // the macro-cell table: the finest power-of-two macro (>= 8 texel cells)
-  // whose codes fit the march's LDS table (spectral march, re-laid-out layouts)
-  if (h->kind == VPTMCM_RENDERER_SPECTRAL && h->layout != kLayoutLinear) {
+  // whose codes fit the march's LDS table (re-laid-out layouts)
+  if (h->layout != kLayoutLinear) {
     for (uint32_t sh = 3; sh < 14 && !h->maj_ok; sh++) {
       const uint64_t nx = ((uint64_t)width + (1u << sh)) >> sh, ny = ((uint64_t)height + (1u << sh)) >> sh,
                      nz = ((uint64_t)depth + (1u << sh)) >> sh;  // ceil((W + 1) / M)
@@ -2177,8 +2178,24 @@ static int set_transfer_function_one(vptmcm* h, const uint8_t* rgba, uint32_t wi
   }
   HIPCHK(h, hipMemcpyAsync(h->tf_rgb, row.data(), width * sizeof(float4), hipMemcpyHostToDevice,
                            enq(h)));
+  // the macro-cell alpha codes' row maxima: per density byte v the largest
+  // alpha byte of the texels a density within one byte of v reaches (texel
+  // floor(d * width - 0.5) and the next, clamped), one texel of margin more
+  // each way; k_macro_alpha widens that to v - 2 .. v + 2
+  uint8_t rowmax[256];
+  for (int v = 0; v < 256; v++) {
+    const double w = (double)width;
+    const long lo = std::max(0L, (long)std::floor((v - 1) / 255.0 * w - 0.5) - 1);
+    const long hi = std::min((long)width - 1, (long)std::floor((v + 1) / 255.0 * w - 0.5) + 2);
+    uint8_t m = 0;
+    for (long t = lo; t <= hi; t++) m = std::max(m, rgba[4 * (size_t)t + 3]);
+    rowmax[v] = m;
+  }
+  HIPCHK(h, hipMemcpyAsync(h->tf_rowmax, rowmax, 256, hipMemcpyHostToDevice, enq(h)));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->tf_rgb_w = width;
+  h->maj_valid = false;
+  maj_tune_reset(h);
   return VPTMCM_OK;
 }
 
