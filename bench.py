@@ -563,15 +563,15 @@ def main():
     if a.near_steps > 0 and single and a.camera == "default":
         r.synchronize()
         mn = cf.golden_mvp("near")
-        nseeds = cf.seed_stream(a.near_steps + 193, start=3, rank=rank)
+        nseeds = cf.seed_stream(a.near_steps + 321, start=3, rank=rank)
         r.reset(mn, nseeds[0])
-        # the photons' depth distribution and the deal settle; six launches also
+        # the photons' depth distribution and the deal settle; ten launches also
         # give the library's macro-skip tuner its pairs for this camera
-        r.render_passes(mn, nseeds[1:193])
+        r.render_passes(mn, nseeds[1:321])
         r.synchronize()
         r.enable_kernel_timing(not a.no_timing)
         t6 = time.perf_counter()
-        nl = passes_on(nseeds, 193, a.near_steps, m=mn)
+        nl = passes_on(nseeds, 321, a.near_steps, m=mn)
         r.synchronize()
         el6 = time.perf_counter() - t6
         nk_ms, nn = r.kernel_time()
@@ -681,9 +681,9 @@ def main():
         q.set_transfer_function(ttf)
         q.set_environment((255, 255, 255, 255))
         q.set_params(extinction=a.extinction, anisotropy=0.7, bounces=8, steps=S)
-        rseeds = cf.seed_stream(a.rgb_steps + 193, start=2, rank=rank)
+        rseeds = cf.seed_stream(a.rgb_steps + 321, start=2, rank=rank)
         q.reset(mvp, rseeds[0])
-        for k in range(6):  # settle; the macro-skip tuner's pairs for this renderer
+        for k in range(10):  # settle; the macro-skip tuner's pairs for this renderer
             q.render_passes(mvp, rseeds[1 + 32 * k:33 + 32 * k])
         q.synchronize()
         q.enable_kernel_timing(not a.no_timing)
@@ -691,7 +691,7 @@ def main():
         done = 0
         while done < a.rgb_steps:
             n = min(F, a.rgb_steps - done)
-            q.render_passes(mvp, rseeds[193 + done:193 + done + n])
+            q.render_passes(mvp, rseeds[321 + done:321 + done + n])
             done += n
         q.synchronize()
         el4 = time.perf_counter() - t4

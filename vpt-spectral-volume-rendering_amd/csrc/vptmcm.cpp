@@ -282,6 +282,7 @@ struct vptmcm {
   // caller that enqueues many launches ahead of the GPU still gets its
   // measurements.
   static constexpr int kPairs = 8;
+  static constexpr int kQuads = 2;
   struct MajTuner {
     int mode = 2;                 // 0 off, 1 on, 2 auto
     int choice = 0;               // the last pick measured, for sizes with none yet
@@ -296,6 +297,9 @@ struct vptmcm {
     // saves 1.6 %).
     float ratio[kMaxFusedPasses + 1];
     float half[kMaxFusedPasses + 1];         // a pair's ratio awaiting the other order (-1: none)
+    // pairs of pairs folded into ratio[n]: it decides from kQuads on (until
+    // then every launch of size n outside a timed region is a probe)
+    uint8_t quads[kMaxFusedPasses + 1];
     uint32_t launches[kMaxFusedPasses + 1];  // launches of size n since its last pair
     uint8_t first[kMaxFusedPasses + 1];      // the first choice of size n's next pair
     uint8_t half_first[kMaxFusedPasses + 1]; // the first choice of the pair held in half
@@ -813,6 +817,7 @@ int time_close(vptmcm* h) {
 void maj_tune_reset(vptmcm* h) {
   for (uint32_t n = 0; n <= kMaxFusedPasses; n++) {
     h->maj_tune.ratio[n] = h->maj_tune.half[n] = -1.0f;
+    h->maj_tune.quads[n] = 0;
     h->maj_tune.launches[n] = 0;
     h->maj_tune.first[n] = 0;
   }
@@ -904,7 +909,8 @@ void maj_tune_harvest(vptmcm* h) {
     t.half[n] = -1.0f;
     float& q = t.ratio[n];
     q = q < 0.0f ? rr : 0.5f * q + 0.5f * rr;
-    t.choice = q < 1.0f ? 1 : 0;
+    if (t.quads[n] < 255) t.quads[n]++;
+    if (t.quads[n] >= vptmcm::kQuads) t.choice = q < 1.0f ? 1 : 0;
     if (const char* v = getenv("VPTMCM_MAJ_TRACE"))
       if (v[0] == '1')
         fprintf(stderr, "maj_tune: pairs n=%u on %.3f off %.3f us/pass, ratio %.4f (both orders %.4f) -> %.4f, "
@@ -925,7 +931,8 @@ int maj_tune_pick(vptmcm* h, const float* mvp, uint32_t n, hipEvent_t* pb, hipEv
     memcpy(t.mvp, mvp, sizeof t.mvp);
     maj_tune_reset(h);
   }
-  const int pick = t.ratio[n] < 0.0f ? t.choice : t.ratio[n] < 1.0f ? 1 : 0;
+  const bool decided = t.quads[n] >= vptmcm::kQuads;
+  const int pick = !decided ? t.choice : t.ratio[n] < 1.0f ? 1 : 0;
   auto* open = t.count > 0 ? &t.pairs[(t.head + t.count - 1) % vptmcm::kPairs] : nullptr;
   if (open && open->stage != 1) open = nullptr;
   if (open && (h->timing || open->n != n || open->epoch != t.epoch)) {
@@ -939,7 +946,7 @@ int maj_tune_pick(vptmcm* h, const float* mvp, uint32_t n, hipEvent_t* pb, hipEv
     *pe = open->e[1];
     return open->first ^ 1;
   }
-  if (t.count == vptmcm::kPairs || !(t.ratio[n] < 0.0f || ++t.launches[n] >= 16)) return pick;
+  if (t.count == vptmcm::kPairs || !(!decided || ++t.launches[n] >= 16)) return pick;
   auto& pr = t.pairs[(t.head + t.count) % vptmcm::kPairs];
   for (int k = 0; k < 2; k++)
     if ((!pr.b[k] && hipEventCreate(&pr.b[k]) != hipSuccess) || (!pr.e[k] && hipEventCreate(&pr.e[k]) != hipSuccess)) {
