@@ -87,6 +87,11 @@ def parse():
                          "stream (inline: VPTMCM_ALLREDUCE_INLINE, no event hop to the side stream; "
                          "the composite is about to be read) or on the side stream like the ones "
                          "between launches, which overlap the next march")
+    ap.add_argument("--shard-composite", choices=["on", "off"], default="on",
+                    help="N > 1 under a launcher: the composites reduce-scatter (on: "
+                         "VPTMCM_ALLREDUCE_SHARDED, each rank keeps the summed (rgb*n, n) of 1/N of the "
+                         "pixels, half the all-reduce's traffic; reading the image all-gathers the shards, "
+                         "as the device-list composite's readers do) or all-reduce (off)")
     ap.add_argument("--per-pass-steps", type=int, default=64,
                     help="N > 1: passes of a second timed region compositing after EVERY pass "
                          "(north_star's 'all-reduce each progressive pass'; one launch per pass; "
@@ -359,11 +364,13 @@ def main():
 
     # the composite that ends a region (and runs every `every` passes): the
     # RCCL all-reduce across ranks, or the device-list handle's composite
-    composite = r.allreduce_radiance if multi else (r.composite if grouped else None)
+    shard = a.shard_composite == "on"
+    composite = ((lambda: r.allreduce_radiance(sharded=shard)) if multi
+                 else (r.composite if grouped else None))
     # the composite that ends a region (what the display reads next)
     composite_last = composite
     if multi and a.final_composite == "inline":
-        composite_last = lambda: r.allreduce_radiance(inline=True)  # noqa: E731
+        composite_last = lambda: r.allreduce_radiance(inline=True, sharded=shard)  # noqa: E731
     single = not multi and not grouped
     n_unfused = a.unfused_steps if single else 0
     n_api = a.api_steps if single else 0
@@ -716,7 +723,7 @@ def main():
     if multi:
         parallelism = (f"photon-parallel replicas x{world}, one process per GPU, RCCL all-reduce of "
                        f"(rgb*n, n) every {every} pass(es)")
-        comp_kind = "rccl-allreduce"
+        comp_kind = "rccl-reduce-scatter" if a.shard_composite == "on" else "rccl-allreduce"
     elif grouped:
         parallelism = (f"photon-parallel replicas x{group} in one process (device-list handle over "
                        f"devices {devs}), composite of (rgb*n, n) on device {devs[0]} every {every} "

@@ -310,6 +310,14 @@ int vptmcm_comm_allreduce_radiance(vptmcm* h);
  * lowest latency for a composite about to be read / shown; the next march
  * waits for it). Same results either way. */
 #define VPTMCM_ALLREDUCE_INLINE 1u
+/* VPTMCM_ALLREDUCE_SHARDED: a reduce-scatter instead of the all-reduce — rank
+ * r keeps the summed (rgb*n, n) of pixels [r*R*R/N, (r+1)*R*R/N), half the
+ * all-reduce's traffic per rank (the image stays sharded, as the device-list
+ * composite's does); the next vptmcm_comm_read_composite / _read_composite
+ * all-gathers the shards first and is then a COLLECTIVE call (every rank makes
+ * it). When N does not divide R*R the flag is ignored (a plain all-reduce).
+ * Same composite either way (RCCL's summation order aside). */
+#define VPTMCM_ALLREDUCE_SHARDED 2u
 int vptmcm_comm_allreduce_radiance_ex(vptmcm* h, uint32_t flags);
 
 /* Wait for the last all-reduce and return the composite rgb = sum(rgb*n)/sum(n)

@@ -66,8 +66,8 @@ DRIVER = textwrap.dedent('''
             return (time.perf_counter() - self.t0) * 1e3 + 1e-3, self.launches
         def last_launch(self):
             return {"mode": 2, "tpl": 5, "spec": True, "macro": False, "passes": 32, "launches": 0}
-        def allreduce_radiance(self, inline=False):
-            LOG.append(["allreduce_inline" if inline else "allreduce"])
+        def allreduce_radiance(self, inline=False, sharded=False):
+            LOG.append(["allreduce_inline" if inline else "allreduce", bool(sharded)])
             if os.environ.get("FAKE_DIE_RANK") == os.environ["RANK"]:
                 os._exit(3)  # this rank dies before its first composite
         def read_composite(self):
@@ -144,6 +144,8 @@ def test_bench_two_ranks_driver_command_line(tmp_path, world):
         rk = [e[0] for e in rest if e[0] in ("passes", "allreduce", "allreduce_inline")]
         assert rk[:128] == ["passes", "allreduce"] * 63 + ["passes", "allreduce_inline"]
         assert all(len(e[1]) == 1 for e in rest if e[0] == "passes")
+        # the composites reduce-scatter by default (--shard-composite on)
+        assert all(e[1] for e in lg if e[0] in ("allreduce", "allreduce_inline"))
     seeds = [[s for e in lg if e[0] == "passes" for s in e[1]] for lg in logs]
     for a in range(world):
         for b in range(a + 1, world):

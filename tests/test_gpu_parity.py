@@ -414,8 +414,10 @@ def test_composite_single_rank():
 def test_composite_single_rank_inline_and_side_stream():
     """VPTMCM_ALLREDUCE_INLINE (the all-reduce on the march stream) and the
     side-stream all-reduce, interleaved on one communicator, with and without
-    a read between them: every composite read equals the division of k_pack's
-    buffer of the frame it follows, bit for bit, and so the two modes agree."""
+    a read between them, each also as a reduce-scatter (VPTMCM_ALLREDUCE_SHARDED,
+    read through the all-gather; one rank: the whole frame is its shard): every
+    composite read equals the division of k_pack's buffer of the frame it
+    follows, bit for bit, and so the modes agree."""
     gpu, _ = make_pair(64, cf.sphere_in_cube(64), cf.tf_spectral())
     gpu.comm_init(vptmcm.unique_id(), 1, 0)
     mvp = cf.default_mvp_inverse()
@@ -426,22 +428,24 @@ def test_composite_single_rank_inline_and_side_stream():
             return np.where(pk[..., 3:] > 0, pk[..., :3] / pk[..., 3:], np.float32(0)).astype(np.float32)
 
     seeds = cf.seed_stream(40, start=50)
-    modes = [True, False, True, True, False, False, True, False]
-    for k, inline in enumerate(modes):
+    modes = [(True, False), (False, True), (True, True), (True, False), (False, False), (False, True),
+             (True, True), (False, False), (True, True)]
+    for k, (inline, sharded) in enumerate(modes):
         gpu.render_passes(mvp, seeds[4 * k:4 * k + 4])
-        gpu.allreduce_radiance(inline=inline)
+        gpu.allreduce_radiance(inline=inline, sharded=sharded)
         if k % 3 != 1:  # some composites are never read: the next one overtakes them
             rgb, n = gpu.read_composite()
-            assert_rgb32_equal(rgb, from_pack(gpu.pack_radiance()), f"composite {k} inline={inline}")
+            assert_rgb32_equal(rgb, from_pack(gpu.pack_radiance()),
+                               f"composite {k} inline={inline} sharded={sharded}")
             assert np.array_equal(n.reshape(-1), gpu.read_photons()[:, 7].astype(np.float32))
     # a render() queued behind an inline all-reduce, then one more inline one
     gpu.allreduce_radiance(inline=True)
     gpu.render(mvp, seeds[-1])
-    gpu.allreduce_radiance(inline=True)
+    gpu.allreduce_radiance(inline=True, sharded=True)
     rgb, n = gpu.read_composite()
     assert_rgb32_equal(rgb, from_pack(gpu.pack_radiance()), "after a queued render")
     with pytest.raises(vptmcm.VptError, match="unknown flags"):
-        gpu._ck(gpu.L.vptmcm_comm_allreduce_radiance_ex(gpu.h, 6))
+        gpu._ck(gpu.L.vptmcm_comm_allreduce_radiance_ex(gpu.h, 5))
     gpu.close()
 
 

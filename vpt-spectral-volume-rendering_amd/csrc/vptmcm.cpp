@@ -341,6 +341,7 @@ struct vptmcm {
   hipEvent_t comp_ready[2] = {nullptr, nullptr};
   hipEvent_t comp_done[2] = {nullptr, nullptr};
   int comp_next = 0, comp_last = -1;
+  bool comp_sharded[2] = {false, false};  // comp[k] holds only this rank's reduce-scattered shard
   // Lazily fused render() calls: consecutive passes with one matrix are queued
   // and launched as one multi-pass march when anything observes or changes
   // the renderer (every other entry point flushes first), or at 32 passes.
@@ -2654,9 +2655,21 @@ int vptmcm_comm_allreduce_radiance_ex(vptmcm* h, uint32_t flags) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (int rc_ = flush_renders(h)) return rc_;
   if (!h->comm) FAIL(h, VPTMCM_ECOMM, "comm_allreduce_radiance: no communicator");
-  if (flags & ~(uint32_t)VPTMCM_ALLREDUCE_INLINE) FAIL(h, VPTMCM_EINVAL, "comm_allreduce_radiance: unknown flags");
+  if (flags & ~(uint32_t)(VPTMCM_ALLREDUCE_INLINE | VPTMCM_ALLREDUCE_SHARDED))
+    FAIL(h, VPTMCM_EINVAL, "comm_allreduce_radiance: unknown flags");
   HIPCHK(h, hipSetDevice(h->device));
   int k = h->comp_next;
+  const size_t words = (size_t)h->R * h->R * 4;  // R*R float4
+  // reduce-scatter: equal shards of whole pixels, rank r's in place at r * shard
+  const bool shard = (flags & VPTMCM_ALLREDUCE_SHARDED) && h->nranks > 0 &&
+                     ((size_t)h->R * h->R) % (size_t)h->nranks == 0;
+  const size_t shard_words = shard ? words / (size_t)h->nranks : words;
+  float* base = reinterpret_cast<float*>(h->comp[k]);
+  auto collective = [&](hipStream_t st) {
+    return shard ? ncclReduceScatter(base, base + (size_t)h->rank * shard_words, shard_words, ncclFloat32,
+                                     ncclSum, h->comm, st)
+                 : ncclAllReduce(base, base, words, ncclFloat32, ncclSum, h->comm, st);
+  };
   if (!h->pack_fresh) {  // the stream does not end with a march that packed comp[k]
     stream_op(h);
     // the buffer must be free of the all-reduce issued two passes ago
@@ -2670,21 +2683,16 @@ int vptmcm_comm_allreduce_radiance_ex(vptmcm* h, uint32_t flags) {
     // next march waits for it. Ordered after the side stream's last
     // all-reduce, so the communicator's collectives stay in issue order.
     HIPCHK(h, hipStreamWaitEvent(enq(h), h->comp_done[k ^ 1], 0));
-    if (int rc = comm_call(h, ncclAllReduce(h->comp[k], h->comp[k], (size_t)h->R * h->R * 4,
-                                            ncclFloat32, ncclSum, h->comm, enq(h)),
-                           "comm_allreduce_radiance"))
-      return rc;
+    if (int rc = comm_call(h, collective(enq(h)), "comm_allreduce_radiance")) return rc;
     HIPCHK(h, hipEventRecord(h->comp_done[k], enq(h)));
   } else {
     stream_op(h);
     HIPCHK(h, hipEventRecord(h->comp_ready[k], enq(h)));
     HIPCHK(h, hipStreamWaitEvent(h->comm_stream, h->comp_ready[k], 0));
-    if (int rc = comm_call(h, ncclAllReduce(h->comp[k], h->comp[k], (size_t)h->R * h->R * 4,
-                                            ncclFloat32, ncclSum, h->comm, h->comm_stream),
-                           "comm_allreduce_radiance"))
-      return rc;
+    if (int rc = comm_call(h, collective(h->comm_stream), "comm_allreduce_radiance")) return rc;
     HIPCHK(h, hipEventRecord(h->comp_done[k], h->comm_stream));
   }
+  h->comp_sharded[k] = shard;
   h->comp_last = k;
   h->comp_next = k ^ 1;
   return VPTMCM_OK;
@@ -2745,6 +2753,16 @@ int vptmcm_read_composite(vptmcm* h, uint16_t* rgba16f, float* rgb, float* count
   S.p[0] = h->comp[h->comp_last];
   // (an all-reduce issued inline ran on the march stream)
   HIPCHK(h, hipStreamWaitEvent(h->comm_stream, h->comp_done[h->comp_last], 0));
+  if (h->comp_sharded[h->comp_last]) {  // every rank's shard, in place (collective)
+    const size_t shard_words = npx * 4 / (size_t)h->nranks;
+    float* base = reinterpret_cast<float*>(h->comp[h->comp_last]);
+    if (int rc = comm_call(h, ncclAllGather(base + (size_t)h->rank * shard_words, base, shard_words, ncclFloat32,
+                                            h->comm, h->comm_stream),
+                           "read_composite"))
+      return rc;
+    HIPCHK(h, hipEventRecord(h->comp_done[h->comp_last], h->comm_stream));
+    h->comp_sharded[h->comp_last] = false;
+  }
   HIPCHK(h, launch_composite(S, (uint32_t)npx, h->comp_rgb32, h->comp_rgba, h->comp_counts,
                              h->comm_stream));
   if (rgba16f)

@@ -470,11 +470,13 @@ static napi_value js_comm_init(napi_env env, napi_callback_info info) {
                                           (int)get_u32(env, argv[3])));
 }
 
-/* commAllreduceRadiance(h[, inline]): inline = true runs the all-reduce on
- * the march stream (VPTMCM_ALLREDUCE_INLINE, for a composite about to be shown) */
+/* commAllreduceRadiance(h[, inline[, sharded]]): inline = true runs the
+ * all-reduce on the march stream (VPTMCM_ALLREDUCE_INLINE, for a composite
+ * about to be shown); sharded = true reduce-scatters (VPTMCM_ALLREDUCE_SHARDED:
+ * the next commReadComposite is collective) */
 static napi_value js_comm_allreduce_radiance(napi_env env, napi_callback_info info) {
-    napi_value argv[2];
-    size_t argc = 2;
+    napi_value argv[3];
+    size_t argc = 3;
     if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return NULL;
     if (argc < 1) {
         napi_throw_type_error(env, NULL, "too few arguments");
@@ -487,7 +489,13 @@ static napi_value js_comm_allreduce_radiance(napi_env env, napi_callback_info in
         napi_throw_type_error(env, NULL, "inline must be a boolean");
         return NULL;
     }
-    return check(env, h, vptmcm_comm_allreduce_radiance_ex(h, inl ? VPTMCM_ALLREDUCE_INLINE : 0u));
+    bool shd = false;
+    if (argc > 2 && napi_get_value_bool(env, argv[2], &shd) != napi_ok) {
+        napi_throw_type_error(env, NULL, "sharded must be a boolean");
+        return NULL;
+    }
+    return check(env, h, vptmcm_comm_allreduce_radiance_ex(
+                             h, (inl ? VPTMCM_ALLREDUCE_INLINE : 0u) | (shd ? VPTMCM_ALLREDUCE_SHARDED : 0u)));
 }
 
 /* commReadComposite(h, Float32Array(R*R*3), R) */

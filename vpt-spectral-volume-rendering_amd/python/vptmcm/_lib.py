@@ -19,6 +19,7 @@ VARIANT_DIR = PKG.parent / "build" / "variants"
 
 OK, EINVAL, EHIP, ESTATE, ENOMEM, ECOMM = 0, -1, -2, -3, -4, -5
 ALLREDUCE_INLINE = 1  # VPTMCM_ALLREDUCE_INLINE
+ALLREDUCE_SHARDED = 2  # VPTMCM_ALLREDUCE_SHARDED
 LAYOUT_LINEAR, LAYOUT_CORNER8, LAYOUT_BRICK8, LAYOUT_COLUMN4 = 0, 1, 2, 3
 RENDERER_SPECTRAL, RENDERER_RGB = 0, 1
 PHOTON_RGB_BYTES = 64
@@ -401,11 +402,14 @@ class Renderer:
         u = (C.c_uint8 * 128).from_buffer_copy(uid)
         self._ck(self.L.vptmcm_comm_init(self.h, u, nranks, rank))
 
-    def allreduce_radiance(self, inline: bool = False) -> None:
+    def allreduce_radiance(self, inline: bool = False, sharded: bool = False) -> None:
         """The cross-rank composite; inline=True runs it on the march stream
-        (VPTMCM_ALLREDUCE_INLINE: soonest ready, the next march waits)."""
-        if inline:
-            self._ck(self.L.vptmcm_comm_allreduce_radiance_ex(self.h, ALLREDUCE_INLINE))
+        (VPTMCM_ALLREDUCE_INLINE: soonest ready, the next march waits);
+        sharded=True reduce-scatters instead (VPTMCM_ALLREDUCE_SHARDED: the
+        next read_composite is collective, every rank calls it)."""
+        flags = (ALLREDUCE_INLINE if inline else 0) | (ALLREDUCE_SHARDED if sharded else 0)
+        if flags:
+            self._ck(self.L.vptmcm_comm_allreduce_radiance_ex(self.h, flags))
         else:
             self._ck(self.L.vptmcm_comm_allreduce_radiance(self.h))
 
