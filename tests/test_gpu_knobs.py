@@ -117,7 +117,9 @@ def test_auto_bound_follows_the_measurement(monkeypatch):
     the macro-cell alpha bound outside timed regions and keeps the faster: at
     the near camera on C3's 512^3 volume the bound saves ~26 % of a pass
     (profiles/r06/s18), far beyond the pairs' spread, so after a dozen
-    32-pass launches read back by synchronize the march runs with it."""
+    32-pass launches read back by synchronize the march runs with it. A camera
+    that then moves every launch (an interactive rotation) never completes a
+    pair of launches, so the decision stands."""
     for var in ("VPTMCM_MAJ", "VPTMCM_MARCH_VARIANT"):
         monkeypatch.delenv(var, raising=False)
     vol = cf.fbm_volume(512, 512, nthreads=8)
@@ -134,5 +136,12 @@ def test_auto_bound_follows_the_measurement(monkeypatch):
         gpu.render_passes(mn, seeds[1 + 32 * j: 1 + 32 * (j + 1)])
         gpu.synchronize()
     info = gpu.last_launch()
-    gpu.close()
     assert info["macro"] and info["passes"] == 32, info
+    rseeds = cf.seed_stream(8 * 32, start=900)
+    for j in range(8):  # a new matrix every launch
+        m = mn.copy()
+        m[12] += np.float32(1e-4 * (j + 1))
+        gpu.render_passes(m, rseeds[32 * j: 32 * (j + 1)])
+        gpu.synchronize()
+        assert gpu.last_launch()["macro"], j
+    gpu.close()

@@ -297,9 +297,12 @@ struct vptmcm {
     // saves 1.6 %).
     float ratio[kMaxFusedPasses + 1];
     float half[kMaxFusedPasses + 1];         // a pair's ratio awaiting the other order (-1: none)
-    // pairs of pairs folded into ratio[n]: it decides from kQuads on (until
-    // then every launch of size n outside a timed region is a probe)
+    // pairs of pairs folded into ratio[n] since the last reset or camera
+    // change: it decides from kQuads on (until then every launch of size n
+    // outside a timed region is a probe, and a ratio from the previous camera,
+    // if any, still picks)
     uint8_t quads[kMaxFusedPasses + 1];
+    uint32_t cam_launches = 0;    // launches since the camera last changed (pairs start only from 1 on)
     uint32_t launches[kMaxFusedPasses + 1];  // launches of size n since its last pair
     uint8_t first[kMaxFusedPasses + 1];      // the first choice of size n's next pair
     uint8_t half_first[kMaxFusedPasses + 1]; // the first choice of the pair held in half
@@ -825,6 +828,18 @@ void maj_tune_reset(vptmcm* h) {
   h->maj_tune.epoch++;
 }
 
+// A new camera: measure again, but keep each size's ratio as the pick until
+// the new one decides (a camera that moves every launch — an interactive
+// rotation — never gets a pair, and keeps the last decision).
+void maj_tune_camera(vptmcm* h) {
+  for (uint32_t n = 0; n <= kMaxFusedPasses; n++) {
+    h->maj_tune.half[n] = -1.0f;
+    h->maj_tune.quads[n] = 0;
+  }
+  h->maj_tune.cam_launches = 0;
+  h->maj_tune.epoch++;
+}
+
 // Re-lay out the cells of the blocks that arrived since the last relayout
 // (vptmcm::vol_dirty) from the staging copy, on the handle's stream.
 int flush_relayout(vptmcm* h) {
@@ -909,7 +924,7 @@ void maj_tune_harvest(vptmcm* h) {
     const float rr = sqrtf(t.half[n] * r);
     t.half[n] = -1.0f;
     float& q = t.ratio[n];
-    q = q < 0.0f ? rr : 0.5f * q + 0.5f * rr;
+    q = (q < 0.0f || t.quads[n] == 0) ? rr : 0.5f * q + 0.5f * rr;  // (a previous camera's ratio is replaced)
     if (t.quads[n] < 255) t.quads[n]++;
     if (t.quads[n] >= vptmcm::kQuads) t.choice = q < 1.0f ? 1 : 0;
     if (const char* v = getenv("VPTMCM_MAJ_TRACE"))
@@ -930,10 +945,12 @@ int maj_tune_pick(vptmcm* h, const float* mvp, uint32_t n, hipEvent_t* pb, hipEv
   if (!h->timing) maj_tune_harvest(h);  // (no event queries inside the caller's timed regions)
   if (memcmp(t.mvp, mvp, sizeof t.mvp) != 0) {  // the volume's screen coverage moved
     memcpy(t.mvp, mvp, sizeof t.mvp);
-    maj_tune_reset(h);
+    maj_tune_camera(h);
+  } else if (t.cam_launches < 0xffffffffu) {
+    t.cam_launches++;
   }
   const bool decided = t.quads[n] >= vptmcm::kQuads;
-  const int pick = !decided ? t.choice : t.ratio[n] < 1.0f ? 1 : 0;
+  const int pick = t.ratio[n] < 0.0f ? t.choice : t.ratio[n] < 1.0f ? 1 : 0;
   auto* open = t.count > 0 ? &t.pairs[(t.head + t.count - 1) % vptmcm::kPairs] : nullptr;
   if (open && open->stage != 1) open = nullptr;
   if (open && (h->timing || open->n != n || open->epoch != t.epoch)) {
@@ -947,7 +964,9 @@ int maj_tune_pick(vptmcm* h, const float* mvp, uint32_t n, hipEvent_t* pb, hipEv
     *pe = open->e[1];
     return open->first ^ 1;
   }
-  if (t.count == vptmcm::kPairs || !(!decided || ++t.launches[n] >= 16)) return pick;
+  // a pair starts once the camera held for a launch (its second launch is then
+  // likely to share it), at once while undecided, else every 16 launches
+  if (t.count == vptmcm::kPairs || t.cam_launches == 0 || !(!decided || ++t.launches[n] >= 16)) return pick;
   auto& pr = t.pairs[(t.head + t.count) % vptmcm::kPairs];
   for (int k = 0; k < 2; k++)
     if ((!pr.b[k] && hipEventCreate(&pr.b[k]) != hipSuccess) || (!pr.e[k] && hipEventCreate(&pr.e[k]) != hipSuccess)) {
