@@ -271,7 +271,7 @@ struct vptmcm {
   MarchLaunchInfo last_launch{};
   // Whether the march skips certain null collisions' gathers (MarchParams::
   // maj_on; same results either way) is measured, not guessed: it pays where
-  // the march waits on volume line fills (a volume filling the frame, +31 %
+  // the march waits on volume line fills (a volume filling the frame, +35 %
   // per pass at 512^3; 1024^3, +5 %) and costs where it does not (the
   // default camera, -6 %; a cache-resident 256^3 volume). VPTMCM_MAJ=auto
   // (default): launches outside timed regions are timed now and then with
@@ -306,8 +306,8 @@ struct vptmcm {
     uint32_t launches[kMaxFusedPasses + 1];  // launches of size n since its last pair
     uint8_t first[kMaxFusedPasses + 1];      // the first choice of size n's next pair
     uint8_t half_first[kMaxFusedPasses + 1]; // the first choice of the pair held in half
-    float mvp[16] = {};           // the camera the ratio holds (another one: start over)
-    uint32_t epoch = 0;           // bumped by a reset: pairs of an older epoch are dropped
+    float mvp[16] = {};           // the camera of the launches measured (another one: measure again)
+    uint32_t epoch = 0;           // bumped by a reset or a new camera: pairs of an older epoch are dropped
     struct Pair {
       hipEvent_t b[2] = {nullptr, nullptr}, e[2] = {nullptr, nullptr};
       int first = 0;              // the choice of the pair's first launch (the second: the other)
