@@ -60,6 +60,10 @@ def parse():
                     help="untimed clock-settling passes before the warm-up (wall ms)")
     ap.add_argument("--resolution", type=int, default=512)
     ap.add_argument("--volume", type=int, default=512)
+    ap.add_argument("--volume-kind", choices=["fbm", "two_spheres"], default="fbm",
+                    help="fbm: the benchmark's fBm cloud (fills the cube); two_spheres: the "
+                         "reference's test volume (generate_test_volume.ipynb) at that size, two "
+                         "spheres in empty space (analysis only: empty-space traversal)")
     ap.add_argument("--photon-steps", type=int, default=8, help="S: steps per pass")
     ap.add_argument("--extinction", type=float, default=32.0)
     ap.add_argument("--layout", choices=["corner8", "brick8", "column4", "linear"], default="column4")
@@ -300,7 +304,8 @@ def main():
 
     # ---- inputs (synthetic)
     t = time.perf_counter()
-    vol = cf.fbm_volume(a.volume, volume_seed(a.volume))
+    vol = (cf.fbm_volume(a.volume, volume_seed(a.volume)) if a.volume_kind == "fbm"
+           else cf.two_spheres(a.volume))
     gen_s = time.perf_counter() - t
     tf = {"spectral": cf.tf_spectral, "grey": cf.tf_grey, "zero": cf.tf_zero,
           "materials": lambda: cf.tf_materials(True),
@@ -738,8 +743,10 @@ def main():
             "ms_per_step": round(el_max * 1e3 / a.steps, 5), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {
-                "workload": f"{config_name(a.volume, n_gpus)}: {a.volume}^3 fBm volume (seed "
-                            f"{volume_seed(a.volume)}), {TF_DESC.get(a.tf, a.tf + ' TF')}, R={R}, S={S}, "
+                "workload": (f"{config_name(a.volume, n_gpus)}: {a.volume}^3 fBm volume (seed "
+                             f"{volume_seed(a.volume)})" if a.volume_kind == "fbm" else
+                             f"custom: {a.volume}^3 two-spheres volume (generate_test_volume.ipynb)")
+                            + f", {TF_DESC.get(a.tf, a.tf + ' TF')}, R={R}, S={S}, "
                             f"{a.bins} bins, extinction {a.extinction}, "
                             + (f"{a.camera} camera" if a.camera_mix is None else
                                f"camera mix {a.camera_mix} (default -> near)"),

@@ -145,3 +145,45 @@ def test_auto_bound_follows_the_measurement(monkeypatch):
         gpu.synchronize()
         assert gpu.last_launch()["macro"], j
     gpu.close()
+
+
+@pytest.mark.parametrize("layout", [vptmcm.LAYOUT_COLUMN4, vptmcm.LAYOUT_CORNER8, vptmcm.LAYOUT_BRICK8])
+def test_macro_bound_empty_space_bitexact(layout, monkeypatch):
+    """The reference's two-spheres test volume (generate_test_volume.ipynb):
+    mostly empty space, whose macro cells carry alpha code 0 (every wheel from
+    2^-16 up skips the gather there), beside the spheres' cells. Spectral and
+    RGB renderers with the bound pinned on, bit-exact against their oracles."""
+    import oracle as orc
+    from test_gpu_rgb import same_words, tf_rgb
+    monkeypatch.setenv("VPTMCM_MAJ", "on")
+    vol = cf.two_spheres(48)
+    gpu, cpu = make_pair(64, vol, cf.tf_spectral(), ext=24.0, layout=layout)
+    mvp, seeds = cf.golden_mvp("orbit"), cf.seed_stream(10, start=21)
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0], nthreads=16)
+    gpu.render_passes(mvp, seeds[1:6])
+    for s in seeds[1:6]:
+        rgb, want = cpu.render(mvp, s, nthreads=16)
+    assert gpu.last_launch()["macro"]
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "two spheres, bound on")
+    assert_rgb32_equal(gpu.read_rgb(), rgb, "two spheres, bound on")
+    assert_rgba_equal(gpu.read_rgba16f(), want, "two spheres, bound on")
+    gpu.close()
+    g = vptmcm.Renderer(64, device=0, layout=layout, renderer=vptmcm.RENDERER_RGB)
+    c = orc.OracleRGB(64)
+    tf = tf_rgb("ramp")
+    g.set_transfer_function(tf)
+    g.set_environment((255, 255, 255, 255))
+    g.set_volume(vol)
+    g.set_params(extinction=24.0, anisotropy=0.6, bounces=8, steps=8)
+    c.volume, c.tf, c.env = vol, tf, np.array((255, 255, 255, 255), np.uint8)
+    c.params.update(extinction=24.0, anisotropy=0.6, bounces=8, steps=8)
+    g.reset(mvp, seeds[0])
+    c.reset(mvp, seeds[0])
+    g.render_passes(mvp, seeds[1:6])
+    for s in seeds[1:6]:
+        _, want = c.render(mvp, s)
+    assert g.last_launch()["macro"]
+    assert same_words(g.read_photons(), c.photons).all(), "rgb two spheres, bound on"
+    assert np.array_equal(g.read_rgba16f(), want)
+    g.close()

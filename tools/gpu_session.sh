@@ -146,12 +146,12 @@ for s in $STEPS; do
     echo "finalab rc=0" | tee -a $OUT/status.txt; cat $OUT/finalab.jsonl ;;
   majab)  # the macro-cell alpha bound off (VPTMCM_MARCH_VARIANT=256) / on, default and near camera, alternating
     for c in ${MAJ_CASES:-256:default 0:default 256:near 0:near 256:default 0:default 256:near 0:near}; do
-      IFS=: read v cam vol <<< "$c"
+      IFS=: read v cam vol kind <<< "$c"
       case $cam in mix*) camarg="--camera-mix ${cam#mix}";; *) camarg="--camera $cam";; esac
       case $v in auto|on|off) export VPTMCM_MAJ=$v; v=0;; *) unset VPTMCM_MAJ;; esac
-      VPTMCM_MARCH_VARIANT=$v timeout -k 10 300 python bench.py $camarg --volume ${vol:-512} --steps 256 --warmup 1024 --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 0 --unfused-steps 64 --near-steps 0 > $OUT/maj.json 2>> $OUT/majab.err
+      VPTMCM_MARCH_VARIANT=$v timeout -k 10 300 python bench.py $camarg --volume ${vol:-512} --volume-kind ${kind:-fbm} --steps 256 --warmup 1024 --cpu-seconds 0 --js-steps 0 --rgb-steps 0 --general-steps 0 --api-steps 0 --unfused-steps 64 --near-steps 0 > $OUT/maj.json 2>> $OUT/majab.err
       rc=$?; [ $rc -ne 0 ] && { echo "majab rc=$rc" | tee -a $OUT/status.txt; exit $rc; }
-      python3 -c "import json; d=json.load(open('$OUT/maj.json')); print(json.dumps({'variant': $v, 'maj': '${VPTMCM_MAJ:-auto}', 'camera': '$cam', 'volume': ${vol:-512}, 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'unfused_us': d['unfused']['kernel_avg_us']}))" >> $OUT/majab.jsonl
+      python3 -c "import json; d=json.load(open('$OUT/maj.json')); print(json.dumps({'variant': $v, 'maj': '${VPTMCM_MAJ:-auto}', 'camera': '$cam', 'volume': ${vol:-512}, 'kind': '${kind:-fbm}', 'value': d['value'], 'us_per_pass': d['roofline']['kernel_us_per_pass'], 'unfused_us': d['unfused']['kernel_avg_us']}))" >> $OUT/majab.jsonl
     done
     echo "majab rc=0" | tee -a $OUT/status.txt; cat $OUT/majab.jsonl ;;
   rgbab)  # the RGB sibling's line with the macro-cell bound on / off / auto, "maj:camera" cases

@@ -80,9 +80,12 @@ def sphere_in_cube(n: int = 64) -> np.ndarray:
 
 
 def two_spheres(n: int = 64) -> np.ndarray:
-    """generate_test_volume.ipynb cell 3 at size n."""
+    """generate_test_volume.ipynb cell 3 at size n. np.meshgrid's 'xy' axes
+    (X along axis 1, Y along axis 0, Z along axis 2) by broadcasting: the same
+    float64 values element for element, without three n^3 coordinate arrays."""
     V = np.zeros((n, n, n), dtype=np.uint8)
-    X, Y, Z = np.meshgrid(np.linspace(-1, 1, n), np.linspace(-1, 1, n), np.linspace(-1, 1, n))
+    t = np.linspace(-1, 1, n)
+    X, Y, Z = t[None, :, None], t[:, None, None], t[None, None, :]
     V[X ** 2 + Y ** 2 + (Z - 0.5) ** 2 < 0.4 ** 2] += 200
     V[X ** 2 + Y ** 2 + (Z + 0.5) ** 2 < 0.4 ** 2] += 100
     return V
