@@ -591,11 +591,26 @@ def main():
         nmacro = bool(r.last_launch().get("macro", False))
         nbytes = sum(cf.algorithmic_bytes_per_launch(R, S, n) for n in nl)
         nshapes = sorted(set(nl))
+        # the same region with the macro-cell bound switched off (what the march
+        # costs here without it; the line above keeps the library's choice)
+        nk_off = None
+        if not a.no_timing and nmacro:
+            r.set_macro_skip("off")
+            r.render_passes(mn, nseeds[1:33])  # one launch at the new setting, untimed
+            r.synchronize()
+            r.enable_kernel_timing(True)
+            passes_on(nseeds, 321, a.near_steps, m=mn)
+            r.synchronize()
+            nk_off, _ = r.kernel_time()
+            r.enable_kernel_timing(False)
+            r.set_macro_skip(os.environ.get("VPTMCM_MAJ", "auto") if os.environ.get("VPTMCM_MAJ") in
+                             ("on", "off", "auto") else "auto")
         near = {"value": round(R * R * S * a.near_steps / el6 / 1e6, 3),
                 "ms_per_step": round(el6 * 1e3 / a.near_steps, 5), "steps": a.near_steps,
                 "passes_per_launch": nshapes[0] if len(nshapes) == 1 else nshapes,
                 "kernel_us_per_pass": None, "roofline": None, "gather_roofline": None,
                 "macro_skip": nmacro,
+                "kernel_us_per_pass_bound_off": (round(nk_off * 1e3 / a.near_steps, 3) if nk_off else None),
                 "workload": "same volume, TF, bins and launch shape as the main line with the golden "
                             "'near' camera: the volume fills the frame, every photon-step gathers"}
         if not a.no_timing:

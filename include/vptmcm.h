@@ -276,6 +276,13 @@ int vptmcm_enable_kernel_timing(vptmcm* h, int enable);
  * the same launches, and untimed launches enqueue faster. */
 int vptmcm_kernel_time(vptmcm* h, double* total_ms, uint64_t* launches);
 
+/* The macro-cell alpha bound (no reference counterpart — a
+ * measurement and tuning control like VPTMCM_MAJ, which sets the initial mode
+ * at create): 0 off, 1 on, 2 auto (measure and keep the faster). Applies to
+ * every replica of a device-list handle and restarts the auto measurements.
+ * Same results in every mode. */
+int vptmcm_set_macro_skip(vptmcm* h, int mode);
+
 /* ---- multi-GPU (photon-parallel replicas, RCCL over xGMI) ----------------- */
 
 /* ncclGetUniqueId on rank 0; the caller ships the 128 bytes to other ranks. */

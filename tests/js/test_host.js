@@ -135,7 +135,7 @@ test('addon loads; renderer construction fails loudly without a GPU', () => {
     'setMaterialTF', 'setLight', 'setSpectrum', 'setParams', 'reset', 'render', 'renderPasses',
     'synchronize', 'readRGBA16F', 'readPhotons', 'writePhotons', 'enableKernelTiming', 'kernelTime',
     'commUniqueId', 'commInit', 'commAllreduceRadiance', 'commReadComposite', 'commBarrier', 'setBand', 'commGatherBands', 'version',
-    'tonemapArtistic', 'readRGB', 'lastLaunch', 'composite', 'readComposite', 'groupDevices']) {
+    'tonemapArtistic', 'readRGB', 'lastLaunch', 'composite', 'readComposite', 'groupDevices', 'setMacroSkip']) {
     assert.strictEqual(typeof A[f], 'function', f);
   }
   assert.ok(/gfx950/.test(A.version()));

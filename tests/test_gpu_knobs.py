@@ -187,3 +187,26 @@ def test_macro_bound_empty_space_bitexact(layout, monkeypatch):
     assert same_words(g.read_photons(), c.photons).all(), "rgb two spheres, bound on"
     assert np.array_equal(g.read_rgba16f(), want)
     g.close()
+
+
+def test_set_macro_skip_modes(monkeypatch):
+    """vptmcm_set_macro_skip switches the bound per handle (the env knob only
+    sets the initial mode): off / on run k_march<..., MAJ> as asked, the bits
+    equal the oracle's either way, a bad mode is refused."""
+    monkeypatch.delenv("VPTMCM_MAJ", raising=False)
+    gpu, cpu = make_pair(64, cf.fbm_volume(48, 21, nthreads=8), cf.tf_spectral(), ext=24.0,
+                         layout=vptmcm.LAYOUT_COLUMN4)
+    mvp, seeds = cf.golden_mvp("near"), cf.seed_stream(7, start=33)
+    gpu.reset(mvp, seeds[0])
+    cpu.reset(mvp, seeds[0], nthreads=16)
+    for k, mode in enumerate(["off", "on", "off", "on", "auto", "on"]):
+        gpu.set_macro_skip(mode)
+        gpu.render_passes(mvp, seeds[1 + k:2 + k])
+        rgb, want = cpu.render(mvp, seeds[1 + k], nthreads=16)
+        if mode != "auto":
+            assert gpu.last_launch()["macro"] == (mode == "on"), mode
+    assert_photons_equal(gpu.read_photons(), cpu.photons, "set_macro_skip")
+    assert_rgba_equal(gpu.read_rgba16f(), want, "set_macro_skip")
+    with pytest.raises(vptmcm.VptError, match="set_macro_skip"):
+        gpu._ck(gpu.L.vptmcm_set_macro_skip(gpu.h, 3))
+    gpu.close()

@@ -3037,6 +3037,17 @@ int vptmcm_enable_kernel_timing(vptmcm* h, int enable) {
   return enable_kernel_timing_one(h, enable);  // replica 0 only (see vptmcm_kernel_time)
 }
 
+int vptmcm_set_macro_skip(vptmcm* h, int mode) {
+  if (check_handle(h)) return VPTMCM_EINVAL;
+  if (mode < 0 || mode > 2) FAIL(h, VPTMCM_EINVAL, "set_macro_skip: mode %d (0 off, 1 on, 2 auto)", mode);
+  if (int rc = flush_renders(h)) return rc;  // queued passes keep the mode they were queued under
+  return for_replicas(h, [&](vptmcm* c) {
+    c->maj_tune.mode = mode;
+    maj_tune_reset(c);
+    return VPTMCM_OK;
+  });
+}
+
 int vptmcm_composite(vptmcm* h) {
   if (check_handle(h)) return VPTMCM_EINVAL;
   if (!composited(h)) return VPTMCM_OK;

@@ -428,6 +428,20 @@ static napi_value js_enable_kernel_timing(napi_env env, napi_callback_info info)
     return check(env, h, vptmcm_enable_kernel_timing(h, on ? 1 : 0));
 }
 
+/* setMacroSkip(h, mode): 0 off, 1 on, 2 auto (vptmcm_set_macro_skip) */
+static napi_value js_set_macro_skip(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (get_args(env, info, 2, argv)) return NULL;
+    vptmcm* h = get_handle(env, argv[0]);
+    if (!h) return NULL;
+    int32_t mode = 0;
+    if (napi_get_value_int32(env, argv[1], &mode) != napi_ok) {
+        napi_throw_type_error(env, NULL, "mode must be 0, 1 or 2");
+        return NULL;
+    }
+    return check(env, h, vptmcm_set_macro_skip(h, mode));
+}
+
 /* kernelTime(h) -> { ms, launches } */
 static napi_value js_kernel_time(napi_env env, napi_callback_info info) {
     napi_value argv[1];
@@ -653,6 +667,7 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("setBand", js_set_band);
     EXPORT("commGatherBands", js_comm_gather_bands);
     EXPORT("lastLaunch", js_last_launch);
+    EXPORT("setMacroSkip", js_set_macro_skip);
     EXPORT("composite", js_composite);
     EXPORT("readComposite", js_read_composite);
     EXPORT("groupDevices", js_group_devices);

@@ -40,7 +40,7 @@ EXPORTS = [
     "vptmcm_comm_read_composite",
     "vptmcm_comm_barrier", "vptmcm_comm_allreduce_host", "vptmcm_debug_eval",
     "vptmcm_debug_verify", "vptmcm_debug_last_launch", "vptmcm_debug_schedule", "vptmcm_version",
-    "vptmcm_read_composite", "vptmcm_composite", "vptmcm_group_devices",
+    "vptmcm_read_composite", "vptmcm_composite", "vptmcm_group_devices", "vptmcm_set_macro_skip",
 ]
 MAX_DEVICES = 8
 GROUP_PEER, GROUP_RCCL = 0, 1
@@ -118,6 +118,7 @@ def load() -> C.CDLL:
         "vptmcm_read_photons": (C.c_int, [vp, vp]),
         "vptmcm_write_photons": (C.c_int, [vp, vp]),
         "vptmcm_enable_kernel_timing": (C.c_int, [vp, C.c_int]),
+        "vptmcm_set_macro_skip": (C.c_int, [vp, C.c_int]),
         "vptmcm_kernel_time": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
         "vptmcm_comm_unique_id": (C.c_int, [u8p]),
         "vptmcm_comm_init": (C.c_int, [vp, u8p, C.c_int, C.c_int]),
@@ -391,6 +392,10 @@ class Renderer:
     # -- measurement
     def enable_kernel_timing(self, on: bool = True) -> None:
         self._ck(self.L.vptmcm_enable_kernel_timing(self.h, 1 if on else 0))
+
+    def set_macro_skip(self, mode: str) -> None:
+        """The macro-cell alpha bound: "off", "on" or "auto" (vptmcm_set_macro_skip)."""
+        self._ck(self.L.vptmcm_set_macro_skip(self.h, {"off": 0, "on": 1, "auto": 2}[mode]))
 
     def kernel_time(self):
         ms, n = C.c_double(), C.c_uint64()
