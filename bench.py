@@ -14,7 +14,7 @@ Launch: `python bench.py --gpus N --steps K --warmup W`, or under
 one process per GPU (LOCAL_RANK), RCCL bootstrapped torch-free (rendezvous.py).
 Without a launcher (no WORLD_SIZE) and N > 1, one process drives the N GPUs
 through one device-list handle (the north_star's one-process JS host shape:
-replica k on device k, composited on device 0); it fails if fewer than N
+replica k on device k, each compositing its 1/N pixel shard); it fails if fewer than N
 devices are visible. Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -741,13 +741,16 @@ def main():
 
     n_gpus = world * group
     if multi:
-        parallelism = (f"photon-parallel replicas x{world}, one process per GPU, RCCL all-reduce of "
-                       f"(rgb*n, n) every {every} pass(es)")
+        parallelism = (f"photon-parallel replicas x{world}, one process per GPU, RCCL "
+                       + ("reduce-scatter (summed frame kept sharded over the ranks)"
+                          if a.shard_composite == "on" else "all-reduce")
+                       + f" of (rgb*n, n) every {every} pass(es)")
         comp_kind = "rccl-reduce-scatter" if a.shard_composite == "on" else "rccl-allreduce"
     elif grouped:
         parallelism = (f"photon-parallel replicas x{group} in one process (device-list handle over "
-                       f"devices {devs}), composite of (rgb*n, n) on device {devs[0]} every {every} "
-                       f"pass(es)")
+                       f"devices {devs}), composite of (rgb*n, n) every {every} pass(es)"
+                       + (", each device compositing its 1/N pixel shard over xGMI peer reads"
+                          if a.transport == "peer" else f", reduced to device {devs[0]}"))
         comp_kind = {"peer": "peer-sharded", "rccl": "rccl-reduce"}[a.transport]
     else:
         parallelism, comp_kind = "single GPU", None
